@@ -1,0 +1,177 @@
+/*
+ * voxtral_hip.h -- C ABI of the MI355X (gfx950 / CDNA4) backend for voxtral.c.
+ *
+ * This header is the drop-in boundary.  It replaces the reference's Metal backend
+ * interface (voxtral_metal.h, SeungheonOh/voxtral.c @ 2026-02-20); every entry point
+ * below cites the reference declaration it replaces.  Signatures use plain pointers and
+ * sizes only.  All functions are synchronous with respect to host pointers they are
+ * given, like the Metal backend (voxtral_metal.m waits on every command buffer).
+ *
+ * Differences from voxtral_metal.h that the discrete-GPU design forces (see
+ * INTEGRATION.md for the call-site patch):
+ *   - the Metal backend read weights and KV state out of the reference's vox_ctx_t via
+ *     `void *ctx` (voxtral_metal.m:2888-3174).  Here weights are handed over once as a
+ *     table of host pointers (vox_hip_weights_t, filled from vox_ctx_t at vox_load) and
+ *     per-stream device state lives in an opaque vox_hip_stream_t;
+ *   - the decoder/encoder KV caches live in HBM as rolling buffers indexed by LOGICAL
+ *     position (slot = pos mod capacity), so the host-side memmove compaction of
+ *     voxtral_decoder.c:354-384 / voxtral_encoder.c:431-449 becomes unnecessary.  The
+ *     step functions therefore take the logical start position instead of the physical
+ *     cache length.  Attention semantics are unchanged: the last `window` logical
+ *     positions are visible (identical to the CPU path after compaction).
+ *
+ * Errors: functions returning int return a negative value on failure (the reference's
+ * step functions return -1 to request the CPU fallback; this backend never falls back
+ * silently -- a failure is reported and the caller decides).
+ */
+#ifndef VOXTRAL_HIP_H
+#define VOXTRAL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------
+ * Runtime (voxtral_metal.h:20-26)
+ * ------------------------------------------------------------------------ */
+int vox_hip_init(void);          /* voxtral_metal.h:20  vox_metal_init: 1 on success */
+int vox_hip_available(void);     /* voxtral_metal.h:23  vox_metal_available */
+void vox_hip_shutdown(void);     /* voxtral_metal.h:26  vox_metal_shutdown */
+size_t vox_hip_memory_used(void);/* voxtral_metal.h:282 vox_metal_memory_used */
+const char *vox_hip_last_error(void);
+int vox_hip_set_device(int device);
+
+/* ------------------------------------------------------------------------
+ * Model dimensions (voxtral.h:18-50 are compile-time #defines in the reference;
+ * here they are a runtime record so test configurations can shrink the model).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    int enc_dim, enc_layers, enc_heads, enc_kv_heads, enc_head_dim, enc_hidden, enc_window;
+    int dec_dim, dec_layers, dec_heads, dec_kv_heads, dec_head_dim, dec_hidden, dec_window;
+    int vocab, mel_bins, downsample, ada_dim;
+    float rope_theta, enc_eps, dec_eps;
+    int gelu_erf; /* 0: tanh GELU (voxtral_kernels.c:505-513), the default */
+} vox_hip_config_t;
+
+void vox_hip_config_voxtral_4b(vox_hip_config_t *cfg); /* voxtral.h:26-50 values */
+
+/* Weight table: host pointers, exactly the views vox_ctx_t holds after vox_load
+ * (voxtral.h:56-239): bf16 matrices straight off the safetensors mmap, small tensors
+ * already converted to f32.  Per-layer tensors are arrays of `layers` pointers. */
+typedef struct {
+    const float *conv0_w, *conv0_b, *conv1_w, *conv1_b;
+    const uint16_t **enc_wq, **enc_wk, **enc_wv, **enc_wo, **enc_w1, **enc_w2, **enc_w3;
+    const float **enc_wq_b, **enc_wv_b, **enc_wo_b, **enc_w2_b, **enc_attn_norm, **enc_ffn_norm;
+    const float *enc_norm;
+    const uint16_t *ad0, *ad1;
+    const uint16_t *tok_emb;
+    const uint16_t **dec_wq, **dec_wk, **dec_wv, **dec_wo, **dec_w1, **dec_w2, **dec_w3;
+    const float **dec_attn_norm, **dec_ffn_norm, **dec_ada_down, **dec_ada_up;
+    const float *dec_norm;
+} vox_hip_weights_t;
+
+typedef struct vox_hip_model vox_hip_model_t;
+typedef struct vox_hip_stream vox_hip_stream_t;
+
+/* Upload + pack all weights into HBM once (replaces the Metal warm-up and weight
+ * caches, voxtral.c:186-284 / voxtral_metal.m:133-501: QKV and W1|W3 are merged here).
+ * delay_tokens sets the time conditioning (voxtral.c:47-80). */
+vox_hip_model_t *vox_hip_model_create(const vox_hip_config_t *cfg, const vox_hip_weights_t *w,
+                                      int delay_tokens);
+void vox_hip_model_free(vox_hip_model_t *m);
+/* vox_set_delay (voxtral.c:1681-1687): recompute ada_scale and re-upload it (the Metal
+ * backend's pointer-keyed f32 cache went stale here, voxtral_metal.m:471-501). */
+int vox_hip_model_set_delay(vox_hip_model_t *m, int delay_tokens);
+/* ada_scale [dec_layers*dec_dim] as computed on the host (for tests). */
+int vox_hip_model_ada_scale(vox_hip_model_t *m, float *out);
+
+/* Per-stream device state: encoder/decoder rolling KV, conv-stem tails, adapter buffer,
+ * scratch and a HIP stream.  One model serves many streams. */
+vox_hip_stream_t *vox_hip_stream_create(vox_hip_model_t *m);
+void vox_hip_stream_free(vox_hip_stream_t *s);
+/* stream_reset_full_state (voxtral.c:786-814) / stream_reset_decoder_state (:766-783) */
+int vox_hip_stream_reset(vox_hip_stream_t *s);
+int vox_hip_stream_reset_decoder(vox_hip_stream_t *s);
+
+/* ------------------------------------------------------------------------
+ * Device-resident streaming pipeline (the fast path).  Inputs are log-mel frames
+ * [n, mel_bins] as produced by vox_mel_feed/vox_mel_finish (voxtral_audio.c:560-633).
+ * ------------------------------------------------------------------------ */
+/* stream_run_encoder body (voxtral.c:845-951): incremental conv stem (voxtral.c:581-759),
+ * 32-layer encoder with rolling KV (voxtral_encoder.c:495-693), 4x downsample with the
+ * leftover-row residual, adapter (voxtral_encoder.c:699-737); adapter rows stay in HBM.
+ * mel is a host pointer (mel_on_device=0) or a device pointer (1).
+ * Returns the number of adapter tokens appended, <0 on error. */
+int vox_hip_stream_encode_mel(vox_hip_stream_t *s, const float *mel, int n_frames,
+                              int mel_on_device);
+int vox_hip_stream_adapter_tokens(vox_hip_stream_t *s);
+/* Copy adapter rows [first, first+n) to host (tests). */
+int vox_hip_stream_read_adapter(vox_hip_stream_t *s, int first, int n, float *out);
+
+/* stream_run_decoder (voxtral.c:1013-1145), non-continuous part: prefill when enough
+ * adapter tokens exist (prompt BOS + STREAMING_PAD x (32+delay)), then greedy steps
+ * while adapter tokens remain.  Generates at most max_steps tokens; stop_at_eos stops
+ * after token 2 (EOS).  tokens_out receives the ids; logits_out (may be NULL) receives
+ * [n, vocab] logits.  Returns the number of tokens generated (<0 on error). */
+int vox_hip_stream_decode(vox_hip_stream_t *s, int max_steps, int stop_at_eos,
+                          int *tokens_out, float *logits_out);
+/* Decoder state snapshot: [0]=kv logical length, [1]=next adapter row, [2]=prev token,
+ * [3]=started, [4]=eos_seen, [5]=tokens generated. */
+int vox_hip_stream_state(vox_hip_stream_t *s, int *out6);
+
+/* ------------------------------------------------------------------------
+ * Reference-boundary twins (host pointers in and out, synchronous).  These are what
+ * voxtral_encoder.c / voxtral_decoder.c / voxtral_kernels.c call under USE_HIP in
+ * place of the vox_metal_* functions.
+ * ------------------------------------------------------------------------ */
+/* voxtral_metal.h:38  C[M,N] = A[M,K] @ B[N,K]^T (B is a host bf16 weight pointer,
+ * uploaded once and cached by pointer like voxtral_metal.m:165-201) */
+void vox_hip_sgemm_bf16(int M, int N, int K, const float *A, const uint16_t *B_bf16, float *C);
+/* voxtral_metal.h:59 */
+void vox_hip_fused_qkv_bf16(int M, int K, const float *input,
+                            const uint16_t *wq_bf16, int Nq, const uint16_t *wk_bf16, int Nk,
+                            const uint16_t *wv_bf16, int Nv, float *q, float *k, float *v);
+/* voxtral_metal.h:86 */
+void vox_hip_fused_ffn_bf16(int M, int dim, int hidden, const float *input,
+                            const uint16_t *w1_bf16, const uint16_t *w3_bf16,
+                            const uint16_t *w2_bf16, float *output);
+/* voxtral_metal.h:136  (same semantics as vox_causal_attention, voxtral_kernels.c:541-611) */
+void vox_hip_encoder_attention(float *out, const float *Q, const float *K, const float *V,
+                               int seq_q, int seq_k, int n_heads, int n_kv_heads,
+                               int head_dim, float scale, int window_size, int q_offset);
+/* voxtral_metal.h:245  32 encoder layers + final norm in place on host x [new_len, enc_dim];
+ * K/V appended to the stream's rolling cache at logical positions
+ * logical_start..logical_start+new_len-1.  rope_freqs [new_len, head_dim/2, 2] from the
+ * caller (vox_compute_rope_freqs).  Returns 0 / <0. */
+int vox_hip_encoder_full_step(vox_hip_stream_t *s, float *x, int new_len,
+                              const float *rope_freqs, int logical_start);
+/* voxtral_metal.h:254  26 decoder layers on seq_len rows, KV written at logical
+ * positions logical_start.. ; x [seq_len, dec_dim] updated in place. */
+int vox_hip_decoder_prefill_step(vox_hip_stream_t *s, float *x, int seq_len,
+                                 const float *rope_freqs, int logical_start);
+/* voxtral_metal.h:161/164  upload the step input / release it */
+void vox_hip_decoder_start(vox_hip_stream_t *s, const float *x, int dim);
+void vox_hip_decoder_end(vox_hip_stream_t *s);
+/* voxtral_metal.h:219  one token through all layers + final norm + LM head + argmax.
+ * KV written at logical position logical_pos; returns the argmax id (first max wins,
+ * voxtral_decoder.c:771-779) and fills logits [vocab] if non-NULL. */
+int vox_hip_decoder_full_step(vox_hip_stream_t *s, const float *rope_freqs, int logical_pos,
+                              float *logits);
+
+/* ------------------------------------------------------------------------
+ * Timing hooks for the benchmark (HIP events on the stream's own queue).
+ * ------------------------------------------------------------------------ */
+/* Average device time (ms) of the last decode call's dominant per-layer GEMV launches and
+ * the bytes they streamed; filled only when profiling was enabled. */
+int vox_hip_stream_set_profiling(vox_hip_stream_t *s, int enable);
+int vox_hip_stream_profile(vox_hip_stream_t *s, double *out8);
+/* Synchronise the stream's HIP queue. */
+int vox_hip_stream_sync(vox_hip_stream_t *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VOXTRAL_HIP_H */

@@ -1,0 +1,103 @@
+"""End-to-end parity of the HIP path against the CPU oracle on the TINY configuration
+(same structure and head dims as Voxtral-4B, short windows so the rolling KV wraps).
+
+Tolerances: greedy ids must be identical; logits within 1e-3 relative to the largest
+logit magnitude (f32 arithmetic with a different summation order; the MFMA GEMMs use the
+exact 3-term bf16 split of the activations)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = 1e-3
+ADAPTER_TOL = 1e-3
+
+
+def rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1e-6, float(np.max(np.abs(b)))))
+
+
+@pytest.fixture(scope="module")
+def models(tiny_cfg, tiny_weights):
+    import vox_hip
+    import vox_oracle
+    hm = vox_hip.Model(tiny_cfg, tiny_weights)
+    om = vox_oracle.OracleModel(tiny_cfg, tiny_weights)
+    yield hm, om
+    hm.close()
+    om.close()
+
+
+def test_ada_scale_matches(models):
+    hm, om = models
+    np.testing.assert_array_equal(hm.ada_scale(), om.ada_scale())
+
+
+def test_encode_chunks_match(models, tiny_cfg):
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    rng = np.random.default_rng(3)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    # ragged chunk sizes incl. 1-frame and odd chunks (conv stride residual paths)
+    for n in [313, 1, 2, 7, 50, 1, 1, 200, 3]:
+        mel = rng.uniform(-0.6, 1.4, size=(n, tiny_cfg.mel_bins)).astype(np.float32)
+        a = hs.encode_mel(mel)
+        b = os_.encode_mel(mel)
+        assert a == b, (n, a, b)
+    ha, oa = hs.read_adapter(), os_.read_adapter()
+    assert ha.shape == oa.shape
+    assert rel(ha, oa) < ADAPTER_TOL, rel(ha, oa)
+    hs.close()
+    os_.close()
+
+
+def test_jfk_transcribe_tokens_match(models, jfk_samples):
+    """vox_transcribe_audio schedule on jfk.wav (1355 / 140 / 1 mel-frame chunks)."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    events = vox_oracle.transcribe_mel_schedule(jfk_samples)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    hsess, osess = vox_hip.Session(hs), vox_oracle.OracleSession(os_)
+    for kind, mel in events:
+        getattr(hsess, kind)(mel, stop_at_eos=False)
+        getattr(osess, kind)(mel, stop_at_eos=False)
+    assert hsess.chunks == osess.chunks == [1355, 140, 1]
+    assert len(osess.tokens) == 149
+    assert hsess.tokens == osess.tokens
+    hs.close()
+    os_.close()
+
+
+def test_streaming_interval_and_logits(models, jfk_samples):
+    """`-I 0.5` style feeding (1 s feeds, 50-frame encoder chunks), logits per step."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    events = vox_oracle.transcribe_mel_schedule(jfk_samples[:80000], feed_size=16000)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    hsess, osess = vox_hip.Session(hs, 0.5), vox_oracle.OracleSession(os_, 0.5)
+    hl, ol = [], []
+    for kind, mel in events:
+        hsess._run_encoder(mel, 1 if kind == "flush" else hsess.min_new_mel) if kind != "finish" else None
+        if kind == "finish":
+            hsess.finished = True
+            hsess._run_encoder(mel, hsess.min_new_mel)
+        t, l = hs.decode(stop_at_eos=False, want_logits=True)
+        hl.append(l)
+        hsess.tokens += t.tolist()
+        getattr(osess, "_enc")(mel, 1 if kind == "flush" else osess.min_new) if kind != "finish" else None
+        if kind == "finish":
+            osess.finished = True
+            osess._enc(mel, osess.min_new)
+        t, l = os_.decode(stop_at_eos=False, want_logits=True)
+        ol.append(l)
+        osess.tokens += t.tolist()
+    assert hsess.chunks == osess.chunks
+    assert hsess.tokens == osess.tokens
+    hl, ol = np.concatenate(hl), np.concatenate(ol)
+    assert hl.shape == ol.shape and hl.shape[0] > 0
+    assert rel(hl, ol) < LOGIT_TOL, rel(hl, ol)
+    hs.close()
+    os_.close()

@@ -1,0 +1,1091 @@
+// vox_hip.hip -- host side of the MI355X backend: implements include/voxtral_hip.h.
+//
+// Replaces voxtral_metal.m (SeungheonOh/voxtral.c) for the hot path.  Model weights are
+// uploaded once into HBM and packed (Q|K|V merged, W1|W3 interleaved); each stream owns
+// its rolling KV caches, conv-stem tails and adapter buffer in HBM; the decoder step is
+// one hipGraph replay whose kernels read the step position from device memory, so a run
+// of greedy steps never returns to the host (DESIGN.md "Decoder step").
+#include "../../include/voxtral_hip.h"
+#include "vox_hip_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace vox;
+
+#define TOKEN_BOS 1
+#define TOKEN_EOS 2
+#define TOKEN_STREAMING_PAD 32
+
+static thread_local std::string g_err;
+static int g_inited = 0;
+static size_t g_mem_used = 0;
+
+static int set_err(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    fprintf(stderr, "voxtral_hip: %s\n", buf);
+    return -1;
+}
+
+#define CK(expr)                                                                          \
+    do {                                                                                  \
+        hipError_t e__ = (expr);                                                          \
+        if (e__ != hipSuccess)                                                            \
+            return set_err("%s failed at %s:%d: %s", #expr, __FILE__, __LINE__, hipGetErrorString(e__)); \
+    } while (0)
+
+template <class T>
+static hipError_t dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e == hipSuccess) {
+        g_mem_used += n * sizeof(T);
+        e = hipMemset(*p, 0, n * sizeof(T));
+    }
+    return e;
+}
+template <class T>
+static void dfree(T*& p) {
+    if (p) hipFree((void*)p);
+    p = nullptr;
+}
+
+extern "C" const char* vox_hip_last_error(void) { return g_err.c_str(); }
+
+extern "C" int vox_hip_init(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_err("no HIP device");
+        return 0;
+    }
+    g_inited = 1;
+    return 1;
+}
+extern "C" int vox_hip_available(void) { return g_inited; }
+extern "C" void vox_hip_shutdown(void) { g_inited = 0; }
+extern "C" size_t vox_hip_memory_used(void) { return g_mem_used; }
+extern "C" int vox_hip_set_device(int device) {
+    CK(hipSetDevice(device));
+    return 0;
+}
+
+extern "C" void vox_hip_config_voxtral_4b(vox_hip_config_t* c) {
+    // voxtral.h:26-50
+    c->enc_dim = 1280; c->enc_layers = 32; c->enc_heads = 32; c->enc_kv_heads = 32;
+    c->enc_head_dim = 64; c->enc_hidden = 5120; c->enc_window = 750;
+    c->dec_dim = 3072; c->dec_layers = 26; c->dec_heads = 32; c->dec_kv_heads = 8;
+    c->dec_head_dim = 128; c->dec_hidden = 9216; c->dec_window = 8192;
+    c->vocab = 131072; c->mel_bins = 128; c->downsample = 4; c->ada_dim = 32;
+    c->rope_theta = 1000000.0f; c->enc_eps = 1e-5f; c->dec_eps = 1e-5f; c->gelu_erf = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Host math that the reference runs on the CPU once per load (kept bit-identical)
+// ---------------------------------------------------------------------------
+static float host_gelu(float v, int erf_mode) {
+    if (erf_mode) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+    float x3 = v * v * v;
+    float inner = 0.7978845608028654f * (v + 0.044715f * x3);
+    return 0.5f * v * (1.0f + tanhf(inner));
+}
+
+// vox_compute_rope_freqs (voxtral_kernels.c:617-629) for positions [p0, p0+n)
+static void host_rope(float* out, int p0, int n, int dim, float theta) {
+    int half = dim / 2;
+    for (int s = 0; s < n; s++) {
+        float p = (float)(p0 + s);
+        for (int d = 0; d < half; d++) {
+            float freq = 1.0f / powf(theta, (float)(2 * d) / (float)dim);
+            float ang = p * freq;
+            out[(size_t)s * dim + 2 * d] = cosf(ang);
+            out[(size_t)s * dim + 2 * d + 1] = sinf(ang);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Model
+// ---------------------------------------------------------------------------
+struct EncLayerD {
+    uint16_t *wqkv, *wo, *w13, *w2;
+    float *bqkv, *bo, *b2, *attn_norm, *ffn_norm;
+};
+struct DecLayerD {
+    uint16_t *wqkv, *wo, *w13, *w2;
+    float *attn_norm, *ffn_norm;
+};
+
+struct vox_hip_model {
+    vox_hip_config_t c;
+    int delay_tokens;
+    uint16_t *conv0_w, *conv1_w;
+    float *conv0_b, *conv1_b, *enc_norm, *dec_norm;
+    std::vector<EncLayerD> enc;
+    std::vector<DecLayerD> dec;
+    uint16_t *ad0, *ad1, *tok_emb;
+    float* ada_scale;              // device [dec_layers][dec_dim]
+    std::vector<float> ada_host;   // host copy
+    std::vector<std::vector<float>> ada_down, ada_up;
+    float *rope_enc, *rope_dec;    // device tables [rope_positions][hd]
+    int rope_positions;
+};
+
+static int upload(void* dst, const void* src, size_t bytes) {
+    if (!src) return set_err("null weight pointer");
+    CK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// f32 tensor that holds bf16 values (the reference's load_f32 of a BF16 tensor) -> bf16
+static int upload_f32_as_bf16(uint16_t* dst, const float* src, size_t n) {
+    std::vector<uint16_t> tmp(n);
+    for (size_t i = 0; i < n; i++) {
+        uint32_t u;
+        memcpy(&u, &src[i], 4);
+        if (u & 0xffffu) return set_err("conv weight is not bf16-representable (element %zu)", i);
+        tmp[i] = (uint16_t)(u >> 16);
+    }
+    return upload(dst, tmp.data(), n * 2);
+}
+
+// rows 32g..32g+15 <- w1 rows 16g..16g+15, rows 32g+16..32g+31 <- w3 rows 16g..
+static int upload_w13(uint16_t* dst, const uint16_t* w1, const uint16_t* w3, int hidden, int K) {
+    if (!w1 || !w3) return set_err("null w1/w3");
+    if (hidden % 16) return set_err("hidden %d not a multiple of 16", hidden);
+    size_t grp = (size_t)16 * K * 2;
+    CK(hipMemcpy2D(dst, 2 * grp, w1, grp, grp, hidden / 16, hipMemcpyHostToDevice));
+    CK(hipMemcpy2D((char*)dst + grp, 2 * grp, w3, grp, grp, hidden / 16, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int model_update_ada(vox_hip_model_t* m) {
+    // vox_update_time_conditioning (voxtral.c:31-80)
+    const vox_hip_config_t& c = m->c;
+    int D = c.dec_dim, A = c.ada_dim;
+    std::vector<float> t_cond(D), hidden(A);
+    int half = D / 2;
+    float log_theta = logf(10000.0f);
+    float t = (float)m->delay_tokens;
+    for (int i = 0; i < half; i++) {
+        float inv_freq = expf(-log_theta * (float)i / (float)half);
+        float emb = t * inv_freq;
+        t_cond[i] = cosf(emb);
+        t_cond[i + half] = sinf(emb);
+    }
+    m->ada_host.assign((size_t)c.dec_layers * D, 0.f);
+    for (int l = 0; l < c.dec_layers; l++) {
+        const float* down = m->ada_down[l].data();
+        const float* up = m->ada_up[l].data();
+        for (int i = 0; i < A; i++) {
+            float sum = 0.f;
+            for (int j = 0; j < D; j++) sum += down[(size_t)i * D + j] * t_cond[j];
+            hidden[i] = host_gelu(sum, c.gelu_erf);
+        }
+        float* sc = m->ada_host.data() + (size_t)l * D;
+        for (int i = 0; i < D; i++) {
+            float sum = 0.f;
+            for (int j = 0; j < A; j++) sum += up[(size_t)i * A + j] * hidden[j];
+            sc[i] = sum;
+        }
+    }
+    CK(hipMemcpy(m->ada_scale, m->ada_host.data(), m->ada_host.size() * 4, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int model_rope_tables(vox_hip_model_t* m, int positions) {
+    const vox_hip_config_t& c = m->c;
+    dfree(m->rope_enc);
+    dfree(m->rope_dec);
+    std::vector<float> t((size_t)positions * std::max(c.enc_head_dim, c.dec_head_dim));
+    CK(dalloc(&m->rope_enc, (size_t)positions * c.enc_head_dim));
+    host_rope(t.data(), 0, positions, c.enc_head_dim, c.rope_theta);
+    CK(hipMemcpy(m->rope_enc, t.data(), (size_t)positions * c.enc_head_dim * 4, hipMemcpyHostToDevice));
+    CK(dalloc(&m->rope_dec, (size_t)positions * c.dec_head_dim));
+    host_rope(t.data(), 0, positions, c.dec_head_dim, c.rope_theta);
+    CK(hipMemcpy(m->rope_dec, t.data(), (size_t)positions * c.dec_head_dim * 4, hipMemcpyHostToDevice));
+    m->rope_positions = positions;
+    return 0;
+}
+
+static int check_config(const vox_hip_config_t* c) {
+    if (c->enc_head_dim != 64 && c->enc_head_dim != 128) return set_err("enc_head_dim must be 64/128");
+    if (c->dec_head_dim != 64 && c->dec_head_dim != 128) return set_err("dec_head_dim must be 64/128");
+    if (c->enc_heads % c->enc_kv_heads || c->dec_heads % c->dec_kv_heads)
+        return set_err("heads must be a multiple of kv heads");
+    if (c->dec_heads / c->dec_kv_heads > 4 || c->enc_heads / c->enc_kv_heads > 4)
+        return set_err("GQA ratio > 4 unsupported");
+    int dims[] = {c->enc_dim, c->enc_hidden, c->dec_dim, c->dec_hidden,
+                  c->enc_heads * c->enc_head_dim, c->dec_heads * c->dec_head_dim,
+                  c->dec_kv_heads * c->dec_head_dim, c->mel_bins * 3};
+    for (int d : dims)
+        if (d % 64) return set_err("dimension %d not a multiple of 64", d);
+    if (c->vocab % 2) return set_err("vocab must be even");
+    if (c->downsample != 4) return set_err("downsample must be 4");
+    return 0;
+}
+
+extern "C" void vox_hip_model_free(vox_hip_model_t* m);
+
+extern "C" vox_hip_model_t* vox_hip_model_create(const vox_hip_config_t* cfg,
+                                                 const vox_hip_weights_t* w, int delay_tokens) {
+    if (!g_inited && !vox_hip_init()) return nullptr;
+    if (check_config(cfg)) return nullptr;
+    vox_hip_model_t* m = new vox_hip_model_t();
+    memset(&m->c, 0, sizeof m->c);
+    m->c = *cfg;
+    m->delay_tokens = delay_tokens;
+    m->conv0_w = m->conv1_w = m->ad0 = m->ad1 = m->tok_emb = nullptr;
+    m->conv0_b = m->conv1_b = m->enc_norm = m->dec_norm = m->ada_scale = nullptr;
+    m->rope_enc = m->rope_dec = nullptr;
+    const vox_hip_config_t& c = *cfg;
+    const int ED = c.enc_dim, EQ = c.enc_heads * c.enc_head_dim, EKV = c.enc_kv_heads * c.enc_head_dim;
+    const int EH = c.enc_hidden;
+    const int DD = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
+    const int DH = c.dec_hidden;
+    auto fail = [&]() -> vox_hip_model_t* { vox_hip_model_free(m); return nullptr; };
+#define TRY(x) do { if ((x) != 0) return fail(); } while (0)
+#define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
+    // conv stem
+    TRYH(dalloc(&m->conv0_w, (size_t)ED * c.mel_bins * 3));
+    TRY(upload_f32_as_bf16(m->conv0_w, w->conv0_w, (size_t)ED * c.mel_bins * 3));
+    TRYH(dalloc(&m->conv1_w, (size_t)ED * ED * 3));
+    TRY(upload_f32_as_bf16(m->conv1_w, w->conv1_w, (size_t)ED * ED * 3));
+    TRYH(dalloc(&m->conv0_b, ED));
+    TRY(upload(m->conv0_b, w->conv0_b, ED * 4));
+    TRYH(dalloc(&m->conv1_b, ED));
+    TRY(upload(m->conv1_b, w->conv1_b, ED * 4));
+    // encoder layers
+    m->enc.resize(c.enc_layers);
+    for (int l = 0; l < c.enc_layers; l++) {
+        EncLayerD& L = m->enc[l];
+        memset(&L, 0, sizeof L);
+        TRYH(dalloc(&L.wqkv, (size_t)(EQ + 2 * EKV) * ED));
+        TRY(upload(L.wqkv, w->enc_wq[l], (size_t)EQ * ED * 2));
+        TRY(upload(L.wqkv + (size_t)EQ * ED, w->enc_wk[l], (size_t)EKV * ED * 2));
+        TRY(upload(L.wqkv + (size_t)(EQ + EKV) * ED, w->enc_wv[l], (size_t)EKV * ED * 2));
+        TRYH(dalloc(&L.bqkv, EQ + 2 * EKV));  // k part stays zero: wk has no bias
+        TRY(upload(L.bqkv, w->enc_wq_b[l], EQ * 4));
+        TRY(upload(L.bqkv + EQ + EKV, w->enc_wv_b[l], EKV * 4));
+        TRYH(dalloc(&L.wo, (size_t)ED * EQ));
+        TRY(upload(L.wo, w->enc_wo[l], (size_t)ED * EQ * 2));
+        TRYH(dalloc(&L.bo, ED));
+        TRY(upload(L.bo, w->enc_wo_b[l], ED * 4));
+        TRYH(dalloc(&L.w13, (size_t)2 * EH * ED));
+        TRY(upload_w13(L.w13, w->enc_w1[l], w->enc_w3[l], EH, ED));
+        TRYH(dalloc(&L.w2, (size_t)ED * EH));
+        TRY(upload(L.w2, w->enc_w2[l], (size_t)ED * EH * 2));
+        TRYH(dalloc(&L.b2, ED));
+        TRY(upload(L.b2, w->enc_w2_b[l], ED * 4));
+        TRYH(dalloc(&L.attn_norm, ED));
+        TRY(upload(L.attn_norm, w->enc_attn_norm[l], ED * 4));
+        TRYH(dalloc(&L.ffn_norm, ED));
+        TRY(upload(L.ffn_norm, w->enc_ffn_norm[l], ED * 4));
+    }
+    TRYH(dalloc(&m->enc_norm, ED));
+    TRY(upload(m->enc_norm, w->enc_norm, ED * 4));
+    // adapter
+    TRYH(dalloc(&m->ad0, (size_t)DD * ED * c.downsample));
+    TRY(upload(m->ad0, w->ad0, (size_t)DD * ED * c.downsample * 2));
+    TRYH(dalloc(&m->ad1, (size_t)DD * DD));
+    TRY(upload(m->ad1, w->ad1, (size_t)DD * DD * 2));
+    // decoder
+    TRYH(dalloc(&m->tok_emb, (size_t)c.vocab * DD));
+    TRY(upload(m->tok_emb, w->tok_emb, (size_t)c.vocab * DD * 2));
+    m->dec.resize(c.dec_layers);
+    m->ada_down.resize(c.dec_layers);
+    m->ada_up.resize(c.dec_layers);
+    for (int l = 0; l < c.dec_layers; l++) {
+        DecLayerD& L = m->dec[l];
+        memset(&L, 0, sizeof L);
+        TRYH(dalloc(&L.wqkv, (size_t)(DQ + 2 * DKV) * DD));
+        TRY(upload(L.wqkv, w->dec_wq[l], (size_t)DQ * DD * 2));
+        TRY(upload(L.wqkv + (size_t)DQ * DD, w->dec_wk[l], (size_t)DKV * DD * 2));
+        TRY(upload(L.wqkv + (size_t)(DQ + DKV) * DD, w->dec_wv[l], (size_t)DKV * DD * 2));
+        TRYH(dalloc(&L.wo, (size_t)DD * DQ));
+        TRY(upload(L.wo, w->dec_wo[l], (size_t)DD * DQ * 2));
+        TRYH(dalloc(&L.w13, (size_t)2 * DH * DD));
+        TRY(upload_w13(L.w13, w->dec_w1[l], w->dec_w3[l], DH, DD));
+        TRYH(dalloc(&L.w2, (size_t)DD * DH));
+        TRY(upload(L.w2, w->dec_w2[l], (size_t)DD * DH * 2));
+        TRYH(dalloc(&L.attn_norm, DD));
+        TRY(upload(L.attn_norm, w->dec_attn_norm[l], DD * 4));
+        TRYH(dalloc(&L.ffn_norm, DD));
+        TRY(upload(L.ffn_norm, w->dec_ffn_norm[l], DD * 4));
+        if (!w->dec_ada_down[l] || !w->dec_ada_up[l]) { set_err("null ada weights"); return fail(); }
+        m->ada_down[l].assign(w->dec_ada_down[l], w->dec_ada_down[l] + (size_t)c.ada_dim * DD);
+        m->ada_up[l].assign(w->dec_ada_up[l], w->dec_ada_up[l] + (size_t)DD * c.ada_dim);
+    }
+    TRYH(dalloc(&m->dec_norm, DD));
+    TRY(upload(m->dec_norm, w->dec_norm, DD * 4));
+    TRYH(dalloc(&m->ada_scale, (size_t)c.dec_layers * DD));
+    TRY(model_update_ada(m));
+    TRY(model_rope_tables(m, 32768));
+#undef TRY
+#undef TRYH
+    return m;
+}
+
+extern "C" void vox_hip_model_free(vox_hip_model_t* m) {
+    if (!m) return;
+    dfree(m->conv0_w); dfree(m->conv1_w); dfree(m->conv0_b); dfree(m->conv1_b);
+    for (auto& L : m->enc) {
+        dfree(L.wqkv); dfree(L.wo); dfree(L.w13); dfree(L.w2);
+        dfree(L.bqkv); dfree(L.bo); dfree(L.b2); dfree(L.attn_norm); dfree(L.ffn_norm);
+    }
+    for (auto& L : m->dec) {
+        dfree(L.wqkv); dfree(L.wo); dfree(L.w13); dfree(L.w2);
+        dfree(L.attn_norm); dfree(L.ffn_norm);
+    }
+    dfree(m->enc_norm); dfree(m->ad0); dfree(m->ad1); dfree(m->tok_emb); dfree(m->dec_norm);
+    dfree(m->ada_scale); dfree(m->rope_enc); dfree(m->rope_dec);
+    delete m;
+}
+
+extern "C" int vox_hip_model_set_delay(vox_hip_model_t* m, int delay_tokens) {
+    m->delay_tokens = delay_tokens;
+    return model_update_ada(m);
+}
+
+extern "C" int vox_hip_model_ada_scale(vox_hip_model_t* m, float* out) {
+    memcpy(out, m->ada_host.data(), m->ada_host.size() * 4);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Stream
+// ---------------------------------------------------------------------------
+static const int ENC_SUB = 1024;      // encoder rows per pass through the 32 layers
+static const int DEC_SLACK = 64;      // decoder ring capacity = window + slack
+static const int NSPLIT_ATT = 32;     // decode attention key splits
+static const int STEP_BATCH = 16;     // graph replays between EOS checks
+
+struct vox_hip_stream {
+    vox_hip_model_t* m;
+    hipStream_t st;
+    // rolling KV caches [layers][cap][kv_dim]
+    float *ek, *ev, *dk, *dv;
+    int ecap, dcap;
+    long long enc_pos;  // next encoder logical position
+    // conv stem
+    float *mel_p, *mel_tail, *c0_p, *c0_tail, *c0_res, *im2col;
+    int res_count;
+    int frames_cap;   // capacity (mel frames) of the conv buffers
+    // encoder
+    float *x_enc, *xn, *qkv, *q, *att, *gate, *enc_res;
+    int x_rows_cap;
+    int enc_res_count;
+    float *rope_rows;  // per-call rope rows for the boundary twins
+    int rope_rows_cap;
+    // adapter
+    float *adapter, *ad_mid;
+    int adapter_cap, total_adapter;
+    // decoder
+    float *xd, *xnd, *qkvd, *qd_, *attd, *gated, *part, *logits, *pval;
+    int *pidx, *state, *tokens;
+    int dec_rows_cap, tokens_cap;
+    hipGraphExec_t step_exec;
+    int graph_ready;
+    int started, eos_seen, n_generated;
+    int h_state[4];
+    // profiling
+    int profiling;
+    hipEvent_t evt[2];
+    double prof_ms, prof_bytes;
+    long long prof_launches;
+};
+
+static int stream_alloc_frames(vox_hip_stream_t* s, int frames) {
+    if (frames <= s->frames_cap) return 0;
+    const vox_hip_config_t& c = s->m->c;
+    int f = 256;
+    while (f < frames) f *= 2;
+    dfree(s->mel_p); dfree(s->c0_p); dfree(s->im2col); dfree(s->x_enc);
+    CK(dalloc(&s->mel_p, (size_t)(f + 2) * c.mel_bins));
+    CK(dalloc(&s->c0_p, (size_t)(f + 3) * c.enc_dim));
+    size_t im = std::max((size_t)f * c.mel_bins * 3, (size_t)(f / 2 + 2) * c.enc_dim * 3);
+    CK(dalloc(&s->im2col, im));
+    CK(dalloc(&s->x_enc, (size_t)(f / 2 + 8) * c.enc_dim));
+    s->frames_cap = f;
+    return 0;
+}
+
+static int stream_alloc_adapter(vox_hip_stream_t* s, int need) {
+    if (need <= s->adapter_cap) return 0;
+    const int D = s->m->c.dec_dim;
+    int nc = s->adapter_cap ? s->adapter_cap : 1024;
+    while (nc < need) nc *= 2;
+    float* na = nullptr;
+    CK(dalloc(&na, (size_t)nc * D));
+    if (s->adapter && s->total_adapter > 0)
+        CK(hipMemcpyAsync(na, s->adapter, (size_t)s->total_adapter * D * 4, hipMemcpyDeviceToDevice, s->st));
+    CK(hipStreamSynchronize(s->st));
+    dfree(s->adapter);
+    s->adapter = na;
+    s->adapter_cap = nc;
+    s->graph_ready = 0;  // the step graph captured the old pointer
+    return 0;
+}
+
+static int stream_alloc_dec_rows(vox_hip_stream_t* s, int rows) {
+    if (rows <= s->dec_rows_cap) return 0;
+    const vox_hip_config_t& c = s->m->c;
+    int r = 64;
+    while (r < rows) r *= 2;
+    const int DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
+    dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
+    CK(dalloc(&s->xd, (size_t)r * c.dec_dim));
+    CK(dalloc(&s->xnd, (size_t)r * c.dec_dim));
+    CK(dalloc(&s->qkvd, (size_t)r * (DQ + 2 * DKV)));
+    CK(dalloc(&s->qd_, (size_t)r * DQ));
+    CK(dalloc(&s->attd, (size_t)r * DQ));
+    CK(dalloc(&s->gated, (size_t)r * c.dec_hidden));
+    s->dec_rows_cap = r;
+    s->graph_ready = 0;
+    return 0;
+}
+
+extern "C" void vox_hip_stream_free(vox_hip_stream_t* s);
+
+extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
+    vox_hip_stream_t* s = new vox_hip_stream_t();
+    memset(s, 0, sizeof *s);
+    s->m = m;
+    const vox_hip_config_t& c = m->c;
+    auto fail = [&]() -> vox_hip_stream_t* { vox_hip_stream_free(s); return nullptr; };
+#define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
+    TRYH(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    const int EKV = c.enc_kv_heads * c.enc_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
+    const int EQ = c.enc_heads * c.enc_head_dim;
+    s->ecap = c.enc_window + ENC_SUB + 64;
+    s->dcap = c.dec_window + DEC_SLACK;
+    TRYH(dalloc(&s->ek, (size_t)c.enc_layers * s->ecap * EKV));
+    TRYH(dalloc(&s->ev, (size_t)c.enc_layers * s->ecap * EKV));
+    TRYH(dalloc(&s->dk, (size_t)c.dec_layers * s->dcap * DKV));
+    TRYH(dalloc(&s->dv, (size_t)c.dec_layers * s->dcap * DKV));
+    TRYH(dalloc(&s->mel_tail, (size_t)2 * c.mel_bins));
+    TRYH(dalloc(&s->c0_tail, (size_t)2 * c.enc_dim));
+    TRYH(dalloc(&s->c0_res, (size_t)c.enc_dim));
+    TRYH(dalloc(&s->enc_res, (size_t)4 * c.enc_dim));
+    TRYH(dalloc(&s->xn, (size_t)ENC_SUB * c.enc_dim));
+    TRYH(dalloc(&s->qkv, (size_t)ENC_SUB * (EQ + 2 * EKV)));
+    TRYH(dalloc(&s->q, (size_t)ENC_SUB * EQ));
+    TRYH(dalloc(&s->att, (size_t)ENC_SUB * EQ));
+    TRYH(dalloc(&s->gate, (size_t)ENC_SUB * c.enc_hidden));
+    TRYH(dalloc(&s->ad_mid, (size_t)(ENC_SUB / 4 + 4) * c.dec_dim));
+    TRYH(dalloc(&s->part, (size_t)c.dec_heads * NSPLIT_ATT * (c.dec_head_dim + 2) + (size_t)c.enc_heads * NSPLIT_ATT * (c.enc_head_dim + 2)));
+    TRYH(dalloc(&s->logits, (size_t)c.vocab));
+    TRYH(dalloc(&s->pval, GEMV_MAX_BLOCKS));
+    TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
+    TRYH(dalloc(&s->state, 4));
+    s->tokens_cap = 1 << 16;
+    TRYH(dalloc(&s->tokens, s->tokens_cap));
+    TRYH(hipEventCreate(&s->evt[0]));
+    TRYH(hipEventCreate(&s->evt[1]));
+#undef TRYH
+    if (stream_alloc_frames(s, 2048) || stream_alloc_adapter(s, 1024) || stream_alloc_dec_rows(s, 64))
+        return fail();
+    if (vox_hip_stream_reset(s)) return fail();
+    return s;
+}
+
+extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
+    if (!s) return;
+    if (s->st) hipStreamSynchronize(s->st);
+    if (s->step_exec) hipGraphExecDestroy(s->step_exec);
+    dfree(s->ek); dfree(s->ev); dfree(s->dk); dfree(s->dv);
+    dfree(s->mel_p); dfree(s->mel_tail); dfree(s->c0_p); dfree(s->c0_tail); dfree(s->c0_res);
+    dfree(s->im2col); dfree(s->x_enc); dfree(s->xn); dfree(s->qkv); dfree(s->q); dfree(s->att);
+    dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
+    dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
+    dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->tokens);
+    if (s->evt[0]) hipEventDestroy(s->evt[0]);
+    if (s->evt[1]) hipEventDestroy(s->evt[1]);
+    if (s->st) hipStreamDestroy(s->st);
+    delete s;
+}
+
+extern "C" int vox_hip_stream_reset_decoder(vox_hip_stream_t* s) {
+    // stream_reset_decoder_state (voxtral.c:766-783): KV length 0, adapter backlog dropped
+    s->total_adapter = 0;
+    s->started = 0;
+    s->eos_seen = 0;
+    s->n_generated = 0;
+    int st[4] = {0, 0, TOKEN_BOS, 0};
+    memcpy(s->h_state, st, sizeof st);
+    CK(hipMemcpyAsync(s->state, st, sizeof st, hipMemcpyHostToDevice, s->st));
+    CK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+extern "C" int vox_hip_stream_reset(vox_hip_stream_t* s) {
+    // stream_reset_full_state (voxtral.c:786-814)
+    const vox_hip_config_t& c = s->m->c;
+    s->enc_pos = 0;
+    s->res_count = 0;
+    s->enc_res_count = 0;
+    CK(hipMemsetAsync(s->mel_tail, 0, (size_t)2 * c.mel_bins * 4, s->st));
+    CK(hipMemsetAsync(s->c0_tail, 0, (size_t)2 * c.enc_dim * 4, s->st));
+    return vox_hip_stream_reset_decoder(s);
+}
+
+extern "C" int vox_hip_stream_sync(vox_hip_stream_t* s) {
+    CK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Encoder: 32 layers on rows [0, n) of x (logical positions pos0..), in place.
+// voxtral_encoder.c:562-686.  rope: rows for these positions (table slice or per-call).
+// ---------------------------------------------------------------------------
+static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0, const float* rope) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, H = c.enc_heads, KVH = c.enc_kv_heads, hd = c.enc_head_dim;
+    const int EQ = H * hd, EKV = KVH * hd, EH = c.enc_hidden;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = s->st;
+    if (n > ENC_SUB) return set_err("encoder pass of %d rows > %d", n, ENC_SUB);
+    for (int l = 0; l < c.enc_layers; l++) {
+        const EncLayerD& L = m->enc[l];
+        float* Kc = s->ek + (size_t)l * s->ecap * EKV;
+        float* Vc = s->ev + (size_t)l * s->ecap * EKV;
+        CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.attn_norm, nullptr, n, ED, c.enc_eps, st));
+        CK(launch_gemm(EPI_STORE, 3, s->xn, ED, L.wqkv, ED, n, EQ + 2 * EKV, L.bqkv, s->qkv, EQ + 2 * EKV, st));
+        CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
+        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st));
+        CK(launch_gemm(EPI_RESID, 3, s->att, EQ, L.wo, EQ, n, ED, L.bo, x, ED, st));
+        CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.ffn_norm, nullptr, n, ED, c.enc_eps, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, s->xn, ED, L.w13, ED, n, 2 * EH, nullptr, s->gate, EH, st));
+        CK(launch_gemm(EPI_RESID, 3, s->gate, EH, L.w2, EH, n, ED, L.b2, x, ED, st));
+    }
+    CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, n, ED, c.enc_eps, st));
+    return 0;
+}
+
+static int ensure_rope(vox_hip_stream_t* s, long long last_pos) {
+    vox_hip_model_t* m = s->m;
+    if (last_pos < m->rope_positions) return 0;
+    int p = m->rope_positions;
+    while (p <= last_pos) p *= 2;
+    CK(hipDeviceSynchronize());
+    if (model_rope_tables(m, p)) return -1;
+    s->graph_ready = 0;
+    return 0;
+}
+
+extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, int n, int mel_on_device) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int MB = c.mel_bins, ED = c.enc_dim, D = c.dec_dim;
+    hipStream_t st = s->st;
+    if (n <= 0) return 0;
+    if (stream_alloc_frames(s, n + 4)) return -1;
+    // ---- conv0 over [mel_tail(2) | new n] (voxtral.c:594-651) ----
+    CK(hipMemcpyAsync(s->mel_p, s->mel_tail, (size_t)2 * MB * 4, hipMemcpyDeviceToDevice, st));
+    CK(hipMemcpyAsync(s->mel_p + (size_t)2 * MB, mel, (size_t)n * MB * 4,
+                      mel_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    CK(launch_mel_tail(s->mel_p, n, MB, s->mel_tail, st));
+    // c0_p rows: [c0_tail(2) | residual(res_count) | conv0 new (n)]
+    CK(hipMemcpyAsync(s->c0_p, s->c0_tail, (size_t)2 * ED * 4, hipMemcpyDeviceToDevice, st));
+    if (s->res_count)
+        CK(hipMemcpyAsync(s->c0_p + (size_t)2 * ED, s->c0_res, (size_t)ED * 4, hipMemcpyDeviceToDevice, st));
+    float* c0_new = s->c0_p + (size_t)(2 + s->res_count) * ED;
+    CK(launch_im2col3(s->mel_p, MB, n, 1, 0, s->im2col, st));
+    CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, MB * 3, m->conv0_w, MB * 3, n, ED,
+                   m->conv0_b, c0_new, ED, st));
+    // ---- stride alignment (voxtral.c:653-692) ----
+    const int total = s->res_count + n;
+    const int new_res = total & 1;
+    const int feed = total - new_res;
+    if (new_res)
+        CK(hipMemcpyAsync(s->c0_res, s->c0_p + (size_t)(2 + total - 1) * ED, (size_t)ED * 4,
+                          hipMemcpyDeviceToDevice, st));
+    s->res_count = new_res;
+    if (feed <= 0) {
+        CK(hipStreamSynchronize(st));
+        return 0;
+    }
+    // ---- conv1 over [c0_tail(2) | feed], first output discarded (voxtral.c:694-756) ----
+    const int T1 = feed / 2;
+    float* xin = s->x_enc + (size_t)4 * ED;  // 4 spare rows in front for the downsample residual
+    CK(launch_im2col3(s->c0_p, ED, T1, 2, 1, s->im2col, st));
+    CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, ED * 3, m->conv1_w, ED * 3, T1, ED,
+                   m->conv1_b, xin, ED, st));
+    CK(hipMemcpyAsync(s->c0_tail, s->c0_p + (size_t)(2 + feed - 2) * ED, (size_t)2 * ED * 4,
+                      hipMemcpyDeviceToDevice, st));
+    // ---- encoder (voxtral_encoder.c:495-693), sub-chunks through all layers ----
+    if (ensure_rope(s, s->enc_pos + T1 + 1)) return -1;
+    for (int r0 = 0; r0 < T1; r0 += ENC_SUB) {
+        int nr = std::min(ENC_SUB, T1 - r0);
+        long long p0 = s->enc_pos + r0;
+        if (run_encoder_rows(s, xin + (size_t)r0 * ED, nr, p0, m->rope_enc + (size_t)p0 * c.enc_head_dim))
+            return -1;
+    }
+    s->enc_pos += T1;
+    // ---- 4x downsample with residual + adapter (voxtral.c:868-934, encoder.c:699-737) ----
+    const int R = s->enc_res_count;
+    const int tot = R + T1;
+    const int usable = (tot / 4) * 4;
+    const int left = tot - usable;
+    int added = 0;
+    if (usable > 0) {
+        if (R) CK(hipMemcpyAsync(xin - (size_t)R * ED, s->enc_res, (size_t)R * ED * 4, hipMemcpyDeviceToDevice, st));
+        const float* ain = xin - (size_t)R * ED;
+        const int n4 = usable / 4;
+        if (stream_alloc_adapter(s, s->total_adapter + n4)) return -1;
+        for (int r0 = 0; r0 < n4; r0 += ENC_SUB / 4) {
+            int nr = std::min(ENC_SUB / 4, n4 - r0);
+            CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, ain + (size_t)r0 * 4 * ED, 4 * ED, m->ad0,
+                           4 * ED, nr, D, nullptr, s->ad_mid, D, st));
+            CK(launch_gemm(EPI_STORE, 3, s->ad_mid, D, m->ad1, D, nr, D, nullptr,
+                           s->adapter + (size_t)(s->total_adapter + r0) * D, D, st));
+        }
+        s->total_adapter += n4;
+        added = n4;
+        if (left)
+            CK(hipMemcpyAsync(s->enc_res, ain + (size_t)usable * ED, (size_t)left * ED * 4, hipMemcpyDeviceToDevice, st));
+    } else if (T1 > 0) {
+        // fewer than 4 rows in total: keep all of them (old residual followed by new rows)
+        CK(hipMemcpyAsync(s->enc_res + (size_t)R * ED, xin, (size_t)T1 * ED * 4, hipMemcpyDeviceToDevice, st));
+    }
+    s->enc_res_count = left;
+    CK(hipStreamSynchronize(st));
+    return added;
+}
+
+extern "C" int vox_hip_stream_adapter_tokens(vox_hip_stream_t* s) { return s->total_adapter; }
+
+extern "C" int vox_hip_stream_read_adapter(vox_hip_stream_t* s, int first, int n, float* out) {
+    const int D = s->m->c.dec_dim;
+    if (first < 0 || first + n > s->total_adapter) return set_err("adapter rows out of range");
+    CK(hipMemcpy(out, s->adapter + (size_t)first * D, (size_t)n * D * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Decoder
+// ---------------------------------------------------------------------------
+// M>1 rows (prefill) at logical positions pos0.. (voxtral_decoder.c:496-606)
+static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, const float* rope) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
+    const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = s->st;
+    if (stream_alloc_dec_rows(s, n)) return -1;
+    if (n > DEC_SLACK + 1 && pos0 > 0) return set_err("prefill of %d rows on a non-empty cache", n);
+    for (int l = 0; l < c.dec_layers; l++) {
+        const DecLayerD& L = m->dec[l];
+        float* Kc = s->dk + (size_t)l * s->dcap * DKV;
+        float* Vc = s->dv + (size_t)l * s->dcap * DKV;
+        CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.attn_norm, nullptr, n, DD, c.dec_eps, st));
+        CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st));
+        CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st));
+        CK(launch_attn_tiled(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st));
+        CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, DQ, n, DD, nullptr, x, DD, st));
+        CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, n, DD, c.dec_eps, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, s->xnd, DD, L.w13, DD, n, 2 * DH, nullptr, s->gated, DH, st));
+        CK(launch_gemm(EPI_RESID, 3, s->gated, DH, L.w2, DH, n, DD, nullptr, x, DD, st));
+    }
+    return 0;
+}
+
+// One decoder step for the token whose input is already in s->xd[0..D).
+// state != nullptr: positions come from device state (graph mode);
+// otherwise pos/rope_row are host values (boundary twin).
+static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
+    const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = s->st;
+    for (int l = 0; l < c.dec_layers; l++) {
+        const DecLayerD& L = m->dec[l];
+        float* Kc = s->dk + (size_t)l * s->dcap * DKV;
+        float* Vc = s->dv + (size_t)l * s->dcap * DKV;
+        GemvArgs a;
+        memset(&a, 0, sizeof a);
+        // norm -> QKV -> RoPE -> KV append (decoder.c:709-722)
+        a.x = s->xd; a.K = DD; a.W = L.wqkv; a.units = (DQ + 2 * DKV) / 2;
+        a.norm_w = L.attn_norm; a.eps = c.dec_eps; a.y = s->qd_;
+        a.qd = DQ; a.kvd = DKV; a.hd = hd;
+        a.state = state; a.pos = pos;
+        a.rope = state ? m->rope_dec : rope_row - (size_t)pos * hd;
+        a.Kc = Kc; a.Vc = Vc; a.cap = s->dcap;
+        CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
+        // attention over the last min(pos+1, window) keys (decoder.c:724-733)
+        CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
+                              NSPLIT_ATT, s->part, s->attd, st));
+        // wo + residual (decoder.c:735-740)
+        memset(&a, 0, sizeof a);
+        a.x = s->attd; a.K = DQ; a.W = L.wo; a.units = DD / 2; a.y = s->xd;
+        CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
+        // norm * (1 + ada) -> W1|W3 -> silu * up (decoder.c:742-758)
+        memset(&a, 0, sizeof a);
+        a.x = s->xd; a.K = DD; a.W = L.w13; a.units = DH; a.norm_w = L.ffn_norm;
+        a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
+        if (s->profiling && !state) CK(hipEventRecord(s->evt[0], st));
+        CK(launch_gemv(PRO_NORM_ADA, EPI_SWIGLU, a, st));
+        if (s->profiling && !state) {
+            CK(hipEventRecord(s->evt[1], st));
+            CK(hipEventSynchronize(s->evt[1]));
+            float ms = 0.f;
+            CK(hipEventElapsedTime(&ms, s->evt[0], s->evt[1]));
+            s->prof_ms += ms;
+            s->prof_bytes += (double)2 * DH * DD * 2;
+            s->prof_launches++;
+        }
+        // W2 + residual (decoder.c:758-760)
+        memset(&a, 0, sizeof a);
+        a.x = s->gated; a.K = DH; a.W = L.w2; a.units = DD / 2; a.y = s->xd;
+        CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
+    }
+    // final norm + LM head (tied embeddings) + argmax (decoder.c:762-779)
+    GemvArgs a;
+    memset(&a, 0, sizeof a);
+    a.x = s->xd; a.K = DD; a.W = m->tok_emb; a.units = c.vocab / 2; a.norm_w = m->dec_norm;
+    a.eps = c.dec_eps; a.y = s->logits; a.part_val = s->pval; a.part_idx = s->pidx;
+    CK(launch_gemv(PRO_NORM, EPI_LOGITS, a, st));
+    return 0;
+}
+
+static int enqueue_graph_step(vox_hip_stream_t* s) {
+    const vox_hip_config_t& c = s->m->c;
+    CK(launch_embed_step(s->adapter, s->m->tok_emb, s->state, c.dec_dim, s->xd, s->st));
+    if (enqueue_step_layers(s, s->state, 0, nullptr)) return -1;
+    CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab / 2), s->state, s->tokens, s->tokens_cap, s->st));
+    return 0;
+}
+
+static int build_step_graph(vox_hip_stream_t* s) {
+    if (s->step_exec) {
+        hipGraphExecDestroy(s->step_exec);
+        s->step_exec = nullptr;
+    }
+    hipGraph_t g = nullptr;
+    CK(hipStreamBeginCapture(s->st, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_graph_step(s);
+    hipError_t e = hipStreamEndCapture(s->st, &g);
+    if (rc || e != hipSuccess) {
+        if (g) hipGraphDestroy(g);
+        return set_err("graph capture failed: %s", hipGetErrorString(e));
+    }
+    e = hipGraphInstantiate(&s->step_exec, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) return set_err("graph instantiate failed: %s", hipGetErrorString(e));
+    s->graph_ready = 1;
+    return 0;
+}
+
+static int run_steps(vox_hip_stream_t* s, int n) {
+    if (s->profiling) {
+        for (int i = 0; i < n; i++) {
+            // eager with HIP events around the dominant GEMV (profiling mode only)
+            const vox_hip_config_t& c = s->m->c;
+            CK(launch_embed_step(s->adapter, s->m->tok_emb, s->state, c.dec_dim, s->xd, s->st));
+            CK(hipMemcpyAsync(s->h_state, s->state, 16, hipMemcpyDeviceToHost, s->st));
+            CK(hipStreamSynchronize(s->st));
+            const int pos = s->h_state[0];
+            if (enqueue_step_layers(s, nullptr, pos, s->m->rope_dec + (size_t)pos * c.dec_head_dim)) return -1;
+            CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab / 2), s->state, s->tokens, s->tokens_cap, s->st));
+        }
+        return 0;
+    }
+    if (!s->graph_ready && build_step_graph(s)) return -1;
+    for (int i = 0; i < n; i++) CK(hipGraphLaunch(s->step_exec, s->st));
+    return 0;
+}
+
+extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int stop_at_eos,
+                                     int* tokens_out, float* logits_out) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int D = c.dec_dim, V = c.vocab, hd = c.dec_head_dim;
+    const int prompt_len = 1 + 32 + m->delay_tokens;
+    int produced = 0;
+    if (max_steps <= 0 || s->eos_seen) return 0;
+    if (!s->started) {
+        if (s->total_adapter < prompt_len) return 0;
+        // prompt embeds + prefill rows 0..prompt_len-2 (voxtral.c:1036-1057)
+        const int np = prompt_len - 1;
+        if (stream_alloc_dec_rows(s, np)) return -1;
+        if (ensure_rope(s, prompt_len + 1)) return -1;
+        CK(launch_embed_rows(s->adapter, m->tok_emb, 0, np, TOKEN_BOS, TOKEN_STREAMING_PAD, D, s->xd, s->st));
+        if (run_decoder_rows(s, s->xd, np, 0, m->rope_dec)) return -1;
+        int st4[4] = {np, np, TOKEN_STREAMING_PAD, s->n_generated};
+        CK(hipMemcpyAsync(s->state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
+        s->started = 1;
+        // the first generated token comes from row prompt_len-1 through a regular step
+    }
+    const int step_base = s->n_generated;
+    int avail = s->total_adapter - (s->h_state[1] > 0 ? s->h_state[1] : prompt_len - 1);
+    {
+        // host mirror of the device state (positions advance by exactly one per step)
+        int st4[4];
+        CK(hipMemcpyAsync(st4, s->state, sizeof st4, hipMemcpyDeviceToHost, s->st));
+        CK(hipStreamSynchronize(s->st));
+        memcpy(s->h_state, st4, sizeof st4);
+        avail = s->total_adapter - st4[1];
+    }
+    if (ensure_rope(s, (long long)s->h_state[0] + avail + 1)) return -1;
+    if (s->n_generated + avail > s->tokens_cap) avail = s->tokens_cap - s->n_generated;
+    int todo = std::min(max_steps, avail);
+    std::vector<int> tok;
+    while (produced < todo) {
+        int b = std::min(STEP_BATCH, todo - produced);
+        if (logits_out) b = 1;
+        if (run_steps(s, b)) return -1;
+        tok.resize(produced + b);
+        CK(hipMemcpyAsync(tok.data() + produced, s->tokens + step_base + produced, (size_t)b * 4,
+                          hipMemcpyDeviceToHost, s->st));
+        if (logits_out)
+            CK(hipMemcpyAsync(logits_out + (size_t)produced * V, s->logits, (size_t)V * 4, hipMemcpyDeviceToHost, s->st));
+        CK(hipStreamSynchronize(s->st));
+        int eos_at = -1;
+        if (stop_at_eos)
+            for (int i = produced; i < produced + b; i++)
+                if (tok[i] == TOKEN_EOS) { eos_at = i; break; }
+        if (eos_at >= 0) {
+            produced = eos_at + 1;
+            s->eos_seen = 1;
+            break;
+        }
+        produced += b;
+    }
+    if (tokens_out) memcpy(tokens_out, tok.data(), (size_t)produced * 4);
+    s->n_generated += produced;
+    // host mirror; after an EOS the device ran ahead by at most one batch (never read again
+    // in non-continuous mode, voxtral.c:1140-1144)
+    s->h_state[0] += produced;
+    s->h_state[1] += produced;
+    if (produced) s->h_state[2] = tok[produced - 1];
+    s->h_state[3] = s->n_generated;
+    (void)hd;
+    return produced;
+}
+
+extern "C" int vox_hip_stream_state(vox_hip_stream_t* s, int* out6) {
+    out6[0] = s->h_state[0];
+    out6[1] = s->h_state[1];
+    out6[2] = s->h_state[2];
+    out6[3] = s->started;
+    out6[4] = s->eos_seen;
+    out6[5] = s->n_generated;
+    return 0;
+}
+
+extern "C" int vox_hip_stream_set_profiling(vox_hip_stream_t* s, int enable) {
+    s->profiling = enable;
+    s->prof_ms = 0;
+    s->prof_bytes = 0;
+    s->prof_launches = 0;
+    return 0;
+}
+
+extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
+    out8[0] = s->prof_ms;
+    out8[1] = s->prof_bytes;
+    out8[2] = (double)s->prof_launches;
+    out8[3] = s->prof_launches ? s->prof_ms / s->prof_launches : 0.0;
+    out8[4] = out8[5] = out8[6] = out8[7] = 0.0;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Reference-boundary twins (host pointers; voxtral_metal.h)
+// ---------------------------------------------------------------------------
+static std::mutex g_twin_mu;
+static std::unordered_map<const void*, uint16_t*> g_wcache;  // host weight ptr -> device copy
+static hipStream_t g_twin_st = nullptr;
+static float *g_tA = nullptr, *g_tC = nullptr, *g_tQ = nullptr, *g_tK = nullptr, *g_tV = nullptr, *g_tO = nullptr;
+static size_t g_tA_n = 0, g_tC_n = 0, g_tQ_n = 0, g_tK_n = 0, g_tV_n = 0, g_tO_n = 0;
+
+static int twin_buf(float** p, size_t* cap, size_t n) {
+    if (n <= *cap) return 0;
+    dfree(*p);
+    CK(dalloc(p, n));
+    *cap = n;
+    return 0;
+}
+
+static uint16_t* twin_weight(const uint16_t* host, size_t n) {
+    auto it = g_wcache.find(host);
+    if (it != g_wcache.end()) return it->second;
+    uint16_t* d = nullptr;
+    if (dalloc(&d, n) != hipSuccess) { set_err("weight alloc failed"); return nullptr; }
+    if (hipMemcpy(d, host, n * 2, hipMemcpyHostToDevice) != hipSuccess) { set_err("weight upload failed"); return nullptr; }
+    g_wcache[host] = d;
+    return d;
+}
+
+static int twin_init() {
+    if (!g_inited && !vox_hip_init()) return -1;
+    if (!g_twin_st) CK(hipStreamCreateWithFlags(&g_twin_st, hipStreamNonBlocking));
+    return 0;
+}
+
+static int twin_gemm(int M, int N, int K, const float* dA, const uint16_t* dW, float* dC) {
+    if (M == 1 && N % 2 == 0 && K % 8 == 0) {
+        GemvArgs a;
+        memset(&a, 0, sizeof a);
+        a.x = dA; a.K = K; a.W = dW; a.units = N / 2; a.y = dC;
+        CK(launch_gemv(PRO_NONE, EPI_STORE, a, g_twin_st));
+        return 0;
+    }
+    CK(launch_gemm(EPI_STORE, 3, dA, K, dW, K, M, N, nullptr, dC, N, g_twin_st));
+    return 0;
+}
+
+extern "C" void vox_hip_sgemm_bf16(int M, int N, int K, const float* A, const uint16_t* B, float* C) {
+    std::lock_guard<std::mutex> lk(g_twin_mu);
+    if (twin_init()) return;
+    uint16_t* dW = twin_weight(B, (size_t)N * K);
+    if (!dW) return;
+    if (twin_buf(&g_tA, &g_tA_n, (size_t)M * K) || twin_buf(&g_tC, &g_tC_n, (size_t)M * N)) return;
+    if (hipMemcpyAsync(g_tA, A, (size_t)M * K * 4, hipMemcpyHostToDevice, g_twin_st) != hipSuccess) { set_err("upload"); return; }
+    if (twin_gemm(M, N, K, g_tA, dW, g_tC)) return;
+    if (hipMemcpyAsync(C, g_tC, (size_t)M * N * 4, hipMemcpyDeviceToHost, g_twin_st) != hipSuccess) { set_err("download"); return; }
+    hipStreamSynchronize(g_twin_st);
+}
+
+extern "C" void vox_hip_fused_qkv_bf16(int M, int K, const float* input, const uint16_t* wq, int Nq,
+                                       const uint16_t* wk, int Nk, const uint16_t* wv, int Nv,
+                                       float* q, float* k, float* v) {
+    vox_hip_sgemm_bf16(M, Nq, K, input, wq, q);
+    vox_hip_sgemm_bf16(M, Nk, K, input, wk, k);
+    vox_hip_sgemm_bf16(M, Nv, K, input, wv, v);
+}
+
+__global__ void k_silu_mul(float* g, const float* u, size_t n) {
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        float v = g[i];
+        g[i] = v / (1.0f + expf(-v)) * u[i];
+    }
+}
+
+extern "C" void vox_hip_fused_ffn_bf16(int M, int dim, int hidden, const float* input,
+                                       const uint16_t* w1, const uint16_t* w3, const uint16_t* w2,
+                                       float* output) {
+    std::lock_guard<std::mutex> lk(g_twin_mu);
+    if (twin_init()) return;
+    uint16_t* d1 = twin_weight(w1, (size_t)hidden * dim);
+    uint16_t* d3 = twin_weight(w3, (size_t)hidden * dim);
+    uint16_t* d2 = twin_weight(w2, (size_t)dim * hidden);
+    if (!d1 || !d3 || !d2) return;
+    if (twin_buf(&g_tA, &g_tA_n, (size_t)M * dim) || twin_buf(&g_tQ, &g_tQ_n, (size_t)M * hidden) ||
+        twin_buf(&g_tK, &g_tK_n, (size_t)M * hidden) || twin_buf(&g_tC, &g_tC_n, (size_t)M * dim))
+        return;
+    hipMemcpyAsync(g_tA, input, (size_t)M * dim * 4, hipMemcpyHostToDevice, g_twin_st);
+    if (twin_gemm(M, hidden, dim, g_tA, d1, g_tQ) || twin_gemm(M, hidden, dim, g_tA, d3, g_tK)) return;
+    size_t n = (size_t)M * hidden;
+    hipLaunchKernelGGL(k_silu_mul, dim3((n + 255) / 256), dim3(256), 0, g_twin_st, g_tQ, g_tK, n);
+    if (twin_gemm(M, dim, hidden, g_tQ, d2, g_tC)) return;
+    hipMemcpyAsync(output, g_tC, (size_t)M * dim * 4, hipMemcpyDeviceToHost, g_twin_st);
+    hipStreamSynchronize(g_twin_st);
+}
+
+extern "C" void vox_hip_encoder_attention(float* out, const float* Q, const float* K, const float* V,
+                                          int seq_q, int seq_k, int n_heads, int n_kv_heads,
+                                          int head_dim, float scale, int window_size, int q_offset) {
+    std::lock_guard<std::mutex> lk(g_twin_mu);
+    if (twin_init()) return;
+    if (q_offset + seq_q > seq_k) { set_err("encoder_attention: queries beyond keys"); return; }
+    const size_t qn = (size_t)seq_q * n_heads * head_dim, kn = (size_t)seq_k * n_kv_heads * head_dim;
+    if (twin_buf(&g_tQ, &g_tQ_n, qn) || twin_buf(&g_tK, &g_tK_n, kn) || twin_buf(&g_tV, &g_tV_n, kn) ||
+        twin_buf(&g_tO, &g_tO_n, qn))
+        return;
+    hipMemcpyAsync(g_tQ, Q, qn * 4, hipMemcpyHostToDevice, g_twin_st);
+    hipMemcpyAsync(g_tK, K, kn * 4, hipMemcpyHostToDevice, g_twin_st);
+    hipMemcpyAsync(g_tV, V, kn * 4, hipMemcpyHostToDevice, g_twin_st);
+    int W = window_size > 0 ? window_size : (1 << 30);
+    if (launch_attn_tiled(head_dim, g_tQ, n_heads * head_dim, g_tK, g_tV, seq_k, g_tO, n_heads * head_dim,
+                          seq_q, n_heads, n_kv_heads, q_offset, 0, W, scale, g_twin_st) != hipSuccess) {
+        set_err("encoder_attention launch failed");
+        return;
+    }
+    hipMemcpyAsync(out, g_tO, qn * 4, hipMemcpyDeviceToHost, g_twin_st);
+    hipStreamSynchronize(g_twin_st);
+}
+
+static int upload_rope_rows(vox_hip_stream_t* s, const float* rope, size_t n) {
+    if (n > (size_t)s->rope_rows_cap) {
+        dfree(s->rope_rows);
+        CK(dalloc(&s->rope_rows, n));
+        s->rope_rows_cap = (int)n;
+    }
+    CK(hipMemcpyAsync(s->rope_rows, rope, n * 4, hipMemcpyHostToDevice, s->st));
+    return 0;
+}
+
+extern "C" int vox_hip_encoder_full_step(vox_hip_stream_t* s, float* x, int new_len,
+                                         const float* rope_freqs, int logical_start) {
+    const vox_hip_config_t& c = s->m->c;
+    const int ED = c.enc_dim;
+    if (stream_alloc_frames(s, 2 * new_len + 8)) return -1;
+    float* xin = s->x_enc + (size_t)4 * ED;
+    CK(hipMemcpyAsync(xin, x, (size_t)new_len * ED * 4, hipMemcpyHostToDevice, s->st));
+    if (upload_rope_rows(s, rope_freqs, (size_t)new_len * c.enc_head_dim)) return -1;
+    for (int r0 = 0; r0 < new_len; r0 += ENC_SUB) {
+        int nr = std::min(ENC_SUB, new_len - r0);
+        if (run_encoder_rows(s, xin + (size_t)r0 * ED, nr, (long long)logical_start + r0,
+                             s->rope_rows + (size_t)r0 * c.enc_head_dim))
+            return -1;
+    }
+    CK(hipMemcpyAsync(x, xin, (size_t)new_len * ED * 4, hipMemcpyDeviceToHost, s->st));
+    CK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+extern "C" int vox_hip_decoder_prefill_step(vox_hip_stream_t* s, float* x, int seq_len,
+                                            const float* rope_freqs, int logical_start) {
+    const vox_hip_config_t& c = s->m->c;
+    if (stream_alloc_dec_rows(s, seq_len)) return -1;
+    CK(hipMemcpyAsync(s->xd, x, (size_t)seq_len * c.dec_dim * 4, hipMemcpyHostToDevice, s->st));
+    if (upload_rope_rows(s, rope_freqs, (size_t)seq_len * c.dec_head_dim)) return -1;
+    if (run_decoder_rows(s, s->xd, seq_len, logical_start, s->rope_rows)) return -1;
+    CK(hipMemcpyAsync(x, s->xd, (size_t)seq_len * c.dec_dim * 4, hipMemcpyDeviceToHost, s->st));
+    CK(hipStreamSynchronize(s->st));
+    return 0;
+}
+
+extern "C" void vox_hip_decoder_start(vox_hip_stream_t* s, const float* x, int dim) {
+    if (hipMemcpyAsync(s->xd, x, (size_t)dim * 4, hipMemcpyHostToDevice, s->st) != hipSuccess)
+        set_err("decoder_start upload failed");
+}
+
+extern "C" void vox_hip_decoder_end(vox_hip_stream_t* s) { hipStreamSynchronize(s->st); }
+
+extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_freqs, int logical_pos,
+                                         float* logits) {
+    const vox_hip_config_t& c = s->m->c;
+    if (upload_rope_rows(s, rope_freqs, (size_t)c.dec_head_dim)) return -1;
+    if (enqueue_step_layers(s, nullptr, logical_pos, s->rope_rows)) return -1;
+    // argmax into a scratch state so the graph-mode device state is untouched
+    int* tmp_state = s->tokens + s->tokens_cap - 8;
+    int st4[4] = {0, 0, 0, 0};
+    CK(hipMemcpyAsync(tmp_state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
+    CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab / 2), tmp_state, nullptr, 0, s->st));
+    CK(hipMemcpyAsync(st4, tmp_state, sizeof st4, hipMemcpyDeviceToHost, s->st));
+    if (logits) CK(hipMemcpyAsync(logits, s->logits, (size_t)c.vocab * 4, hipMemcpyDeviceToHost, s->st));
+    CK(hipStreamSynchronize(s->st));
+    return st4[2];
+}

@@ -1,0 +1,60 @@
+// vox_hip_internal.h -- kernel launch interface shared by the engine and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vox {
+
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_GELU_ERF = 3, EPI_SWIGLU = 4, EPI_QKV = 5, EPI_LOGITS = 6 };
+enum { PRO_NONE = 0, PRO_NORM = 1, PRO_NORM_ADA = 2 };
+
+constexpr int GEMV_MAX_BLOCKS = 2048;  // 8 blocks of 256 threads per CU on 256 CUs
+
+struct GemvArgs {
+    const float* x;        // input vector [K] (device)
+    int K;
+    const uint16_t* W;     // bf16 [rows, K]
+    int units;             // row pairs (or hidden units for SWIGLU)
+    const float* norm_w;   // PRO_NORM*: RMSNorm weight [K]
+    const float* ada;      // PRO_NORM_ADA: ada_scale row [K]
+    float eps;
+    float* y;              // output
+    const float* bias;     // optional bias (STORE / RESID)
+    // EPI_QKV
+    int qd, kvd, hd;
+    const float* rope;     // rope table [pos][hd]
+    const int* state;      // device state (state[0] = logical position) or null
+    int pos;               // logical position when state == null
+    float* Kc;
+    float* Vc;
+    int cap;
+    // EPI_LOGITS
+    float* part_val;
+    int* part_idx;
+};
+
+int gemv_grid(int units);
+hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,
+                               const float* ada, int M, int D, float eps, hipStream_t st);
+hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const uint16_t* W, int K,
+                       int M, int N, const float* bias, float* C, int ldc, hipStream_t st);
+hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, const float* rope,
+                          int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st);
+hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
+                             int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
+                             int k_first, int window, float scale, hipStream_t st);
+hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st);
+hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
+                              const int* state, int pos_host, int window, float scale, int H,
+                              int KVH, int nsplit, float* part, float* out, hipStream_t st);
+hipError_t launch_embed_step(const float* adapter, const uint16_t* emb, const int* state, int D,
+                             float* x, hipStream_t st);
+hipError_t launch_embed_rows(const float* adapter, const uint16_t* emb, int row0, int n,
+                             int first_tok, int rest_tok, int D, float* x, hipStream_t st);
+hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
+                               int cap, hipStream_t st);
+hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
+                          hipStream_t st);
+hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);
+
+}  // namespace vox

@@ -1,0 +1,821 @@
+// vox_hip_kernels.hip -- CDNA4 (gfx950) kernels for the Voxtral hot path.
+//
+// Layout conventions (DESIGN.md "Data layout in HBM"):
+//   activations  f32 row-major [rows, features]
+//   weights      bf16 row-major [out, in] (nn.Linear layout, voxtral_safetensors.c:446-451);
+//                decoder/encoder Q|K|V merged row-wise, W1|W3 interleaved in 16-row groups
+//                (rows 32g..32g+15 = w1[16g..], rows 32g+16..32g+31 = w3[16g..])
+//   KV caches    f32 rolling buffers [cap][kv_heads*head_dim] per layer, slot = pos % cap
+//   rope tables  f32 [pos][head_dim/2][2] (cos, sin) computed on the host with the
+//                reference's float powf/cosf/sinf (voxtral_kernels.c:617-629)
+//
+// Numerics: every kernel keeps the reference's f32 arithmetic: f32 activations times
+// exact bf16->f32 weights, f32 accumulation (voxtral_kernels.c:154-240).  The MFMA GEMM
+// (M>1) splits each f32 activation into NSPLIT bf16 terms (hi + mid + lo for NSPLIT=3
+// reproduces the f32 value exactly), so products against the exact-bf16 weights are
+// exact and only the summation order differs from the CPU sgemm.
+#include "vox_hip_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vox {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+// streamed-once weights: non-temporal 16-B load (MI355X_MICROARCH.md row nt-weights)
+__device__ __forceinline__ uint4 ldnt(const uint4* p) {
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+__device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// round-to-nearest-even f32 -> bf16 bits (inputs are finite activations)
+__device__ __forceinline__ uint32_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ float gelu_tanh(float v) {  // voxtral_kernels.c:505-513
+    float x3 = v * v * v;
+    float inner = 0.7978845608028654f * (v + 0.044715f * x3);
+    return 0.5f * v * (1.0f + tanhf(inner));
+}
+__device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
+__device__ __forceinline__ float silu(float v) { return v / (1.0f + expf(-v)); }  // :498-503
+
+// dot of 8 bf16 weights (one uint4) with 8 f32 activations
+__device__ __forceinline__ float dot8(uint4 w, float4 a, float4 b, float acc) {
+    acc = fmaf(bflo(w.x), a.x, acc);
+    acc = fmaf(bfhi(w.x), a.y, acc);
+    acc = fmaf(bflo(w.y), a.z, acc);
+    acc = fmaf(bfhi(w.y), a.w, acc);
+    acc = fmaf(bflo(w.z), b.x, acc);
+    acc = fmaf(bfhi(w.z), b.y, acc);
+    acc = fmaf(bflo(w.w), b.z, acc);
+    acc = fmaf(bfhi(w.w), b.w, acc);
+    return acc;
+}
+
+// ============================================================================
+// Row-wise RMSNorm (+ optional ada scale), M>1 paths.  voxtral_kernels.c:475-492,
+// voxtral_decoder.c:564-570.  One block per row.
+// ============================================================================
+__global__ __launch_bounds__(256) void k_rmsnorm_rows(const float* __restrict__ x, int ldx,
+                                                      float* __restrict__ y, int ldy,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ ada, int D,
+                                                      float eps) {
+    __shared__ float red[4];
+    const float* xr = x + (size_t)blockIdx.x * ldx;
+    float* yr = y + (size_t)blockIdx.x * ldy;
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < D; i += 256) ss = fmaf(xr[i], xr[i], ss);
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    float tot = red[0] + red[1] + red[2] + red[3];
+    float inv = 1.0f / sqrtf(tot / (float)D + eps);
+    for (int i = threadIdx.x; i < D; i += 256) {
+        float v = xr[i] * inv * w[i];
+        if (ada) v *= (1.0f + ada[i]);
+        yr[i] = v;
+    }
+}
+
+// ============================================================================
+// MFMA GEMM for M>1:  C[M,N] (op)= A[M,K] (f32) * W[N,K]^T (bf16)
+// tile 64x64x32, 256 threads = 4 waves in 2x2, each wave 32x32 = 2x2 16x16 tiles,
+// v_mfma_f32_16x16x32_bf16.  A is split into NSPLIT bf16 terms in the staging pass.
+// ============================================================================
+#define GB_M 64
+#define GB_N 64
+#define GB_K 32
+#define GB_LDS (GB_K + 8)  // padded bf16 row (80 B) to spread ds_read_b128 lanes
+
+template <int EPI, int NSPLIT>
+__global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int lda,
+                                              const uint16_t* __restrict__ W, int K, int M, int N,
+                                              const float* __restrict__ bias,
+                                              float* __restrict__ C, int ldc) {
+    __shared__ __attribute__((aligned(16))) uint16_t sA[NSPLIT][GB_M][GB_LDS];
+    __shared__ __attribute__((aligned(16))) uint16_t sW[GB_N][GB_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int m0 = blockIdx.y * GB_M, n0 = blockIdx.x * GB_N;
+    const int srow = tid >> 2, skq = (tid & 3) * 8;
+
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const bool arow_ok = (m0 + srow) < M;
+    const float* Ap = A + (size_t)(m0 + srow) * lda + skq;
+    const uint16_t* Wp = W + (size_t)(n0 + srow) * K + skq;
+
+    for (int k0 = 0; k0 < K; k0 += GB_K) {
+        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+        if (arow_ok) {
+            a0 = *reinterpret_cast<const float4*>(Ap + k0);
+            a1 = *reinterpret_cast<const float4*>(Ap + k0 + 4);
+        }
+        uint4 wv = *reinterpret_cast<const uint4*>(Wp + k0);
+        __syncthreads();
+        {
+            float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            uint32_t t[NSPLIT][8];
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                float r = v[e];
+#pragma unroll
+                for (int s = 0; s < NSPLIT; s++) {
+                    uint32_t b = f2bf(r);
+                    t[s][e] = b;
+                    r = r - __uint_as_float(b << 16);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < NSPLIT; s++) {
+                uint4 pk;
+                pk.x = t[s][0] | (t[s][1] << 16);
+                pk.y = t[s][2] | (t[s][3] << 16);
+                pk.z = t[s][4] | (t[s][5] << 16);
+                pk.w = t[s][6] | (t[s][7] << 16);
+                *reinterpret_cast<uint4*>(&sA[s][srow][skq]) = pk;
+            }
+            *reinterpret_cast<uint4*>(&sW[srow][skq]) = wv;
+        }
+        __syncthreads();
+        const int fr = lane & 15, fk = (lane >> 4) * 8;
+        bf16x8 bfrag[2];
+#pragma unroll
+        for (int ni = 0; ni < 2; ni++)
+            bfrag[ni] = *reinterpret_cast<const bf16x8*>(&sW[wc * 32 + ni * 16 + fr][fk]);
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++) {
+#pragma unroll
+            for (int s = 0; s < NSPLIT; s++) {
+                bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&sA[s][wr * 32 + mi * 16 + fr][fk]);
+#pragma unroll
+                for (int ni = 0; ni < 2; ni++)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag[ni], acc[mi][ni], 0, 0, 0);
+            }
+        }
+    }
+
+    // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r
+    const int cc = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+    for (int mi = 0; mi < 2; mi++) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int m = m0 + wr * 32 + mi * 16 + rq + r;
+            if (m >= M) continue;
+            if (EPI == EPI_SWIGLU) {
+                // wave's 32 columns = one interleave group: tile 0 = w1 rows, tile 1 = w3 rows
+                const int g = (n0 + wc * 32) >> 5;
+                const int j = g * 16 + cc;
+                C[(size_t)m * ldc + j] = silu(acc[mi][0][r]) * acc[mi][1][r];
+            } else {
+#pragma unroll
+                for (int ni = 0; ni < 2; ni++) {
+                    const int n = n0 + wc * 32 + ni * 16 + cc;
+                    float v = acc[mi][ni][r];
+                    if (bias) v += bias[n];
+                    float* cp = C + (size_t)m * ldc + n;
+                    if (EPI == EPI_STORE) *cp = v;
+                    else if (EPI == EPI_RESID) *cp += v;
+                    else if (EPI == EPI_GELU) *cp = gelu_tanh(v);
+                    else if (EPI == EPI_GELU_ERF) *cp = gelu_erf(v);
+                }
+            }
+        }
+    }
+}
+
+// ============================================================================
+// RoPE + KV append for M>1 rows (voxtral_encoder.c:580-607, voxtral_decoder.c:531-541).
+// qkv [M, qd + 2*kvd] -> q [M, qd] roped; K/V ring slots (pos0 + i) % cap.
+// ============================================================================
+__global__ __launch_bounds__(256) void k_rope_kv(const float* __restrict__ qkv, int M, int qd,
+                                                 int kvd, int hd, const float* __restrict__ rope,
+                                                 int pos0, float* __restrict__ q,
+                                                 float* __restrict__ Kc, float* __restrict__ Vc,
+                                                 int cap) {
+    const int i = blockIdx.x;
+    const int ld = qd + 2 * kvd;
+    const float* row = qkv + (size_t)i * ld;
+    const float* rp = rope + (size_t)i * hd;  // rope rows for rows i (pos0 + i)
+    const int slot = (pos0 + i) % cap;
+    float* kr = Kc + (size_t)slot * kvd;
+    float* vr = Vc + (size_t)slot * kvd;
+    for (int p = threadIdx.x; p < qd / 2; p += 256) {
+        int d = (2 * p) % hd / 2;
+        float c = rp[2 * d], s = rp[2 * d + 1];
+        float x0 = row[2 * p], x1 = row[2 * p + 1];
+        q[(size_t)i * qd + 2 * p] = x0 * c - x1 * s;
+        q[(size_t)i * qd + 2 * p + 1] = x0 * s + x1 * c;
+    }
+    for (int p = threadIdx.x; p < kvd / 2; p += 256) {
+        int d = (2 * p) % hd / 2;
+        float c = rp[2 * d], s = rp[2 * d + 1];
+        float x0 = row[qd + 2 * p], x1 = row[qd + 2 * p + 1];
+        kr[2 * p] = x0 * c - x1 * s;
+        kr[2 * p + 1] = x0 * s + x1 * c;
+    }
+    for (int p = threadIdx.x; p < kvd; p += 256) vr[p] = row[qd + kvd + p];
+}
+
+// ============================================================================
+// Tiled causal/windowed attention for M>1 queries (encoder chunks, decoder prefill).
+// Semantics of vox_causal_attention (voxtral_kernels.c:541-611) with logical positions:
+// query i sits at q_pos0+i and sees keys p with max(k_first, qp-window+1) <= p <= qp.
+// Block = (head, 16 queries); K/V tiles of 64 keys staged in LDS; online softmax.
+// ============================================================================
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q, int ldq,
+                                                    const float* __restrict__ Kc,
+                                                    const float* __restrict__ Vc, int cap,
+                                                    float* __restrict__ O, int ldo, int M, int H,
+                                                    int KVH, int q_pos0, int k_first, int window,
+                                                    float scale) {
+    constexpr int QT = 16, KT = 64, DPT = HD / 16;
+    __shared__ __attribute__((aligned(16))) float sQ[QT][HD];
+    __shared__ __attribute__((aligned(16))) float sK[KT][HD + 4];
+    __shared__ __attribute__((aligned(16))) float sV[KT][HD];
+    __shared__ float sP[QT][KT];
+    const int h = blockIdx.x, q0 = blockIdx.y * QT;
+    const int kvh = h / (H / KVH);
+    const int kvd = KVH * HD;
+    const int nq = min(QT, M - q0);
+    const int tid = threadIdx.x, qi = tid >> 4, j = tid & 15;
+
+    for (int e = tid; e < QT * HD; e += 256) {
+        int r = e / HD, d = e % HD;
+        sQ[r][d] = (r < nq) ? Q[(size_t)(q0 + r) * ldq + h * HD + d] : 0.f;
+    }
+    const int qp = q_pos0 + q0 + qi;
+    const int qfirst = q_pos0 + q0, qlast = q_pos0 + q0 + nq - 1;
+    int kstart = qfirst - window + 1;
+    if (kstart < k_first) kstart = k_first;
+    const int kend = qlast;
+
+    float m = -1e30f, l = 0.f;
+    float o[DPT];
+#pragma unroll
+    for (int e = 0; e < DPT; e++) o[e] = 0.f;
+    const bool qvalid = qi < nq;
+
+    for (int kb = kstart; kb <= kend; kb += KT) {
+        __syncthreads();
+        for (int e = tid; e < KT * (HD / 4); e += 256) {
+            int r = e / (HD / 4), c4 = e % (HD / 4);
+            int kp = kb + r;
+            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+            if (kp <= kend) {
+                size_t off = (size_t)(kp % cap) * kvd + kvh * HD + c4 * 4;
+                kv = *reinterpret_cast<const float4*>(Kc + off);
+                vv = *reinterpret_cast<const float4*>(Vc + off);
+            }
+            *reinterpret_cast<float4*>(&sK[r][c4 * 4]) = kv;
+            *reinterpret_cast<float4*>(&sV[r][c4 * 4]) = vv;
+        }
+        __syncthreads();
+        float s[4];
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            int key = j + 16 * jj;
+            int kp = kb + key;
+            bool valid = qvalid && kp <= qp && kp >= qp - window + 1 && kp >= k_first && kp <= kend;
+            float acc = 0.f;
+#pragma unroll 8
+            for (int d = 0; d < HD; d += 4) {
+                float4 a = *reinterpret_cast<const float4*>(&sQ[qi][d]);
+                float4 b = *reinterpret_cast<const float4*>(&sK[key][d]);
+                acc = fmaf(a.x, b.x, acc);
+                acc = fmaf(a.y, b.y, acc);
+                acc = fmaf(a.z, b.z, acc);
+                acc = fmaf(a.w, b.w, acc);
+            }
+            s[jj] = valid ? acc * scale : -INFINITY;
+            tmax = fmaxf(tmax, s[jj]);
+        }
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, off, 16));
+        const float mnew = fmaxf(m, tmax);
+        float psum = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            float p = (s[jj] == -INFINITY) ? 0.f : expf(s[jj] - mnew);
+            sP[qi][j + 16 * jj] = p;
+            psum += p;
+        }
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) psum += __shfl_xor(psum, off, 16);
+        const float alpha = expf(m - mnew);
+        l = l * alpha + psum;
+        m = mnew;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < DPT; e++) o[e] *= alpha;
+        const int d0 = j * DPT;
+        for (int key = 0; key < KT; key++) {
+            float p = sP[qi][key];
+#pragma unroll
+            for (int e = 0; e < DPT; e += 4) {
+                float4 v = *reinterpret_cast<const float4*>(&sV[key][d0 + e]);
+                o[e] = fmaf(p, v.x, o[e]);
+                o[e + 1] = fmaf(p, v.y, o[e + 1]);
+                o[e + 2] = fmaf(p, v.z, o[e + 2]);
+                o[e + 3] = fmaf(p, v.w, o[e + 3]);
+            }
+        }
+    }
+    if (qvalid) {
+        float inv = l > 0.f ? 1.0f / l : 0.f;
+        float* op = O + (size_t)(q0 + qi) * ldo + h * HD + j * DPT;
+#pragma unroll
+        for (int e = 0; e < DPT; e++) op[e] = o[e] * inv;
+    }
+}
+
+// ============================================================================
+// M=1 weight-streaming GEMV with fused prologue / epilogue (decoder step).
+// Each wave owns units (row pairs) in a grid-stride loop; 16-B bf16 loads straight to
+// VGPRs, x staged once per block in LDS (normalised there when PRO_NORM).
+// ============================================================================
+template <int PRO, int EPI>
+__global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];
+    __shared__ float red[8];
+    __shared__ int redi[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = a.K;
+    const int K4 = K >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(a.x);
+    float4* xs4 = reinterpret_cast<float4*>(xs);
+    float ss = 0.f;
+    for (int i = tid; i < K4; i += 256) {
+        float4 v = x4[i];
+        xs4[i] = v;
+        if (PRO != PRO_NONE) ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, ss))));
+    }
+    if (PRO != PRO_NONE) {
+        ss = wave_sum(ss);
+        if (lane == 0) red[wave] = ss;
+        __syncthreads();
+        const float tot = red[0] + red[1] + red[2] + red[3];
+        const float inv = 1.0f / sqrtf(tot / (float)K + a.eps);
+        for (int i = tid; i < K; i += 256) {
+            float v = xs[i] * inv * a.norm_w[i];
+            if (PRO == PRO_NORM_ADA) v *= (1.0f + a.ada[i]);
+            xs[i] = v;
+        }
+    }
+    __syncthreads();
+
+    int lp = 0;
+    if (EPI == EPI_QKV) lp = a.state ? a.state[0] : a.pos;
+    float best = -INFINITY;
+    int besti = 0x7fffffff;
+
+    const int nunits = a.units;
+    const int K8 = K >> 3;
+    for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
+        int r0, r1;
+        if (EPI == EPI_SWIGLU) {
+            r0 = ((u >> 4) << 5) + (u & 15);
+            r1 = r0 + 16;
+        } else {
+            r0 = 2 * u;
+            r1 = 2 * u + 1;
+        }
+        const uint4* w0 = reinterpret_cast<const uint4*>(a.W + (size_t)r0 * K);
+        const uint4* w1 = reinterpret_cast<const uint4*>(a.W + (size_t)r1 * K);
+        float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll 4
+        for (int c = lane; c < K8; c += 64) {
+            uint4 p0 = ldnt(w0 + c);
+            uint4 p1 = ldnt(w1 + c);
+            float4 xa = xs4[2 * c], xb = xs4[2 * c + 1];
+            acc0 = dot8(p0, xa, xb, acc0);
+            acc1 = dot8(p1, xa, xb, acc1);
+        }
+        acc0 = wave_sum(acc0);
+        acc1 = wave_sum(acc1);
+        if (EPI == EPI_LOGITS) {
+            // first max wins (voxtral_decoder.c:771-779): strictly greater, lower index on ties
+            if (acc0 > best) { best = acc0; besti = r0; }
+            if (acc1 > best) { best = acc1; besti = r1; }
+        }
+        if (lane == 0) {
+            if (EPI == EPI_STORE) {
+                a.y[r0] = acc0 + (a.bias ? a.bias[r0] : 0.f);
+                a.y[r1] = acc1 + (a.bias ? a.bias[r1] : 0.f);
+            } else if (EPI == EPI_RESID) {
+                a.y[r0] += acc0 + (a.bias ? a.bias[r0] : 0.f);
+                a.y[r1] += acc1 + (a.bias ? a.bias[r1] : 0.f);
+            } else if (EPI == EPI_LOGITS) {
+                a.y[r0] = acc0;
+                a.y[r1] = acc1;
+            } else if (EPI == EPI_SWIGLU) {
+                a.y[u] = silu(acc0) * acc1;
+            } else if (EPI == EPI_QKV) {
+                const int hd = a.hd;
+                if (r0 < a.qd + a.kvd) {
+                    const int col = r0 < a.qd ? r0 : r0 - a.qd;
+                    const int d = (col % hd) >> 1;
+                    const float* rp = a.rope + (size_t)lp * hd;
+                    const float c = rp[2 * d], s = rp[2 * d + 1];
+                    const float o0 = acc0 * c - acc1 * s, o1 = acc0 * s + acc1 * c;
+                    if (r0 < a.qd) {
+                        a.y[r0] = o0;
+                        a.y[r1] = o1;
+                    } else {
+                        float* kr = a.Kc + (size_t)(lp % a.cap) * a.kvd;
+                        kr[col] = o0;
+                        kr[col + 1] = o1;
+                    }
+                } else {
+                    const int col = r0 - a.qd - a.kvd;
+                    float* vr = a.Vc + (size_t)(lp % a.cap) * a.kvd;
+                    vr[col] = acc0;
+                    vr[col + 1] = acc1;
+                }
+            }
+        }
+    }
+    if (EPI == EPI_LOGITS) {
+        __syncthreads();
+        if (lane == 0) {
+            red[wave] = best;
+            redi[wave] = besti;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            float bv = red[0];
+            int bi = redi[0];
+            for (int w = 1; w < 4; w++)
+                if (red[w] > bv || (red[w] == bv && redi[w] < bi)) { bv = red[w]; bi = redi[w]; }
+            a.part_val[blockIdx.x] = bv;
+            a.part_idx[blockIdx.x] = bi;
+        }
+    }
+}
+
+// ============================================================================
+// Decode attention (one query per head, GQA), flash-decoding split over keys.
+// Keys: the last min(lp+1, window) logical positions (voxtral_decoder.c:731-733 after
+// compaction, voxtral_kernels.c:554-560).  Partials [H][nsplit][HD+2].
+// ============================================================================
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_decode(const float* __restrict__ q,
+                                                     const float* __restrict__ Kc,
+                                                     const float* __restrict__ Vc, int cap,
+                                                     const int* __restrict__ state, int pos_host,
+                                                     int window, float scale, int H, int KVH,
+                                                     int nsplit, float* __restrict__ part) {
+    constexpr int DPL = HD / 64;  // dims per lane in PV
+    __shared__ __attribute__((aligned(16))) float sQ[4][HD];
+    const int kvh = blockIdx.y, split = blockIdx.x;
+    const int hpk = H / KVH;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kvd = KVH * HD;
+    const int lp = state ? state[0] : pos_host;
+    const int L = min(lp + 1, window);
+    const int first = lp - L + 1;
+    int per = (L + nsplit - 1) / nsplit;
+    per = ((per + 63) / 64) * 64;
+    const int s0 = first + split * per;
+    const int s1 = min(s0 + per, lp + 1);
+    for (int e = tid; e < hpk * HD; e += 256) sQ[e / HD][e % HD] = q[(size_t)(kvh * hpk) * HD + e];
+    __syncthreads();
+    if (wave >= hpk) return;
+    const int h = kvh * hpk + wave;
+    float* pp = part + ((size_t)h * nsplit + split) * (HD + 2);
+    float m = -1e30f, l = 0.f;
+    float o[DPL];
+#pragma unroll
+    for (int e = 0; e < DPL; e++) o[e] = 0.f;
+    for (int kb = s0; kb < s1; kb += 64) {
+        const int kp = kb + lane;
+        const bool valid = kp < s1;
+        float sc = -INFINITY;
+        if (valid) {
+            const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)(kp % cap) * kvd + kvh * HD);
+            float acc = 0.f;
+#pragma unroll 8
+            for (int d4 = 0; d4 < HD / 4; d4++) {
+                float4 kv = kr[d4];
+                float4 qv = *reinterpret_cast<const float4*>(&sQ[wave][d4 * 4]);
+                acc = fmaf(qv.x, kv.x, acc);
+                acc = fmaf(qv.y, kv.y, acc);
+                acc = fmaf(qv.z, kv.z, acc);
+                acc = fmaf(qv.w, kv.w, acc);
+            }
+            sc = acc * scale;
+        }
+        const float tmax = wave_max(sc);
+        const float mnew = fmaxf(m, tmax);
+        const float p = valid ? expf(sc - mnew) : 0.f;
+        const float psum = wave_sum(p);
+        const float alpha = expf(m - mnew);
+        l = l * alpha + psum;
+        m = mnew;
+#pragma unroll
+        for (int e = 0; e < DPL; e++) o[e] *= alpha;
+        const int nk = min(64, s1 - kb);
+        for (int k = 0; k < nk; k++) {
+            const float pk = __shfl(p, k, 64);
+            const float* vr = Vc + (size_t)((kb + k) % cap) * kvd + kvh * HD + lane * DPL;
+            if (DPL == 2) {
+                float2 v = *reinterpret_cast<const float2*>(vr);
+                o[0] = fmaf(pk, v.x, o[0]);
+                o[DPL - 1] = fmaf(pk, v.y, o[DPL - 1]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < DPL; e++) o[e] = fmaf(pk, vr[e], o[e]);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < DPL; e++) pp[lane * DPL + e] = o[e];
+    if (lane == 0) {
+        pp[HD] = m;
+        pp[HD + 1] = l;
+    }
+}
+
+template <int HD>
+__global__ __launch_bounds__(HD) void k_attn_combine(const float* __restrict__ part, int nsplit,
+                                                     float* __restrict__ out) {
+    const int h = blockIdx.x, d = threadIdx.x;
+    const float* ph = part + (size_t)h * nsplit * (HD + 2);
+    float M = -1e30f;
+    for (int s = 0; s < nsplit; s++) M = fmaxf(M, ph[(size_t)s * (HD + 2) + HD]);
+    float num = 0.f, den = 0.f;
+    for (int s = 0; s < nsplit; s++) {
+        const float* p = ph + (size_t)s * (HD + 2);
+        const float ls = p[HD + 1];
+        if (ls == 0.f) continue;
+        const float f = expf(p[HD] - M);
+        num = fmaf(f, p[d], num);
+        den = fmaf(f, ls, den);
+    }
+    out[(size_t)h * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
+}
+
+// ============================================================================
+// Step input: x = adapter[gen] + bf16->f32(tok_emb[prev]) (voxtral.c:1106-1113)
+// ============================================================================
+__global__ __launch_bounds__(256) void k_embed_step(const float* __restrict__ adapter,
+                                                    const uint16_t* __restrict__ emb,
+                                                    const int* __restrict__ state, int D,
+                                                    float* __restrict__ x) {
+    const int gi = state[1], tok = state[2];
+    const float* a = adapter + (size_t)gi * D;
+    const uint16_t* e = emb + (size_t)tok * D;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < D; i += gridDim.x * 256) x[i] = a[i] + bf2f(e[i]);
+}
+
+// prompt embeds for prefill rows (voxtral.c:1039-1048): token = BOS for logical row 0
+__global__ __launch_bounds__(256) void k_embed_rows(const float* __restrict__ adapter,
+                                                    const uint16_t* __restrict__ emb, int row0,
+                                                    int first_tok, int rest_tok, int D,
+                                                    float* __restrict__ x) {
+    const int r = blockIdx.x;
+    const int tok = (row0 + r == 0) ? first_tok : rest_tok;
+    const float* a = adapter + (size_t)(row0 + r) * D;
+    const uint16_t* e = emb + (size_t)tok * D;
+    for (int i = threadIdx.x; i < D; i += 256) x[(size_t)r * D + i] = a[i] + bf2f(e[i]);
+}
+
+// Final argmax over per-block partials; advance the device-side step state:
+// state = {logical kv pos, next adapter row, prev token, step index}
+__global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ pv,
+                                                      const int* __restrict__ pi, int n,
+                                                      int* __restrict__ state,
+                                                      int* __restrict__ tokens, int tokens_cap) {
+    __shared__ float sv[256];
+    __shared__ int si[256];
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        float v = pv[i];
+        int id = pi[i];
+        if (v > bv || (v == bv && id < bi)) { bv = v; bi = id; }
+    }
+    sv[threadIdx.x] = bv;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            float v = sv[threadIdx.x + s];
+            int id = si[threadIdx.x + s];
+            if (v > sv[threadIdx.x] || (v == sv[threadIdx.x] && id < si[threadIdx.x])) {
+                sv[threadIdx.x] = v;
+                si[threadIdx.x] = id;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int tok = si[0];
+        if (tok == 0x7fffffff) tok = 0;
+        int step = state[3];
+        if (tokens && step < tokens_cap) tokens[step] = tok;
+        state[0] += 1;
+        state[1] += 1;
+        state[2] = tok;
+        state[3] = step + 1;
+    }
+}
+
+// im2col for the causal conv stem (voxtral_kernels.c:430-447):
+// A[t][ic*3 + k] = src[(stride*t + off + k) * C + ic]
+__global__ __launch_bounds__(256) void k_im2col3(const float* __restrict__ src, int C, int T,
+                                                 int stride, int off, float* __restrict__ A) {
+    const int t = blockIdx.x;
+    const int KK = C * 3;
+    for (int e = threadIdx.x; e < KK; e += 256) {
+        int ic = e / 3, k = e % 3;
+        A[(size_t)t * KK + e] = src[(size_t)(stride * t + off + k) * C + ic];
+    }
+}
+
+// mel tail update with the reference's quirk for 1-frame chunks (voxtral.c:637-643):
+// tail = last two frames, or [0, only] when the chunk had a single frame.
+__global__ void k_mel_tail(const float* __restrict__ melp, int n_new, int MB, float* __restrict__ tail) {
+    // melp points at the [tail(2) + new] buffer; tail is its first two rows
+    for (int b = threadIdx.x; b < MB; b += blockDim.x) {
+        float t0, t1;
+        if (n_new >= 2) {
+            t0 = melp[(size_t)(2 + n_new - 2) * MB + b];
+            t1 = melp[(size_t)(2 + n_new - 1) * MB + b];
+        } else {
+            t0 = 0.f;
+            t1 = melp[(size_t)(2 + n_new - 1) * MB + b];
+        }
+        tail[b] = t0;
+        tail[MB + b] = t1;
+    }
+}
+
+// ============================================================================
+// Host-side launchers
+// ============================================================================
+#define LAUNCH_CHECK() \
+    do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return e__; } while (0)
+
+hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,
+                               const float* ada, int M, int D, float eps, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rmsnorm_rows, dim3(M), dim3(256), 0, st, x, ldx, y, ldy, w, ada, D, eps);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+template <int EPI, int NS>
+static hipError_t gemm_t(const float* A, int lda, const uint16_t* W, int K, int M, int N,
+                         const float* bias, float* C, int ldc, hipStream_t st) {
+    dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M);
+    hipLaunchKernelGGL((k_gemm<EPI, NS>), grid, dim3(256), 0, st, A, lda, W, K, M, N, bias, C, ldc);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const uint16_t* W, int K,
+                       int M, int N, const float* bias, float* C, int ldc, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (N % GB_N || K % GB_K || lda % 4) return hipErrorInvalidValue;
+#define GEMM_CASE(E, S) \
+    if (epi == E && nsplit == S) return gemm_t<E, S>(A, lda, W, K, M, N, bias, C, ldc, st);
+    GEMM_CASE(EPI_STORE, 1) GEMM_CASE(EPI_STORE, 2) GEMM_CASE(EPI_STORE, 3)
+    GEMM_CASE(EPI_RESID, 1) GEMM_CASE(EPI_RESID, 2) GEMM_CASE(EPI_RESID, 3)
+    GEMM_CASE(EPI_GELU, 1) GEMM_CASE(EPI_GELU, 2) GEMM_CASE(EPI_GELU, 3)
+    GEMM_CASE(EPI_GELU_ERF, 1) GEMM_CASE(EPI_GELU_ERF, 2) GEMM_CASE(EPI_GELU_ERF, 3)
+    GEMM_CASE(EPI_SWIGLU, 1) GEMM_CASE(EPI_SWIGLU, 2) GEMM_CASE(EPI_SWIGLU, 3)
+#undef GEMM_CASE
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, const float* rope,
+                          int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rope_kv, dim3(M), dim3(256), 0, st, qkv, M, qd, kvd, hd, rope, pos0, q, Kc, Vc, cap);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
+                             int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
+                             int k_first, int window, float scale, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    dim3 grid(H, (M + 15) / 16);
+    if (hd == 64)
+        hipLaunchKernelGGL(k_attn_tiled<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0, k_first, window, scale);
+    else if (hd == 128)
+        hipLaunchKernelGGL(k_attn_tiled<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0, k_first, window, scale);
+    else
+        return hipErrorInvalidValue;
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+int gemv_grid(int units) {
+    int g = (units + 3) / 4;
+    if (g > GEMV_MAX_BLOCKS) g = GEMV_MAX_BLOCKS;
+    return g < 1 ? 1 : g;
+}
+
+hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
+    const int grid = gemv_grid(a.units);
+    const size_t lds = (size_t)a.K * sizeof(float);
+    if (a.K % 8) return hipErrorInvalidValue;
+#define GEMV_CASE(P, E) \
+    if (pro == P && epi == E) { hipLaunchKernelGGL((k_gemv<P, E>), dim3(grid), dim3(256), lds, st, a); LAUNCH_CHECK(); return hipSuccess; }
+    GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_STORE)
+    GEMV_CASE(PRO_NORM, EPI_QKV) GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_SWIGLU)
+    GEMV_CASE(PRO_NONE, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS) GEMV_CASE(PRO_NONE, EPI_LOGITS)
+    GEMV_CASE(PRO_NONE, EPI_QKV)
+#undef GEMV_CASE
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
+                              const int* state, int pos_host, int window, float scale, int H,
+                              int KVH, int nsplit, float* part, float* out, hipStream_t st) {
+    dim3 grid(nsplit, KVH);
+    if (H / KVH > 4) return hipErrorInvalidValue;
+    if (hd == 128) {
+        hipLaunchKernelGGL(k_attn_decode<128>, grid, dim3(256), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, nsplit, part);
+        LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_attn_combine<128>, dim3(H), dim3(128), 0, st, part, nsplit, out);
+    } else if (hd == 64) {
+        hipLaunchKernelGGL(k_attn_decode<64>, grid, dim3(256), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, nsplit, part);
+        LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_attn_combine<64>, dim3(H), dim3(64), 0, st, part, nsplit, out);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_embed_step(const float* adapter, const uint16_t* emb, const int* state, int D,
+                             float* x, hipStream_t st) {
+    hipLaunchKernelGGL(k_embed_step, dim3((D + 255) / 256), dim3(256), 0, st, adapter, emb, state, D, x);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_embed_rows(const float* adapter, const uint16_t* emb, int row0, int n,
+                             int first_tok, int rest_tok, int D, float* x, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_embed_rows, dim3(n), dim3(256), 0, st, adapter, emb, row0, first_tok, rest_tok, D, x);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
+                               int cap, hipStream_t st) {
+    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, pv, pi, n, state, tokens, cap);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
+                          hipStream_t st) {
+    if (T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_im2col3, dim3(T), dim3(256), 0, st, src, C, T, stride, off, A);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st) {
+    hipLaunchKernelGGL(k_mel_tail, dim3(1), dim3(128), 0, st, melp, n_new, MB, tail);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+}  // namespace vox

@@ -1,0 +1,291 @@
+"""Python host-side mirror of the voxtral.c streaming API over the MI355X backend.
+
+Loads libvoxtral_hip.so (built in-tree by __graft_entry__.build()) and exposes the same
+objects the reference's C API has (voxtral.h:251-337): a model loaded once, streams fed
+incrementally, greedy token ids out.  The mel front-end stays on the host and is not
+part of this package (out of scope); streams are fed log-mel frames.
+
+There is no CPU fallback: if the HIP library or a GPU is missing every entry point
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from vox_weights import (VoxConfig, Weights, build_weights_struct, config_struct_class,
+                         weights_struct_class)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvoxtral_hip.so")
+
+TOKEN_BOS, TOKEN_EOS, TOKEN_STREAMING_PAD = 1, 2, 32
+STREAM_FIRST_CHUNK_MIN_MEL = 312          # voxtral.c:405
+STREAM_DEFAULT_INTERVAL = 2.0             # voxtral.c:408
+RAW_AUDIO_LENGTH_PER_TOK = 1280           # voxtral.c:400
+OFFLINE_STREAMING_BUFFER_TOKENS = 10      # voxtral.c:401
+
+ConfigC = config_struct_class()
+WeightsC = weights_struct_class()
+
+# exported symbols, as declared in include/voxtral_hip.h
+EXPORTS = [
+    "vox_hip_init", "vox_hip_available", "vox_hip_shutdown", "vox_hip_memory_used",
+    "vox_hip_last_error", "vox_hip_set_device", "vox_hip_config_voxtral_4b",
+    "vox_hip_model_create", "vox_hip_model_free", "vox_hip_model_set_delay",
+    "vox_hip_model_ada_scale", "vox_hip_stream_create", "vox_hip_stream_free",
+    "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
+    "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
+    "vox_hip_stream_state", "vox_hip_sgemm_bf16", "vox_hip_fused_qkv_bf16",
+    "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
+    "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
+    "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
+    "vox_hip_stream_sync",
+]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fp = ctypes.POINTER(ctypes.c_float)
+    ip = ctypes.POINTER(ctypes.c_int)
+    sig = {
+        "vox_hip_init": (I, []), "vox_hip_available": (I, []), "vox_hip_shutdown": (None, []),
+        "vox_hip_memory_used": (ctypes.c_size_t, []), "vox_hip_last_error": (ctypes.c_char_p, []),
+        "vox_hip_set_device": (I, [I]),
+        "vox_hip_config_voxtral_4b": (None, [P]),
+        "vox_hip_model_create": (P, [P, P, I]), "vox_hip_model_free": (None, [P]),
+        "vox_hip_model_set_delay": (I, [P, I]), "vox_hip_model_ada_scale": (I, [P, fp]),
+        "vox_hip_stream_create": (P, [P]), "vox_hip_stream_free": (None, [P]),
+        "vox_hip_stream_reset": (I, [P]), "vox_hip_stream_reset_decoder": (I, [P]),
+        "vox_hip_stream_encode_mel": (I, [P, P, I, I]),
+        "vox_hip_stream_adapter_tokens": (I, [P]),
+        "vox_hip_stream_read_adapter": (I, [P, I, I, fp]),
+        "vox_hip_stream_decode": (I, [P, I, I, ip, fp]),
+        "vox_hip_stream_state": (I, [P, ip]),
+        "vox_hip_sgemm_bf16": (None, [I, I, I, fp, P, fp]),
+        "vox_hip_fused_qkv_bf16": (None, [I, I, fp, P, I, P, I, P, I, fp, fp, fp]),
+        "vox_hip_fused_ffn_bf16": (None, [I, I, I, fp, P, P, P, fp]),
+        "vox_hip_encoder_attention": (None, [fp, fp, fp, fp, I, I, I, I, I, F, I, I]),
+        "vox_hip_encoder_full_step": (I, [P, fp, I, fp, I]),
+        "vox_hip_decoder_prefill_step": (I, [P, fp, I, fp, I]),
+        "vox_hip_decoder_start": (None, [P, fp, I]), "vox_hip_decoder_end": (None, [P]),
+        "vox_hip_decoder_full_step": (I, [P, fp, I, fp]),
+        "vox_hip_stream_set_profiling": (I, [P, I]),
+        "vox_hip_stream_profile": (I, [P, ctypes.POINTER(ctypes.c_double)]),
+        "vox_hip_stream_sync": (I, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def fptr(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _err(what):
+    msg = lib().vox_hip_last_error()
+    raise RuntimeError(f"{what}: {msg.decode() if msg else 'unknown error'}")
+
+
+def init(device: int | None = None):
+    L = lib()
+    if device is not None and L.vox_hip_set_device(device) != 0:
+        _err("set_device")
+    if not L.vox_hip_init():
+        _err("vox_hip_init (no GPU?)")
+
+
+class Model:
+    """vox_load (voxtral.c:131-383) for the HIP backend: weights uploaded once into HBM."""
+
+    def __init__(self, cfg: VoxConfig, weights: Weights, delay_tokens: int = 6):
+        init()
+        self.cfg = cfg
+        self.delay_tokens = delay_tokens
+        self._cfg_c = cfg.ctypes_struct(ConfigC)
+        wstruct, keep = build_weights_struct(weights, WeightsC)
+        self.h = lib().vox_hip_model_create(ctypes.byref(self._cfg_c), ctypes.byref(wstruct), delay_tokens)
+        if not self.h:
+            _err("vox_hip_model_create")
+
+    def set_delay(self, delay_ms: int):
+        """vox_set_delay (voxtral.c:1681-1687)"""
+        delay_ms = min(max(delay_ms, 80), 2400)
+        self.delay_tokens = delay_ms // 80
+        if lib().vox_hip_model_set_delay(self.h, self.delay_tokens) != 0:
+            _err("set_delay")
+
+    def ada_scale(self):
+        c = self.cfg
+        out = np.empty(c.dec_layers * c.dec_dim, np.float32)
+        lib().vox_hip_model_ada_scale(self.h, fptr(out))
+        return out.reshape(c.dec_layers, c.dec_dim)
+
+    def close(self):
+        if self.h:
+            lib().vox_hip_model_free(self.h)
+            self.h = None
+
+
+class Stream:
+    """Per-stream device state (rolling KV, conv tails, adapter buffer) + decode loop."""
+
+    def __init__(self, model: Model):
+        self.model = model
+        self.cfg = model.cfg
+        self.h = lib().vox_hip_stream_create(model.h)
+        if not self.h:
+            _err("vox_hip_stream_create")
+
+    def reset(self):
+        if lib().vox_hip_stream_reset(self.h) != 0:
+            _err("reset")
+
+    def encode_mel(self, mel: np.ndarray) -> int:
+        mel = np.ascontiguousarray(mel, dtype=np.float32)
+        assert mel.ndim == 2 and mel.shape[1] == self.cfg.mel_bins
+        n = lib().vox_hip_stream_encode_mel(self.h, mel.ctypes.data, mel.shape[0], 0)
+        if n < 0:
+            _err("encode_mel")
+        return n
+
+    def encode_mel_device(self, dev_ptr: int, n_frames: int) -> int:
+        n = lib().vox_hip_stream_encode_mel(self.h, ctypes.c_void_p(dev_ptr), n_frames, 1)
+        if n < 0:
+            _err("encode_mel")
+        return n
+
+    @property
+    def adapter_tokens(self) -> int:
+        return lib().vox_hip_stream_adapter_tokens(self.h)
+
+    def read_adapter(self, first: int = 0, n: int | None = None) -> np.ndarray:
+        if n is None:
+            n = self.adapter_tokens - first
+        out = np.empty((n, self.cfg.dec_dim), np.float32)
+        if n and lib().vox_hip_stream_read_adapter(self.h, first, n, fptr(out)) != 0:
+            _err("read_adapter")
+        return out
+
+    def decode(self, max_steps: int = 1 << 30, stop_at_eos: bool = True, want_logits: bool = False):
+        max_steps = min(max_steps, 1 << 20)
+        cap = min(max_steps, max(self.adapter_tokens + 1, 1))
+        toks = np.zeros(cap, np.int32)
+        logits = np.zeros((cap, self.cfg.vocab), np.float32) if want_logits else None
+        n = lib().vox_hip_stream_decode(self.h, cap, int(stop_at_eos),
+                                        toks.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                        fptr(logits) if want_logits else None)
+        if n < 0:
+            _err("decode")
+        return (toks[:n], logits[:n]) if want_logits else toks[:n]
+
+    def state(self):
+        o = np.zeros(6, np.int32)
+        lib().vox_hip_stream_state(self.h, o.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        return dict(zip(["kv_pos", "gen_pos", "prev_token", "started", "eos_seen", "generated"], o.tolist()))
+
+    def set_profiling(self, on: bool):
+        lib().vox_hip_stream_set_profiling(self.h, int(on))
+
+    def profile(self):
+        o = (ctypes.c_double * 8)()
+        lib().vox_hip_stream_profile(self.h, o)
+        return {"ms": o[0], "bytes": o[1], "launches": int(o[2]), "avg_ms": o[3]}
+
+    def sync(self):
+        lib().vox_hip_stream_sync(self.h)
+
+    def close(self):
+        if self.h:
+            lib().vox_hip_stream_free(self.h)
+            self.h = None
+
+
+class Session:
+    """vox_stream_t's chunk scheduling over log-mel input (voxtral.c:827-851, 1242-1316,
+    1640-1667).  The caller supplies the mel frames produced so far (vox_mel_feed /
+    vox_mel_finish output); the session decides when the encoder runs and drains the
+    decoder, exactly as stream_run_encoder / stream_run_decoder do."""
+
+    def __init__(self, stream: Stream, interval_s: float = STREAM_DEFAULT_INTERVAL):
+        self.s = stream
+        self.mel_cursor = 0
+        self.conv_started = False
+        self.finished = False
+        self.min_new_mel = max(1, int(interval_s * 100.0))
+        self.tokens: list[int] = []
+        self.chunks: list[int] = []
+
+    def _run_encoder(self, mel_all: np.ndarray, min_new: int):
+        total = mel_all.shape[0]
+        new = total - self.mel_cursor
+        need = STREAM_FIRST_CHUNK_MIN_MEL if not self.conv_started else min_new
+        if new < need and not self.finished:
+            return
+        if new <= 0:
+            return
+        self.chunks.append(new)
+        self.s.encode_mel(mel_all[self.mel_cursor:total])
+        self.conv_started = True
+        self.mel_cursor = total
+
+    def _run_decoder(self, stop_at_eos=True):
+        self.tokens += self.s.decode(stop_at_eos=stop_at_eos).tolist()
+
+    def feed(self, mel_all: np.ndarray, stop_at_eos=True):
+        """vox_stream_feed after vox_mel_feed produced mel_all (all frames so far)."""
+        self._run_encoder(mel_all, self.min_new_mel)
+        self._run_decoder(stop_at_eos)
+
+    def flush(self, mel_all: np.ndarray, stop_at_eos=True):
+        """vox_stream_flush (mel_all includes the right-pad frames)."""
+        self._run_encoder(mel_all, 1)
+        self._run_decoder(stop_at_eos)
+
+    def finish(self, mel_all: np.ndarray, stop_at_eos=True):
+        """vox_stream_finish's final pass after vox_mel_finish."""
+        self.finished = True
+        self._run_encoder(mel_all, self.min_new_mel)
+        self._run_decoder(stop_at_eos)
+
+
+def right_pad_samples(n_real_samples: int, delay_tokens: int) -> int:
+    """vox_stream_flush padding (voxtral.c:1645-1649)."""
+    align = (RAW_AUDIO_LENGTH_PER_TOK - (n_real_samples % RAW_AUDIO_LENGTH_PER_TOK)) % RAW_AUDIO_LENGTH_PER_TOK
+    return align + ((delay_tokens + 1) + OFFLINE_STREAMING_BUFFER_TOKENS) * RAW_AUDIO_LENGTH_PER_TOK
+
+
+# ---------------------------------------------------------------------------
+# reference-boundary twins (voxtral_metal.h), host arrays in / out
+# ---------------------------------------------------------------------------
+def sgemm_bf16(A: np.ndarray, B_bf16: np.ndarray) -> np.ndarray:
+    A = np.ascontiguousarray(A, np.float32)
+    M, K = A.shape
+    N = B_bf16.shape[0]
+    C = np.empty((M, N), np.float32)
+    lib().vox_hip_sgemm_bf16(M, N, K, fptr(A), B_bf16.ctypes.data, fptr(C))
+    return C
+
+
+def encoder_attention(Q, K, V, n_heads, n_kv_heads, head_dim, window, q_offset):
+    Q, K, V = (np.ascontiguousarray(x, np.float32) for x in (Q, K, V))
+    out = np.empty_like(Q)
+    lib().vox_hip_encoder_attention(fptr(out), fptr(Q), fptr(K), fptr(V), Q.shape[0], K.shape[0],
+                                    n_heads, n_kv_heads, head_dim, float(1.0 / np.sqrt(head_dim)),
+                                    window, q_offset)
+    return out

@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: decoder tokens/s + encoder RTF, Voxtral-Mini-4B-Realtime bf16 on MI355X.
+
+Workload (BASELINE.json configs[1], "single stream, batch encoder + greedy decode"):
+one `vox_transcribe_audio` pass over an 11.0 s clip shaped exactly like the reference's
+samples/jfk.wav run -- encoder chunks of 1355, 140 and 1 mel frames (one-shot feed,
+flush padding, vox_mel_finish; voxtral.c:1388-1401, 1640-1667), a 38-row decoder
+prefill and 148 further greedy steps (149 tokens, as the reference CPU run in
+BASELINE.md section 2).  A bench "step" is one such transcription.  Weights are seeded
+random values of the exact architecture (no checkpoint offline) and the log-mel input is
+synthetic; both are resident in HBM before timing.  Greedy decoding runs the full 149
+steps regardless of EOS so the work per step is fixed.
+
+Metric: value = decoder tokens/s summed over ranks (prefill excluded, as voxtral.c:
+1363-1368 reports it) = total greedy steps / max over ranks of decode time.
+encoder_rtf = encoder time / audio time (conv stem + encoder + adapter, voxtral.c:842-940).
+
+Multi-GPU: one process per GPU (torch.distributed.run), each an independent replica with
+its own stream (streams shard embarrassingly, SURVEY.md 8e: no collective on the data
+path); gloo carries only the barrier and the max-over-ranks timing.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "voxtral.c_amd"))
+
+import numpy as np  # noqa: E402
+
+JFK_CHUNKS = [1355, 140, 1]      # mel frames per encoder call
+AUDIO_SECONDS = 176000 / 16000.0  # samples/jfk.wav
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+MPS_TOK_S = 1000.0 / 23.5        # M3 Max MPS decoder step, short clip (README.md:323)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed transcriptions")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=8, help="oracle decode steps in the CPU sample")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self, n):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            self.torch, self.dist = torch, dist
+            dist.init_process_group("gloo")
+
+    def barrier(self):
+        if self.torch is not None:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.torch is None:
+            return x
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if self.torch is None:
+            return x
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def transcribe(st, mel_dev, n_mel):
+    """One vox_transcribe_audio-shaped pass; returns per-phase wall times (s)."""
+    st.reset()
+    t0 = time.perf_counter()
+    off = 0
+    for n in JFK_CHUNKS:
+        st.encode_mel_device(mel_dev.ptr + off * n_mel * 4, n)
+        off += n
+    t1 = time.perf_counter()
+    first = st.decode(max_steps=1, stop_at_eos=False)
+    t2 = time.perf_counter()
+    rest = st.decode(stop_at_eos=False)
+    t3 = time.perf_counter()
+    return {"enc": t1 - t0, "prefill": t2 - t1, "steps": len(rest), "step_s": t3 - t2,
+            "tokens": np.concatenate([first, rest])}
+
+
+def cpu_baseline(cfg, weights, mel, n_steps):
+    """The CPU restatement (oracle/, the reference's algorithm) timed on this host on a
+    bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import vox_oracle
+    threads = min(16, os.cpu_count() or 1)
+    om = vox_oracle.OracleModel(cfg, weights)
+    st = vox_oracle.OracleStream(om)
+    vox_oracle.set_threads(threads)        # sgemm threads for the M>1 encoder/prefill
+    t0 = time.perf_counter()
+    off = 0
+    for n in JFK_CHUNKS:
+        st.encode_mel(mel[off:off + n])
+        off += n
+    t1 = time.perf_counter()
+    st.decode(max_steps=1, stop_at_eos=False)   # prefill + first token
+    vox_oracle.set_threads(1)              # the reference decode GEMV is single-threaded
+    t2 = time.perf_counter()
+    st.decode(max_steps=n_steps, stop_at_eos=False)
+    t3 = time.perf_counter()
+    st.close()
+    om.close()
+    ms_step = (t3 - t2) * 1000.0 / n_steps
+    return {"value": round(1000.0 / ms_step, 3), "unit": "tokens/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/ CPU restatement, full Voxtral-4B shapes: {n_steps} greedy decode "
+                       f"steps after the 38-row prefill (single-threaded bf16 GEMV as "
+                       f"voxtral_kernels.c:154-195); encoder = the 3 jfk chunks with "
+                       f"{threads}-thread OpenBLAS sgemm"),
+            "ms_per_token": round(ms_step, 2),
+            "encoder_rtf": round((t1 - t0) / AUDIO_SECONDS, 4),
+            "encoder_threads": threads}
+
+
+def main():
+    args = parse()
+    d = Dist(args.gpus)
+    import vox_hip
+    from vox_weights import VOXTRAL_4B, synth_weights
+    vox_hip.init(device=d.local)
+    cfg = VOXTRAL_4B
+
+    w = synth_weights(cfg, seed=args.seed)
+    model = vox_hip.Model(cfg, w)
+    keep_host = d.rank == 0 and d.world == 1 and not args.no_cpu_baseline
+    if not keep_host:
+        del w
+        w = None
+    st = vox_hip.Stream(model)
+    rng = np.random.default_rng(1234 + d.rank)
+    mel = rng.uniform(-0.6, 1.4, size=(sum(JFK_CHUNKS), cfg.mel_bins)).astype(np.float32)
+    mel_dev = vox_hip.DeviceArray(mel)
+
+    for _ in range(args.warmup):
+        transcribe(st, mel_dev, cfg.mel_bins)
+
+    st.set_profiling(True)   # HIP events around the W1|W3 GEMV on the stream's own queue
+    runs = []
+    d.barrier()
+    st.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runs.append(transcribe(st, mel_dev, cfg.mel_bins))
+    st.sync()
+    t1 = time.perf_counter()
+    d.barrier()
+    prof = st.profile()
+    st.set_profiling(False)
+
+    wall = d.max(t1 - t0)
+    steps_local = sum(r["steps"] for r in runs)
+    dec_s = d.max(sum(r["step_s"] for r in runs))
+    steps_all = d.sum(steps_local)
+    enc_s = d.max(sum(r["enc"] for r in runs))
+    prefill_s = d.max(sum(r["prefill"] for r in runs))
+    tok_s = steps_all / dec_s
+
+    # roofline of the dominant kernel: the fused RMSNorm*(1+ada) -> W1|W3 GEMV -> SiLU*up
+    # (26 launches per token, 43% of the decode bytes; DESIGN.md "Roofline")
+    D, H = cfg.dec_dim, cfg.dec_hidden
+    w13_bytes = 2 * H * D * 2 + D * 4 * 3 + H * 4   # bf16 W1|W3 + x, norm w, ada in + gate out
+    avg_ms = prof["avg_ms"] if prof["launches"] else float("nan")
+    achieved = w13_bytes / (avg_ms * 1e-3) / 1e9 if prof["launches"] else None
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_w13_traffic.json")
+    if os.path.exists(pmc):
+        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+
+    out = {
+        "metric": "decoder tokens/sec + encoder RTF, Voxtral-4B bf16 at 1/2/4/8 MI355X",
+        "value": round(tok_s, 2),
+        "unit": "tokens/s",
+        "n_gpus": d.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall * 1000.0 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(tok_s / d.world / MPS_TOK_S, 2),
+        "vs_baseline_ref": "per-GPU tok/s vs 42.6 tok/s, Apple M3 Max MPS, README.md:323 (BASELINE.md 1)",
+        "dtype": "f32",
+        "weights_dtype": "bf16",
+        "data": "synthetic (seeded random weights of the exact architecture; synthetic log-mel)",
+        "config": {"workload": "jfk.wav one-shot transcription shape: 1355/140/1-frame encoder "
+                               "chunks, 38-row prefill, 148 greedy steps",
+                   "model": "Voxtral-Mini-4B-Realtime", "global_batch": d.world, "seq_len": 149,
+                   "streams_per_gpu": 1, "parallelism": f"replicas x{d.world} (no collective)"},
+        "encoder_rtf": round(enc_s / (AUDIO_SECONDS * args.steps), 5),
+        "prefill_ms": round(prefill_s * 1000.0 / args.steps, 3),
+        "decoder_ms_per_token": round(dec_s * 1000.0 / max(1, steps_local), 4),
+        "roofline": {"bound": "hbm", "kernel": "k_gemv<PRO_NORM_ADA,EPI_SWIGLU> (W1|W3)",
+                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic, "bytes_per_launch": w13_bytes,
+                     "avg_launch_us": round(avg_ms * 1000.0, 3) if prof["launches"] else None,
+                     "launches_timed": prof["launches"]},
+    }
+    if keep_host:
+        out["cpu_baseline"] = cpu_baseline(cfg, w, mel, args.cpu_steps)
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    mel_dev.free()
+    st.close()
+    model.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -171,6 +171,10 @@ int vox_hip_stream_profile(vox_hip_stream_t *s, double *out8);
 /* Synchronise the stream's HIP queue. */
 int vox_hip_stream_sync(vox_hip_stream_t *s);
 
+/* Device buffers for callers that keep their inputs resident in HBM (benchmark, tests). */
+void *vox_hip_device_upload(const void *host, size_t bytes);
+int vox_hip_device_free(void *dev);
+
 #ifdef __cplusplus
 }
 #endif

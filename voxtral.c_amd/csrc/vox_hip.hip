@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <stddef.h>
 #include <algorithm>
 #include <mutex>
 #include <string>
@@ -376,6 +377,7 @@ static const int NSPLIT_ATT = 32;     // decode attention key splits
 static const int STEP_BATCH = 16;     // graph replays between EOS checks
 
 struct vox_hip_stream {
+    vox_hip_stream() { memset((void*)this, 0, offsetof(vox_hip_stream, pev)); }
     vox_hip_model_t* m;
     hipStream_t st;
     // rolling KV caches [layers][cap][kv_dim]
@@ -405,7 +407,9 @@ struct vox_hip_stream {
     int h_state[4];
     // profiling
     int profiling;
+    int graph_prof;               // the captured step graph carries event-record nodes
     hipEvent_t evt[2];
+    std::vector<hipEvent_t> pev;  // [2*dec_layers] around each W1|W3 GEMV in the graph
     double prof_ms, prof_bytes;
     long long prof_launches;
 };
@@ -464,7 +468,6 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s);
 
 extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     vox_hip_stream_t* s = new vox_hip_stream_t();
-    memset(s, 0, sizeof *s);
     s->m = m;
     const vox_hip_config_t& c = m->c;
     auto fail = [&]() -> vox_hip_stream_t* { vox_hip_stream_free(s); return nullptr; };
@@ -516,6 +519,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->tokens);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
+    for (hipEvent_t e : s->pev) hipEventDestroy(e);
     if (s->st) hipStreamDestroy(s->st);
     delete s;
 }
@@ -742,8 +746,11 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         memset(&a, 0, sizeof a);
         a.x = s->xd; a.K = DD; a.W = L.w13; a.units = DH; a.norm_w = L.ffn_norm;
         a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
+        const bool gprof = s->profiling && state && (int)s->pev.size() == 2 * c.dec_layers;
+        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l], st, hipEventRecordExternal));
         if (s->profiling && !state) CK(hipEventRecord(s->evt[0], st));
         CK(launch_gemv(PRO_NORM_ADA, EPI_SWIGLU, a, st));
+        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l + 1], st, hipEventRecordExternal));
         if (s->profiling && !state) {
             CK(hipEventRecord(s->evt[1], st));
             CK(hipEventSynchronize(s->evt[1]));
@@ -776,6 +783,10 @@ static int enqueue_graph_step(vox_hip_stream_t* s) {
 }
 
 static int build_step_graph(vox_hip_stream_t* s) {
+    if (s->profiling && s->pev.empty()) {
+        s->pev.resize(2 * s->m->c.dec_layers);
+        for (auto& e : s->pev) CK(hipEventCreate(&e));
+    }
     if (s->step_exec) {
         hipGraphExecDestroy(s->step_exec);
         s->step_exec = nullptr;
@@ -792,24 +803,46 @@ static int build_step_graph(vox_hip_stream_t* s) {
     hipGraphDestroy(g);
     if (e != hipSuccess) return set_err("graph instantiate failed: %s", hipGetErrorString(e));
     s->graph_ready = 1;
+    s->graph_prof = s->profiling;
+    return 0;
+}
+
+// Sampled kernel timing: after a batch of replays, the event pair around each layer's
+// W1|W3 GEMV holds the last replay's duration on the stream the kernel ran on.
+static int collect_graph_profile(vox_hip_stream_t* s) {
+    if (!s->profiling || !s->graph_prof) return 0;
+    const vox_hip_config_t& c = s->m->c;
+    for (int l = 0; l < c.dec_layers; l++) {
+        float ms = 0.f;
+        CK(hipEventElapsedTime(&ms, s->pev[2 * l], s->pev[2 * l + 1]));
+        s->prof_ms += ms;
+        s->prof_bytes += (double)2 * c.dec_hidden * c.dec_dim * 2;
+        s->prof_launches++;
+    }
     return 0;
 }
 
 static int run_steps(vox_hip_stream_t* s, int n) {
-    if (s->profiling) {
+    if (s->graph_ready && s->graph_prof != s->profiling) s->graph_ready = 0;
+    if (!s->graph_ready && build_step_graph(s)) {
+        if (!s->profiling) return -1;
+        s->graph_ready = 0;
+        s->graph_prof = -1;  // capture with event nodes failed: eager profiling below
+    }
+    if (s->profiling && !s->graph_ready) {
         for (int i = 0; i < n; i++) {
             // eager with HIP events around the dominant GEMV (profiling mode only)
             const vox_hip_config_t& c = s->m->c;
             CK(launch_embed_step(s->adapter, s->m->tok_emb, s->state, c.dec_dim, s->xd, s->st));
-            CK(hipMemcpyAsync(s->h_state, s->state, 16, hipMemcpyDeviceToHost, s->st));
+            int cur[4];
+            CK(hipMemcpyAsync(cur, s->state, 16, hipMemcpyDeviceToHost, s->st));
             CK(hipStreamSynchronize(s->st));
-            const int pos = s->h_state[0];
+            const int pos = cur[0];
             if (enqueue_step_layers(s, nullptr, pos, s->m->rope_dec + (size_t)pos * c.dec_head_dim)) return -1;
             CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab / 2), s->state, s->tokens, s->tokens_cap, s->st));
         }
         return 0;
     }
-    if (!s->graph_ready && build_step_graph(s)) return -1;
     for (int i = 0; i < n; i++) CK(hipGraphLaunch(s->step_exec, s->st));
     return 0;
 }
@@ -859,6 +892,7 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
         if (logits_out)
             CK(hipMemcpyAsync(logits_out + (size_t)produced * V, s->logits, (size_t)V * 4, hipMemcpyDeviceToHost, s->st));
         CK(hipStreamSynchronize(s->st));
+        if (s->graph_ready && collect_graph_profile(s)) return -1;
         int eos_at = -1;
         if (stop_at_eos)
             for (int i = produced; i < produced + b; i++)
@@ -893,6 +927,7 @@ extern "C" int vox_hip_stream_state(vox_hip_stream_t* s, int* out6) {
 }
 
 extern "C" int vox_hip_stream_set_profiling(vox_hip_stream_t* s, int enable) {
+    if (s->profiling != enable) s->graph_ready = 0;
     s->profiling = enable;
     s->prof_ms = 0;
     s->prof_bytes = 0;
@@ -1088,4 +1123,16 @@ extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_
     if (logits) CK(hipMemcpyAsync(logits, s->logits, (size_t)c.vocab * 4, hipMemcpyDeviceToHost, s->st));
     CK(hipStreamSynchronize(s->st));
     return st4[2];
+}
+
+extern "C" void* vox_hip_device_upload(const void* host, size_t bytes) {
+    void* d = nullptr;
+    if (hipMalloc(&d, bytes) != hipSuccess) { set_err("device_upload: hipMalloc(%zu) failed", bytes); return nullptr; }
+    if (hipMemcpy(d, host, bytes, hipMemcpyHostToDevice) != hipSuccess) { hipFree(d); set_err("device_upload: copy failed"); return nullptr; }
+    return d;
+}
+
+extern "C" int vox_hip_device_free(void* dev) {
+    CK(hipFree(dev));
+    return 0;
 }

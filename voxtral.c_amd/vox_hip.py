@@ -42,7 +42,7 @@ EXPORTS = [
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
     "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
-    "vox_hip_stream_sync",
+    "vox_hip_stream_sync", "vox_hip_device_upload", "vox_hip_device_free",
 ]
 
 _lib = None
@@ -83,6 +83,8 @@ def lib():
         "vox_hip_stream_set_profiling": (I, [P, I]),
         "vox_hip_stream_profile": (I, [P, ctypes.POINTER(ctypes.c_double)]),
         "vox_hip_stream_sync": (I, [P]),
+        "vox_hip_device_upload": (P, [P, ctypes.c_size_t]),
+        "vox_hip_device_free": (I, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -268,6 +270,22 @@ def right_pad_samples(n_real_samples: int, delay_tokens: int) -> int:
     """vox_stream_flush padding (voxtral.c:1645-1649)."""
     align = (RAW_AUDIO_LENGTH_PER_TOK - (n_real_samples % RAW_AUDIO_LENGTH_PER_TOK)) % RAW_AUDIO_LENGTH_PER_TOK
     return align + ((delay_tokens + 1) + OFFLINE_STREAMING_BUFFER_TOKENS) * RAW_AUDIO_LENGTH_PER_TOK
+
+
+class DeviceArray:
+    """A host array copied once into HBM (inputs resident before a timed region)."""
+
+    def __init__(self, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        self.shape, self.dtype = a.shape, a.dtype
+        self.ptr = lib().vox_hip_device_upload(a.ctypes.data, a.nbytes)
+        if not self.ptr:
+            _err("device_upload")
+
+    def free(self):
+        if self.ptr:
+            lib().vox_hip_device_free(self.ptr)
+            self.ptr = None
 
 
 # ---------------------------------------------------------------------------

@@ -101,3 +101,25 @@ def test_streaming_interval_and_logits(models, jfk_samples):
     assert rel(hl, ol) < LOGIT_TOL, rel(hl, ol)
     hs.close()
     os_.close()
+
+
+def test_long_stream_multiblock_attention(tiny_weights):
+    """~33 s of audio (jfk x3) on TINY_LONG: 560 decoder positions, so the decode
+    attention runs on up to 3 key blocks (> 256 keys) and merges them."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    samples = np.concatenate([vox_oracle.read_wav(__import__("conftest").GOLDEN + "/jfk.wav")] * 3)
+    events = vox_oracle.transcribe_mel_schedule(samples)
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    hsess, osess = vox_hip.Session(hs), vox_oracle.OracleSession(os_)
+    for kind, mel in events:
+        getattr(hsess, kind)(mel, stop_at_eos=False)
+        getattr(osess, kind)(mel, stop_at_eos=False)
+    assert len(osess.tokens) > 400
+    assert hsess.tokens == osess.tokens
+    # logits of a late step (window > 256 keys)
+    assert hs.state()["kv_pos"] == os_.state()["dec_len"]
+    hs.close(); os_.close(); hm.close(); om.close()

@@ -1,0 +1,119 @@
+// kbench.hip -- isolated timing of the decode-step kernels (HIP events, back-to-back
+// launches on one stream).  Build: make -C tools; run: tools/kbench [iters]
+// Shapes: Voxtral-4B decoder (voxtral.h:37-48).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "../voxtral.c_amd/csrc/vox_hip_internal.h"
+
+using namespace vox;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+static void* dmalloc(size_t bytes, int fill) {
+    void* p;
+    CK(hipMalloc(&p, bytes));
+    // a small constant bf16 pair (finite as f32 too); values do not matter for timing
+    CK(hipMemsetD32(p, fill ? 0x3c003c01u : 0u, bytes / 4));
+    return p;
+}
+
+template <class F>
+static double timeit(F f, int iters, hipStream_t st) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; i++) f();
+    CK(hipEventRecord(a, st));
+    for (int i = 0; i < iters; i++) f();
+    CK(hipEventRecord(b, st));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms * 1000.0 / iters;
+}
+
+int main(int argc, char** argv) {
+    int iters = argc > 1 ? atoi(argv[1]) : 200;
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    const int D = 3072, DQ = 4096, DKV = 1024, DH = 9216, V = 131072, HD = 128, H = 32, KVH = 8;
+    // distinct weight buffers per launch so every launch streams from HBM (26 layers)
+    const int NL = 26;
+    std::vector<uint16_t*> wqkv(NL), wo(NL), w13(NL), w2(NL);
+    for (int l = 0; l < NL; l++) {
+        wqkv[l] = (uint16_t*)dmalloc((size_t)(DQ + 2 * DKV) * D * 2, 1);
+        wo[l] = (uint16_t*)dmalloc((size_t)D * DQ * 2, 1);
+        w13[l] = (uint16_t*)dmalloc((size_t)2 * DH * D * 2, 1);
+        w2[l] = (uint16_t*)dmalloc((size_t)D * DH * 2, 1);
+    }
+    uint16_t* emb = (uint16_t*)dmalloc((size_t)V * D * 2, 1);
+    float* x = (float*)dmalloc(DH * 4, 1);
+    float* y = (float*)dmalloc(V * 4, 0);
+    float* normw = (float*)dmalloc(DH * 4, 1);
+    float* ada = (float*)dmalloc(DH * 4, 1);
+    const int cap = 8192 + 64;
+    float* Kc = (float*)dmalloc((size_t)cap * DKV * 4, 1);
+    float* Vc = (float*)dmalloc((size_t)cap * DKV * 4, 1);
+    float* rope = (float*)dmalloc((size_t)16384 * HD * 4, 1);
+    float* part = (float*)dmalloc((size_t)H * 64 * (HD + 2) * 4, 0);
+    float* pv = (float*)dmalloc(4096 * 4, 0);
+    int* pi = (int*)dmalloc(4096 * 4, 0);
+    int* state;
+    CK(hipMalloc(&state, 16));
+
+    int layer = 0;
+    auto gemv = [&](int pro, int epi, const uint16_t* W, int K, int rows) {
+        GemvArgs a;
+        memset(&a, 0, sizeof a);
+        a.x = x; a.K = K; a.W = W; a.rows = rows; a.norm_w = normw; a.ada = ada; a.eps = 1e-5f;
+        a.y = y; a.qd = DQ; a.kvd = DKV; a.hd = HD; a.rope = rope; a.state = state; a.Kc = Kc; a.Vc = Vc;
+        a.cap = cap; a.part_val = pv; a.part_idx = pi;
+        CK(launch_gemv(pro, epi, a, st));
+    };
+    struct R { const char* name; double us; double bytes; };
+    std::vector<R> res;
+    auto add = [&](const char* n, double us, double bytes) {
+        res.push_back({n, us, bytes});
+        printf("%-34s %9.2f us  %8.1f GB/s\n", n, us, bytes / us / 1e3);
+        fflush(stdout);
+    };
+    add("gemv qkv  (6144x3072, norm+rope)", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D * 2);
+    add("gemv wo   (3072x4096, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ * 2);
+    add("gemv w13  (18432x3072, norm+swiglu)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
+    add("gemv w2   (3072x9216, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH * 2);
+    add("gemv lm   (131072x3072, logits)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D * 2);
+    for (int L : {64, 187, 256, 1000, 4096, 8192}) {
+        int st4[4] = {L - 1, 0, 0, 0};
+        CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
+        char nm[64];
+        snprintf(nm, sizeof nm, "attn decode L=%d", L);
+        const int comb = L > ATT_BLOCK_KEYS;
+        add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, comb, st)); }, iters, st),
+            (double)L * DKV * 2 * 4);
+    }
+    {
+        int st4[4] = {63, 0, 0, 0};
+        CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
+        add("attn L=64 dbg1 (no merge)", timeit([&] { CK(launch_attn_dbg(1, x, Kc, Vc, cap, state, part, y, st)); }, iters, st), 1.0);
+        add("attn L=64 dbg3 (loads+q only)", timeit([&] { CK(launch_attn_dbg(3, x, Kc, Vc, cap, state, part, y, st)); }, iters, st), 1.0);
+    }
+    add("argmax+embed", timeit([&] { CK(launch_argmax_final(pv, pi, 1024, state, nullptr, 0, (float*)emb, 1024, emb, D, x, st)); }, iters, st), 1.0);
+    add("empty-ish (embed step)", timeit([&] { CK(launch_embed_step((float*)emb, emb, state, D, x, st)); }, iters, st), 1.0);
+    // whole-layer sequence (no graph)
+    int st4[4] = {186, 0, 0, 0};
+    CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
+    double t = timeit([&] {
+        int l = layer++ % NL;
+        gemv(PRO_NORM, EPI_QKV, wqkv[l], D, DQ + 2 * DKV);
+        CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, 0, st));
+        gemv(PRO_NONE, EPI_RESID, wo[l], DQ, D);
+        gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[l], D, 2 * DH);
+        gemv(PRO_NONE, EPI_RESID, w2[l], DH, D);
+    }, iters, st);
+    add("layer (5 launches, eager)", t, 232783872.0);
+    return 0;
+}

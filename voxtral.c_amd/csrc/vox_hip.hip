@@ -373,7 +373,6 @@ extern "C" int vox_hip_model_ada_scale(vox_hip_model_t* m, float* out) {
 // ---------------------------------------------------------------------------
 static const int ENC_SUB = 1024;      // encoder rows per pass through the 32 layers
 static const int DEC_SLACK = 64;      // decoder ring capacity = window + slack
-static const int NSPLIT_ATT = 32;     // decode attention key splits
 static const int STEP_BATCH = 16;     // graph replays between EOS checks
 
 struct vox_hip_stream {
@@ -401,13 +400,14 @@ struct vox_hip_stream {
     float *xd, *xnd, *qkvd, *qd_, *attd, *gated, *part, *logits, *pval;
     int *pidx, *state, *tokens;
     int dec_rows_cap, tokens_cap;
-    hipGraphExec_t step_exec;
-    int graph_ready;
+    hipGraphExec_t step_exec[2];  // [0]: context <= ATT_BLOCK_KEYS (no combine), [1]: any
+    int graph_ready;              // bit mask of built graphs
     int started, eos_seen, n_generated;
     int h_state[4];
     // profiling
     int profiling;
     int graph_prof;               // the captured step graph carries event-record nodes
+    int capturing;
     hipEvent_t evt[2];
     std::vector<hipEvent_t> pev;  // [2*dec_layers] around each W1|W3 GEMV in the graph
     double prof_ms, prof_bytes;
@@ -491,7 +491,7 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->att, (size_t)ENC_SUB * EQ));
     TRYH(dalloc(&s->gate, (size_t)ENC_SUB * c.enc_hidden));
     TRYH(dalloc(&s->ad_mid, (size_t)(ENC_SUB / 4 + 4) * c.dec_dim));
-    TRYH(dalloc(&s->part, (size_t)c.dec_heads * NSPLIT_ATT * (c.dec_head_dim + 2) + (size_t)c.enc_heads * NSPLIT_ATT * (c.enc_head_dim + 2)));
+    TRYH(dalloc(&s->part, (size_t)c.dec_heads * attn_maxch(c.dec_window) * (c.dec_head_dim + 2)));
     TRYH(dalloc(&s->logits, (size_t)c.vocab));
     TRYH(dalloc(&s->pval, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
@@ -510,7 +510,8 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
 extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     if (!s) return;
     if (s->st) hipStreamSynchronize(s->st);
-    if (s->step_exec) hipGraphExecDestroy(s->step_exec);
+    for (int g = 0; g < 2; g++)
+        if (s->step_exec[g]) hipGraphExecDestroy(s->step_exec[g]);
     dfree(s->ek); dfree(s->ev); dfree(s->dk); dfree(s->dv);
     dfree(s->mel_p); dfree(s->mel_tail); dfree(s->c0_p); dfree(s->c0_tail); dfree(s->c0_res);
     dfree(s->im2col); dfree(s->x_enc); dfree(s->xn); dfree(s->qkv); dfree(s->q); dfree(s->att);
@@ -714,7 +715,8 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
 // One decoder step for the token whose input is already in s->xd[0..D).
 // state != nullptr: positions come from device state (graph mode);
 // otherwise pos/rope_row are host values (boundary twin).
-static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row) {
+static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row,
+                               int with_combine) {
     vox_hip_model_t* m = s->m;
     const vox_hip_config_t& c = m->c;
     const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
@@ -728,7 +730,7 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         GemvArgs a;
         memset(&a, 0, sizeof a);
         // norm -> QKV -> RoPE -> KV append (decoder.c:709-722)
-        a.x = s->xd; a.K = DD; a.W = L.wqkv; a.units = (DQ + 2 * DKV) / 2;
+        a.x = s->xd; a.K = DD; a.W = L.wqkv; a.rows = DQ + 2 * DKV;
         a.norm_w = L.attn_norm; a.eps = c.dec_eps; a.y = s->qd_;
         a.qd = DQ; a.kvd = DKV; a.hd = hd;
         a.state = state; a.pos = pos;
@@ -737,72 +739,65 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
         // attention over the last min(pos+1, window) keys (decoder.c:724-733)
         CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
-                              NSPLIT_ATT, s->part, s->attd, st));
+                              s->part, s->attd, with_combine, st));
         // wo + residual (decoder.c:735-740)
         memset(&a, 0, sizeof a);
-        a.x = s->attd; a.K = DQ; a.W = L.wo; a.units = DD / 2; a.y = s->xd;
+        a.x = s->attd; a.K = DQ; a.W = L.wo; a.rows = DD; a.y = s->xd;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
         // norm * (1 + ada) -> W1|W3 -> silu * up (decoder.c:742-758)
         memset(&a, 0, sizeof a);
-        a.x = s->xd; a.K = DD; a.W = L.w13; a.units = DH; a.norm_w = L.ffn_norm;
+        a.x = s->xd; a.K = DD; a.W = L.w13; a.rows = 2 * DH; a.norm_w = L.ffn_norm;
         a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
         const bool gprof = s->profiling && state && (int)s->pev.size() == 2 * c.dec_layers;
-        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l], st, hipEventRecordExternal));
-        if (s->profiling && !state) CK(hipEventRecord(s->evt[0], st));
+        const unsigned evflag = s->capturing ? hipEventRecordExternal : 0;
+        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l], st, evflag));
         CK(launch_gemv(PRO_NORM_ADA, EPI_SWIGLU, a, st));
-        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l + 1], st, hipEventRecordExternal));
-        if (s->profiling && !state) {
-            CK(hipEventRecord(s->evt[1], st));
-            CK(hipEventSynchronize(s->evt[1]));
-            float ms = 0.f;
-            CK(hipEventElapsedTime(&ms, s->evt[0], s->evt[1]));
-            s->prof_ms += ms;
-            s->prof_bytes += (double)2 * DH * DD * 2;
-            s->prof_launches++;
-        }
+        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l + 1], st, evflag));
         // W2 + residual (decoder.c:758-760)
         memset(&a, 0, sizeof a);
-        a.x = s->gated; a.K = DH; a.W = L.w2; a.units = DD / 2; a.y = s->xd;
+        a.x = s->gated; a.K = DH; a.W = L.w2; a.rows = DD; a.y = s->xd;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
     }
     // final norm + LM head (tied embeddings) + argmax (decoder.c:762-779)
     GemvArgs a;
     memset(&a, 0, sizeof a);
-    a.x = s->xd; a.K = DD; a.W = m->tok_emb; a.units = c.vocab / 2; a.norm_w = m->dec_norm;
+    a.x = s->xd; a.K = DD; a.W = m->tok_emb; a.rows = c.vocab; a.norm_w = m->dec_norm;
     a.eps = c.dec_eps; a.y = s->logits; a.part_val = s->pval; a.part_idx = s->pidx;
     CK(launch_gemv(PRO_NORM, EPI_LOGITS, a, st));
     return 0;
 }
 
-static int enqueue_graph_step(vox_hip_stream_t* s) {
+static int enqueue_graph_step(vox_hip_stream_t* s, int with_combine) {
     const vox_hip_config_t& c = s->m->c;
-    CK(launch_embed_step(s->adapter, s->m->tok_emb, s->state, c.dec_dim, s->xd, s->st));
-    if (enqueue_step_layers(s, s->state, 0, nullptr)) return -1;
-    CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab / 2), s->state, s->tokens, s->tokens_cap, s->st));
+    if (enqueue_step_layers(s, s->state, 0, nullptr, with_combine)) return -1;
+    CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), s->state, s->tokens, s->tokens_cap,
+                           s->adapter, s->adapter_cap, s->m->tok_emb, c.dec_dim, s->xd, s->st));
     return 0;
 }
 
-static int build_step_graph(vox_hip_stream_t* s) {
+static int build_step_graph(vox_hip_stream_t* s, int gi) {
     if (s->profiling && s->pev.empty()) {
         s->pev.resize(2 * s->m->c.dec_layers);
         for (auto& e : s->pev) CK(hipEventCreate(&e));
     }
-    if (s->step_exec) {
-        hipGraphExecDestroy(s->step_exec);
-        s->step_exec = nullptr;
+    if (s->step_exec[gi]) {
+        hipGraphExecDestroy(s->step_exec[gi]);
+        s->step_exec[gi] = nullptr;
     }
     hipGraph_t g = nullptr;
     CK(hipStreamBeginCapture(s->st, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_graph_step(s);
+    s->capturing = 1;
+    int rc = enqueue_graph_step(s, gi);
+    s->capturing = 0;
     hipError_t e = hipStreamEndCapture(s->st, &g);
     if (rc || e != hipSuccess) {
         if (g) hipGraphDestroy(g);
         return set_err("graph capture failed: %s", hipGetErrorString(e));
     }
-    e = hipGraphInstantiate(&s->step_exec, g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&s->step_exec[gi], g, nullptr, nullptr, 0);
     hipGraphDestroy(g);
     if (e != hipSuccess) return set_err("graph instantiate failed: %s", hipGetErrorString(e));
-    s->graph_ready = 1;
+    s->graph_ready |= 1 << gi;
     s->graph_prof = s->profiling;
     return 0;
 }
@@ -822,28 +817,35 @@ static int collect_graph_profile(vox_hip_stream_t* s) {
     return 0;
 }
 
-static int run_steps(vox_hip_stream_t* s, int n) {
-    if (s->graph_ready && s->graph_prof != s->profiling) s->graph_ready = 0;
-    if (!s->graph_ready && build_step_graph(s)) {
-        if (!s->profiling) return -1;
-        s->graph_ready = 0;
-        s->graph_prof = -1;  // capture with event nodes failed: eager profiling below
+static int use_graphs() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VOX_HIP_GRAPH");
+        v = (e && atoi(e) == 0) ? 0 : 1;
     }
-    if (s->profiling && !s->graph_ready) {
-        for (int i = 0; i < n; i++) {
-            // eager with HIP events around the dominant GEMV (profiling mode only)
-            const vox_hip_config_t& c = s->m->c;
-            CK(launch_embed_step(s->adapter, s->m->tok_emb, s->state, c.dec_dim, s->xd, s->st));
-            int cur[4];
-            CK(hipMemcpyAsync(cur, s->state, 16, hipMemcpyDeviceToHost, s->st));
-            CK(hipStreamSynchronize(s->st));
-            const int pos = cur[0];
-            if (enqueue_step_layers(s, nullptr, pos, s->m->rope_dec + (size_t)pos * c.dec_head_dim)) return -1;
-            CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab / 2), s->state, s->tokens, s->tokens_cap, s->st));
+    return v;
+}
+
+// n steps starting at logical kv position pos0 (host mirror): while every step's context
+// fits one attention block the graph without the combine kernel is replayed.
+static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
+    const vox_hip_config_t& c = s->m->c;
+    const int gi = (std::min(pos0 + n, c.dec_window) <= ATT_BLOCK_KEYS) ? 0 : 1;
+    if (!use_graphs()) {
+        // eager launches of the same device-state kernels (profilers that cannot follow
+        // graph replays; VOX_HIP_GRAPH=0)
+        if (s->profiling && s->pev.empty()) {
+            s->pev.resize(2 * c.dec_layers);
+            for (auto& e : s->pev) CK(hipEventCreate(&e));
         }
+        s->graph_prof = s->profiling;
+        for (int i = 0; i < n; i++)
+            if (enqueue_graph_step(s, gi)) return -1;
         return 0;
     }
-    for (int i = 0; i < n; i++) CK(hipGraphLaunch(s->step_exec, s->st));
+    if (s->graph_ready && s->graph_prof != s->profiling) s->graph_ready = 0;
+    if (!(s->graph_ready & (1 << gi)) && build_step_graph(s, gi)) return -1;
+    for (int i = 0; i < n; i++) CK(hipGraphLaunch(s->step_exec[gi], s->st));
     return 0;
 }
 
@@ -879,20 +881,23 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
         avail = s->total_adapter - st4[1];
     }
     if (ensure_rope(s, (long long)s->h_state[0] + avail + 1)) return -1;
+    // step input for the first step of this call (later inputs are built by the previous
+    // step's argmax kernel)
+    if (avail > 0) CK(launch_embed_step(s->adapter, m->tok_emb, s->state, D, s->xd, s->st));
     if (s->n_generated + avail > s->tokens_cap) avail = s->tokens_cap - s->n_generated;
     int todo = std::min(max_steps, avail);
     std::vector<int> tok;
     while (produced < todo) {
         int b = std::min(STEP_BATCH, todo - produced);
         if (logits_out) b = 1;
-        if (run_steps(s, b)) return -1;
+        if (run_steps(s, b, s->h_state[0] + produced)) return -1;
         tok.resize(produced + b);
         CK(hipMemcpyAsync(tok.data() + produced, s->tokens + step_base + produced, (size_t)b * 4,
                           hipMemcpyDeviceToHost, s->st));
         if (logits_out)
             CK(hipMemcpyAsync(logits_out + (size_t)produced * V, s->logits, (size_t)V * 4, hipMemcpyDeviceToHost, s->st));
         CK(hipStreamSynchronize(s->st));
-        if (s->graph_ready && collect_graph_profile(s)) return -1;
+        if (collect_graph_profile(s)) return -1;
         int eos_at = -1;
         if (stop_at_eos)
             for (int i = produced; i < produced + b; i++)
@@ -978,10 +983,10 @@ static int twin_init() {
 }
 
 static int twin_gemm(int M, int N, int K, const float* dA, const uint16_t* dW, float* dC) {
-    if (M == 1 && N % 2 == 0 && K % 8 == 0) {
+    if (M == 1 && N % GEMV_RB == 0 && K % 8 == 0 && K <= 5 * 2048) {
         GemvArgs a;
         memset(&a, 0, sizeof a);
-        a.x = dA; a.K = K; a.W = dW; a.units = N / 2; a.y = dC;
+        a.x = dA; a.K = K; a.W = dW; a.rows = N; a.y = dC;
         CK(launch_gemv(PRO_NONE, EPI_STORE, a, g_twin_st));
         return 0;
     }
@@ -1113,12 +1118,13 @@ extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_
                                          float* logits) {
     const vox_hip_config_t& c = s->m->c;
     if (upload_rope_rows(s, rope_freqs, (size_t)c.dec_head_dim)) return -1;
-    if (enqueue_step_layers(s, nullptr, logical_pos, s->rope_rows)) return -1;
+    if (enqueue_step_layers(s, nullptr, logical_pos, s->rope_rows, 1)) return -1;
     // argmax into a scratch state so the graph-mode device state is untouched
     int* tmp_state = s->tokens + s->tokens_cap - 8;
     int st4[4] = {0, 0, 0, 0};
     CK(hipMemcpyAsync(tmp_state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
-    CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab / 2), tmp_state, nullptr, 0, s->st));
+    CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), tmp_state, nullptr, 0, nullptr, 0,
+                           nullptr, c.dec_dim, nullptr, s->st));
     CK(hipMemcpyAsync(st4, tmp_state, sizeof st4, hipMemcpyDeviceToHost, s->st));
     if (logits) CK(hipMemcpyAsync(logits, s->logits, (size_t)c.vocab * 4, hipMemcpyDeviceToHost, s->st));
     CK(hipStreamSynchronize(s->st));

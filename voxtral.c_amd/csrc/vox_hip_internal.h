@@ -8,13 +8,14 @@ namespace vox {
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_GELU_ERF = 3, EPI_SWIGLU = 4, EPI_QKV = 5, EPI_LOGITS = 6 };
 enum { PRO_NONE = 0, PRO_NORM = 1, PRO_NORM_ADA = 2 };
 
-constexpr int GEMV_MAX_BLOCKS = 2048;  // 8 blocks of 256 threads per CU on 256 CUs
+constexpr int GEMV_MAX_BLOCKS = 1024;  // 4 blocks of 256 threads per CU on 256 CUs
+constexpr int GEMV_RB = 4;             // rows per block iteration (even: rope / swiglu pairs)
 
 struct GemvArgs {
     const float* x;        // input vector [K] (device)
     int K;
     const uint16_t* W;     // bf16 [rows, K]
-    int units;             // row pairs (or hidden units for SWIGLU)
+    int rows;              // output rows streamed (2*hidden for SWIGLU)
     const float* norm_w;   // PRO_NORM*: RMSNorm weight [K]
     const float* ada;      // PRO_NORM_ADA: ada_scale row [K]
     float eps;
@@ -33,7 +34,8 @@ struct GemvArgs {
     int* part_idx;
 };
 
-int gemv_grid(int units);
+int gemv_grid(int rows);
+int attn_maxch(int window);
 hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,
                                const float* ada, int M, int D, float eps, hipStream_t st);
 hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const uint16_t* W, int K,
@@ -46,13 +48,17 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st);
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
-                              int KVH, int nsplit, float* part, float* out, hipStream_t st);
+                              int KVH, float* part, float* out, int with_combine, hipStream_t st);
+constexpr int ATT_BLOCK_KEYS = 256;  // keys one decode-attention block covers
+hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
+                           const int* state, float* part, float* out, hipStream_t st);
 hipError_t launch_embed_step(const float* adapter, const uint16_t* emb, const int* state, int D,
                              float* x, hipStream_t st);
 hipError_t launch_embed_rows(const float* adapter, const uint16_t* emb, int row0, int n,
                              int first_tok, int rest_tok, int D, float* x, hipStream_t st);
 hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
-                               int cap, hipStream_t st);
+                               int cap, const float* adapter, int adapter_rows,
+                               const uint16_t* emb, int D, float* x, hipStream_t st);
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

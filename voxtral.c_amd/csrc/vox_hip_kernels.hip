@@ -42,14 +42,37 @@ __device__ __forceinline__ uint32_t f2bf(float f) {
     return u >> 16;
 }
 
+// Cross-lane reductions: DPP inside each 16-lane row (quad_perm xor1 / xor2, row half
+// mirror, row mirror -- VALU ops with no LDS round trip), then two ds_bpermute steps
+// across rows.  The pairing pattern is fixed, so results are deterministic.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp<0x141>(v);  // row_half_mirror
+    v += dpp<0x140>(v);  // row_mirror
+    return v;
+}
+__device__ __forceinline__ float row_max16(float v) {
+    v = fmaxf(v, dpp<0xB1>(v));
+    v = fmaxf(v, dpp<0x4E>(v));
+    v = fmaxf(v, dpp<0x141>(v));
+    v = fmaxf(v, dpp<0x140>(v));
+    return v;
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v = row_sum16(v);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
     return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    v = row_max16(v);
+    v = fmaxf(v, __shfl_xor(v, 16, 64));
+    v = fmaxf(v, __shfl_xor(v, 32, 64));
     return v;
 }
 
@@ -361,228 +384,386 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
 
 // ============================================================================
 // M=1 weight-streaming GEMV with fused prologue / epilogue (decoder step).
-// Each wave owns units (row pairs) in a grid-stride loop; 16-B bf16 loads straight to
-// VGPRs, x staged once per block in LDS (normalised there when PRO_NORM).
+//
+// A block (4 waves) owns groups of RB rows and streams them with K split across its
+// waves: wave w reads the 1-KiB chunk blocks j*4+w of every row, so each wave keeps only
+// its quarter of x in registers (loaded once per block, normalised there when PRO_NORM),
+// never stages x through LDS, and a launch needs no more blocks than CUs x 4 to stay
+// balanced (grid-stride over groups).  Weights: 16-B non-temporal loads straight to
+// VGPRs (cdna_hip_programming.md "GEMV / M <= 16" row).  Partial sums meet in LDS; wave
+// 0 applies the epilogue.  Summation order is fixed (deterministic).
 // ============================================================================
-template <int PRO, int EPI>
-__global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float xs[];
-    __shared__ float red[8];
-    __shared__ int redi[4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int K = a.K;
-    const int K4 = K >> 2;
-    const float4* x4 = reinterpret_cast<const float4*>(a.x);
-    float4* xs4 = reinterpret_cast<float4*>(xs);
-    float ss = 0.f;
-    for (int i = tid; i < K4; i += 256) {
-        float4 v = x4[i];
-        xs4[i] = v;
-        if (PRO != PRO_NONE) ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, ss))));
-    }
-    if (PRO != PRO_NONE) {
-        ss = wave_sum(ss);
-        if (lane == 0) red[wave] = ss;
-        __syncthreads();
-        const float tot = red[0] + red[1] + red[2] + red[3];
-        const float inv = 1.0f / sqrtf(tot / (float)K + a.eps);
-        for (int i = tid; i < K; i += 256) {
-            float v = xs[i] * inv * a.norm_w[i];
-            if (PRO == PRO_NORM_ADA) v *= (1.0f + a.ada[i]);
-            xs[i] = v;
+template <int EPI, int RB>
+__device__ __forceinline__ void gemv_rows(int g, int (&rows)[RB]) {
+#pragma unroll
+    for (int i = 0; i < RB; i++) {
+        if (EPI == EPI_SWIGLU) {
+            // pair i = (w1 row, w3 row) of hidden unit u = g*RB/2 + i/2 (16-row interleave)
+            const int u = g * (RB / 2) + (i >> 1);
+            rows[i] = ((u >> 4) << 5) + (u & 15) + ((i & 1) << 4);
+        } else {
+            rows[i] = g * RB + i;
         }
     }
-    __syncthreads();
+}
+
+template <int RB, int KQ>
+__device__ __forceinline__ void gemv_load(const uint16_t* __restrict__ W, int K, int K8,
+                                          const int (&rows)[RB], int wave, int lane,
+                                          uint4 (&wv)[KQ][RB]) {
+    // Chunks past K (K not a multiple of 8*256) re-load chunk 0 and meet x = 0: every load
+    // is unconditional, so hipcc issues them all before the first wait (a guarded load
+    // makes it wait vmcnt(0) at each branch join).
+#pragma unroll
+    for (int j = 0; j < KQ; j++) {
+        const int c0 = (j * 4 + wave) * 64 + lane;
+        const int c = c0 < K8 ? c0 : 0;
+#pragma unroll
+        for (int i = 0; i < RB; i++) wv[j][i] = ldnt(reinterpret_cast<const uint4*>(W + (size_t)rows[i] * K) + c);
+    }
+}
+
+template <int PRO, int EPI, int RB, int KQ>
+__global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
+    __shared__ float red[2][4][RB];
+    __shared__ float sred[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = a.K, K8 = K >> 3;
+    const int ngroups = a.rows / RB;
+    int g = blockIdx.x;
+    int rows[RB];
+    uint4 wv[KQ][RB];
+    // first group's weights are independent of x: issue them before the prologue
+    gemv_rows<EPI, RB>(g, rows);
+    gemv_load<RB, KQ>(a.W, K, K8, rows, wave, lane, wv);
+
+    float4 xr[KQ][2];
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < KQ; j++) {
+        const int c = (j * 4 + wave) * 64 + lane;
+        const float4* xp = reinterpret_cast<const float4*>(a.x) + 2 * (c < K8 ? c : 0);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 x0 = xp[0], x1 = xp[1];
+        xr[j][0] = c < K8 ? x0 : z;
+        xr[j][1] = c < K8 ? x1 : z;
+        if (PRO != PRO_NONE) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const float4 v = xr[j][h];
+                ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, ss))));
+            }
+        }
+    }
+    if (PRO != PRO_NONE) {
+        // RMSNorm prologue (voxtral_kernels.c:475-492; ada: voxtral_decoder.c:742-745)
+        ss = wave_sum(ss);
+        if (lane == 0) sred[wave] = ss;
+        __syncthreads();
+        const float tot = sred[0] + sred[1] + sred[2] + sred[3];
+        const float inv = 1.0f / sqrtf(tot / (float)K + a.eps);
+#pragma unroll
+        for (int j = 0; j < KQ; j++) {
+            const int c0 = (j * 4 + wave) * 64 + lane;
+            const int c = c0 < K8 ? c0 : 0;
+            const float4* wp = reinterpret_cast<const float4*>(a.norm_w) + 2 * c;
+            const float4* ap = reinterpret_cast<const float4*>(PRO == PRO_NORM_ADA ? a.ada : a.norm_w) + 2 * c;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                float4 v = xr[j][h];
+                const float4 nw = wp[h];
+                v.x = v.x * inv * nw.x; v.y = v.y * inv * nw.y;
+                v.z = v.z * inv * nw.z; v.w = v.w * inv * nw.w;
+                if (PRO == PRO_NORM_ADA) {
+                    const float4 ad = ap[h];
+                    v.x *= (1.0f + ad.x); v.y *= (1.0f + ad.y);
+                    v.z *= (1.0f + ad.z); v.w *= (1.0f + ad.w);
+                }
+                xr[j][h] = v;
+            }
+        }
+    }
 
     int lp = 0;
     if (EPI == EPI_QKV) lp = a.state ? a.state[0] : a.pos;
     float best = -INFINITY;
     int besti = 0x7fffffff;
-
-    const int nunits = a.units;
-    const int K8 = K >> 3;
-    for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
-        int r0, r1;
-        if (EPI == EPI_SWIGLU) {
-            r0 = ((u >> 4) << 5) + (u & 15);
-            r1 = r0 + 16;
-        } else {
-            r0 = 2 * u;
-            r1 = 2 * u + 1;
+    int buf = 0;
+    for (;;) {
+        float acc[RB];
+#pragma unroll
+        for (int i = 0; i < RB; i++) acc[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < KQ; j++)
+#pragma unroll
+            for (int i = 0; i < RB; i++) acc[i] = dot8(wv[j][i], xr[j][0], xr[j][1], acc[i]);
+        const int gcur = g;
+        int rcur[RB];
+#pragma unroll
+        for (int i = 0; i < RB; i++) rcur[i] = rows[i];
+        g += gridDim.x;
+        if (g < ngroups) {  // next group's loads go out before this group's reduction
+            gemv_rows<EPI, RB>(g, rows);
+            gemv_load<RB, KQ>(a.W, K, K8, rows, wave, lane, wv);
         }
-        const uint4* w0 = reinterpret_cast<const uint4*>(a.W + (size_t)r0 * K);
-        const uint4* w1 = reinterpret_cast<const uint4*>(a.W + (size_t)r1 * K);
-        float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll 4
-        for (int c = lane; c < K8; c += 64) {
-            uint4 p0 = ldnt(w0 + c);
-            uint4 p1 = ldnt(w1 + c);
-            float4 xa = xs4[2 * c], xb = xs4[2 * c + 1];
-            acc0 = dot8(p0, xa, xb, acc0);
-            acc1 = dot8(p1, xa, xb, acc1);
-        }
-        acc0 = wave_sum(acc0);
-        acc1 = wave_sum(acc1);
-        if (EPI == EPI_LOGITS) {
-            // first max wins (voxtral_decoder.c:771-779): strictly greater, lower index on ties
-            if (acc0 > best) { best = acc0; besti = r0; }
-            if (acc1 > best) { best = acc1; besti = r1; }
-        }
+#pragma unroll
+        for (int i = 0; i < RB; i++) acc[i] = wave_sum(acc[i]);
         if (lane == 0) {
-            if (EPI == EPI_STORE) {
-                a.y[r0] = acc0 + (a.bias ? a.bias[r0] : 0.f);
-                a.y[r1] = acc1 + (a.bias ? a.bias[r1] : 0.f);
-            } else if (EPI == EPI_RESID) {
-                a.y[r0] += acc0 + (a.bias ? a.bias[r0] : 0.f);
-                a.y[r1] += acc1 + (a.bias ? a.bias[r1] : 0.f);
-            } else if (EPI == EPI_LOGITS) {
-                a.y[r0] = acc0;
-                a.y[r1] = acc1;
-            } else if (EPI == EPI_SWIGLU) {
-                a.y[u] = silu(acc0) * acc1;
-            } else if (EPI == EPI_QKV) {
-                const int hd = a.hd;
-                if (r0 < a.qd + a.kvd) {
-                    const int col = r0 < a.qd ? r0 : r0 - a.qd;
-                    const int d = (col % hd) >> 1;
-                    const float* rp = a.rope + (size_t)lp * hd;
-                    const float c = rp[2 * d], s = rp[2 * d + 1];
-                    const float o0 = acc0 * c - acc1 * s, o1 = acc0 * s + acc1 * c;
-                    if (r0 < a.qd) {
-                        a.y[r0] = o0;
-                        a.y[r1] = o1;
+#pragma unroll
+            for (int i = 0; i < RB; i++) red[buf][wave][i] = acc[i];
+        }
+        __syncthreads();
+        if (wave == 0 && lane == 0) {
+            float v[RB];
+#pragma unroll
+            for (int i = 0; i < RB; i++) v[i] = ((red[buf][0][i] + red[buf][1][i]) + red[buf][2][i]) + red[buf][3][i];
+#pragma unroll
+            for (int i = 0; i < RB; i += 2) {
+                const int r0 = rcur[i], r1 = rcur[i + 1];
+                const float acc0 = v[i], acc1 = v[i + 1];
+                if (EPI == EPI_STORE) {
+                    a.y[r0] = acc0 + (a.bias ? a.bias[r0] : 0.f);
+                    a.y[r1] = acc1 + (a.bias ? a.bias[r1] : 0.f);
+                } else if (EPI == EPI_RESID) {
+                    a.y[r0] += acc0 + (a.bias ? a.bias[r0] : 0.f);
+                    a.y[r1] += acc1 + (a.bias ? a.bias[r1] : 0.f);
+                } else if (EPI == EPI_LOGITS) {
+                    a.y[r0] = acc0;
+                    a.y[r1] = acc1;
+                    // first max wins (voxtral_decoder.c:771-779): rows ascend within a block
+                    if (acc0 > best) { best = acc0; besti = r0; }
+                    if (acc1 > best) { best = acc1; besti = r1; }
+                } else if (EPI == EPI_SWIGLU) {
+                    a.y[gcur * (RB / 2) + (i >> 1)] = silu(acc0) * acc1;
+                } else if (EPI == EPI_QKV) {
+                    const int hd = a.hd;
+                    if (r0 < a.qd + a.kvd) {
+                        const int col = r0 < a.qd ? r0 : r0 - a.qd;
+                        const int d = (col % hd) >> 1;
+                        const float* rp = a.rope + (size_t)lp * hd;
+                        const float cs = rp[2 * d], sn = rp[2 * d + 1];
+                        const float o0 = acc0 * cs - acc1 * sn, o1 = acc0 * sn + acc1 * cs;
+                        if (r0 < a.qd) {
+                            a.y[r0] = o0;
+                            a.y[r1] = o1;
+                        } else {
+                            float* kr = a.Kc + (size_t)(lp % a.cap) * a.kvd;
+                            kr[col] = o0;
+                            kr[col + 1] = o1;
+                        }
                     } else {
-                        float* kr = a.Kc + (size_t)(lp % a.cap) * a.kvd;
-                        kr[col] = o0;
-                        kr[col + 1] = o1;
+                        const int col = r0 - a.qd - a.kvd;
+                        float* vr = a.Vc + (size_t)(lp % a.cap) * a.kvd;
+                        vr[col] = acc0;
+                        vr[col + 1] = acc1;
                     }
-                } else {
-                    const int col = r0 - a.qd - a.kvd;
-                    float* vr = a.Vc + (size_t)(lp % a.cap) * a.kvd;
-                    vr[col] = acc0;
-                    vr[col + 1] = acc1;
                 }
             }
         }
+        buf ^= 1;
+        if (g >= ngroups) break;
     }
-    if (EPI == EPI_LOGITS) {
-        __syncthreads();
-        if (lane == 0) {
-            red[wave] = best;
-            redi[wave] = besti;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            float bv = red[0];
-            int bi = redi[0];
-            for (int w = 1; w < 4; w++)
-                if (red[w] > bv || (red[w] == bv && redi[w] < bi)) { bv = red[w]; bi = redi[w]; }
-            a.part_val[blockIdx.x] = bv;
-            a.part_idx[blockIdx.x] = bi;
-        }
+    if (EPI == EPI_LOGITS && wave == 0 && lane == 0) {
+        a.part_val[blockIdx.x] = best;
+        a.part_idx[blockIdx.x] = besti;
     }
 }
 
 // ============================================================================
-// Decode attention (one query per head, GQA), flash-decoding split over keys.
+// Decode attention (one query per head, GQA group of <= 4 heads per kv head).
 // Keys: the last min(lp+1, window) logical positions (voxtral_decoder.c:731-733 after
-// compaction, voxtral_kernels.c:554-560).  Partials [H][nsplit][HD+2].
+// compaction; voxtral_kernels.c:554-560).  A block owns up to 256 consecutive keys of
+// one kv head; each wave walks 64 of them in 16-key chunks (lanes = key x quarter of
+// head_dim for Q.K, lanes = dims for P.V, every K/V load shared by the GQA heads) with an
+// online softmax; the 4 waves merge in LDS.  With one block per kv head (L <= 256) the
+// block writes the attention output directly; otherwise it writes an (o, m, l) partial
+// and k_attn_combine merges the blocks.
 // ============================================================================
-template <int HD>
-__global__ __launch_bounds__(256) void k_attn_decode(const float* __restrict__ q,
-                                                     const float* __restrict__ Kc,
-                                                     const float* __restrict__ Vc, int cap,
-                                                     const int* __restrict__ state, int pos_host,
-                                                     int window, float scale, int H, int KVH,
-                                                     int nsplit, float* __restrict__ part) {
-    constexpr int DPL = HD / 64;  // dims per lane in PV
+constexpr int ATT_CH = 16;      // keys per wave
+constexpr int ATT_WAVES = 16;   // waves per block (1024 threads)
+constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per block
+
+template <int HD, int DBG = 0>
+__global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ q,
+                                                      const float* __restrict__ Kc,
+                                                      const float* __restrict__ Vc, int cap,
+                                                      const int* __restrict__ state, int pos_host,
+                                                      int window, float scale, int H, int KVH,
+                                                      int maxs, float* __restrict__ part,
+                                                      float* __restrict__ out) {
+    constexpr int DQ = HD / 4;   // dims per lane for Q.K
+    constexpr int DPL = HD / 64; // dims per lane for P.V
     __shared__ __attribute__((aligned(16))) float sQ[4][HD];
-    const int kvh = blockIdx.y, split = blockIdx.x;
+    __shared__ float sM[ATT_WAVES][4], sL[ATT_WAVES][4], sF[ATT_WAVES][4];
+    __shared__ float sDen[4], sMax[4];
+    __shared__ __attribute__((aligned(16))) float sO[ATT_WAVES][4][HD];
+    const int kvh = blockIdx.y, sb = blockIdx.x;
     const int hpk = H / KVH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvd = KVH * HD;
     const int lp = state ? state[0] : pos_host;
     const int L = min(lp + 1, window);
     const int first = lp - L + 1;
-    int per = (L + nsplit - 1) / nsplit;
-    per = ((per + 63) / 64) * 64;
-    const int s0 = first + split * per;
-    const int s1 = min(s0 + per, lp + 1);
-    for (int e = tid; e < hpk * HD; e += 256) sQ[e / HD][e % HD] = q[(size_t)(kvh * hpk) * HD + e];
-    __syncthreads();
-    if (wave >= hpk) return;
-    const int h = kvh * hpk + wave;
-    float* pp = part + ((size_t)h * nsplit + split) * (HD + 2);
-    float m = -1e30f, l = 0.f;
-    float o[DPL];
+    const int S = (L + ATT_BK - 1) / ATT_BK;
+    if (sb >= S) return;  // uniform per block
+    const int k0 = first + sb * ATT_BK + wave * ATT_CH;
+    const int kn = min(ATT_CH, lp + 1 - k0);  // may be <= 0 for trailing waves
+    const int kk = lane & 15, dq = lane >> 4;
+
+    // K quarter-rows and V dims for this wave's 16 keys: issued before anything else
+    float4 kv[DQ / 4];
+    float vv[ATT_CH][DPL];
+    {
+        const int key = k0 + (kk < kn ? kk : 0);
+        const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)((key < 0 ? 0 : key) % cap) * kvd + kvh * HD + dq * DQ);
 #pragma unroll
-    for (int e = 0; e < DPL; e++) o[e] = 0.f;
-    for (int kb = s0; kb < s1; kb += 64) {
-        const int kp = kb + lane;
-        const bool valid = kp < s1;
-        float sc = -INFINITY;
-        if (valid) {
-            const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)(kp % cap) * kvd + kvh * HD);
-            float acc = 0.f;
-#pragma unroll 8
-            for (int d4 = 0; d4 < HD / 4; d4++) {
-                float4 kv = kr[d4];
-                float4 qv = *reinterpret_cast<const float4*>(&sQ[wave][d4 * 4]);
-                acc = fmaf(qv.x, kv.x, acc);
-                acc = fmaf(qv.y, kv.y, acc);
-                acc = fmaf(qv.z, kv.z, acc);
-                acc = fmaf(qv.w, kv.w, acc);
-            }
-            sc = acc * scale;
-        }
-        const float tmax = wave_max(sc);
-        const float mnew = fmaxf(m, tmax);
-        const float p = valid ? expf(sc - mnew) : 0.f;
-        const float psum = wave_sum(p);
-        const float alpha = expf(m - mnew);
-        l = l * alpha + psum;
-        m = mnew;
+        for (int i = 0; i < DQ / 4; i++) kv[i] = kr[i];
 #pragma unroll
-        for (int e = 0; e < DPL; e++) o[e] *= alpha;
-        const int nk = min(64, s1 - kb);
-        for (int k = 0; k < nk; k++) {
-            const float pk = __shfl(p, k, 64);
-            const float* vr = Vc + (size_t)((kb + k) % cap) * kvd + kvh * HD + lane * DPL;
+        for (int k = 0; k < ATT_CH; k++) {
+            int kp = k0 + (k < kn ? k : 0);
+            kp = kp < 0 ? 0 : kp;
+            const float* vr = Vc + (size_t)(kp % cap) * kvd + kvh * HD + lane * DPL;
             if (DPL == 2) {
-                float2 v = *reinterpret_cast<const float2*>(vr);
-                o[0] = fmaf(pk, v.x, o[0]);
-                o[DPL - 1] = fmaf(pk, v.y, o[DPL - 1]);
+                const float2 t = *reinterpret_cast<const float2*>(vr);
+                vv[k][0] = t.x;
+                vv[k][DPL - 1] = t.y;
             } else {
-#pragma unroll
-                for (int e = 0; e < DPL; e++) o[e] = fmaf(pk, vr[e], o[e]);
+                vv[k][0] = vr[0];
             }
         }
     }
+    for (int e = tid; e < hpk * HD; e += 1024) sQ[e / HD][e % HD] = q[(size_t)(kvh * hpk) * HD + e];
+    __syncthreads();
+    if (DBG == 3) {
+        if (lane == 0) out[wave] = kv[0].x + vv[3][0];
+        return;
+    }
+
+    float sc[4];
 #pragma unroll
-    for (int e = 0; e < DPL; e++) pp[lane * DPL + e] = o[e];
+    for (int h = 0; h < 4; h++) {
+        float acc = 0.f;
+        if (h < hpk) {
+#pragma unroll
+            for (int i = 0; i < DQ / 4; i++) {
+                const float4 qv = *reinterpret_cast<const float4*>(&sQ[h][dq * DQ + 4 * i]);
+                acc = fmaf(qv.x, kv[i].x, acc);
+                acc = fmaf(qv.y, kv[i].y, acc);
+                acc = fmaf(qv.z, kv[i].z, acc);
+                acc = fmaf(qv.w, kv[i].w, acc);
+            }
+        }
+        acc += __shfl_xor(acc, 16, 64);
+        acc += __shfl_xor(acc, 32, 64);
+        sc[h] = (kk < kn) ? acc * scale : -INFINITY;
+    }
+    float m[4], l[4], p[4], o[4][DPL];
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const float mx = row_max16(sc[h]);
+        m[h] = (kn > 0) ? mx : -1e30f;
+        p[h] = (kk < kn) ? expf(sc[h] - mx) : 0.f;
+        l[h] = row_sum16(p[h]);
+#pragma unroll
+        for (int e = 0; e < DPL; e++) o[h][e] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < ATT_CH; k++) {
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            // lane k holds key k's weight (zero past the valid keys): a scalar broadcast
+            const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[h]), k));
+#pragma unroll
+            for (int e = 0; e < DPL; e++) o[h][e] = fmaf(pk, vv[k][e], o[h][e]);
+        }
+    }
+    if (DBG == 1) {
+        out[tid] = o[0][0] + o[1][0] + m[0] + l[1];
+        return;
+    }
+    // ---- merge the waves (in LDS): factors once per (wave, head), then a 16-term sum ----
     if (lane == 0) {
-        pp[HD] = m;
-        pp[HD + 1] = l;
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            sM[wave][h] = m[h];
+            sL[wave][h] = l[h];
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 4; h++)
+        if (h < hpk)
+#pragma unroll
+            for (int e = 0; e < DPL; e++) sO[wave][h][lane * DPL + e] = o[h][e];
+    __syncthreads();
+    if (wave == 0) {
+        const int w = lane >> 2, h = lane & 3;  // 64 lanes = 16 waves x 4 heads
+        float M = -1e30f;
+#pragma unroll
+        for (int i = 0; i < ATT_WAVES; i++) M = fmaxf(M, sM[i][h]);
+        const float f = expf(sM[w][h] - M);
+        float den = f * sL[w][h];
+        den += __shfl_xor(den, 4, 64);
+        den += __shfl_xor(den, 8, 64);
+        den += __shfl_xor(den, 16, 64);
+        den += __shfl_xor(den, 32, 64);
+        sF[w][h] = f;
+        if (w == 0) {
+            sDen[h] = den;
+            sMax[h] = M;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < hpk * HD; e += 1024) {
+        const int h = e / HD, d = e % HD;
+        float num = 0.f;
+#pragma unroll
+        for (int w = 0; w < ATT_WAVES; w++) num = fmaf(sF[w][h], sO[w][h][d], num);
+        const float den = sDen[h];
+        const int hh = kvh * hpk + h;
+        if (S == 1) {
+            out[(size_t)hh * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
+        } else {
+            float* pp = part + ((size_t)hh * maxs + sb) * (HD + 2);
+            pp[d] = num;
+            if (d == 0) {
+                pp[HD] = sMax[h];
+                pp[HD + 1] = den;
+            }
+        }
     }
 }
 
 template <int HD>
-__global__ __launch_bounds__(HD) void k_attn_combine(const float* __restrict__ part, int nsplit,
-                                                     float* __restrict__ out) {
-    const int h = blockIdx.x, d = threadIdx.x;
-    const float* ph = part + (size_t)h * nsplit * (HD + 2);
-    float M = -1e30f;
-    for (int s = 0; s < nsplit; s++) M = fmaxf(M, ph[(size_t)s * (HD + 2) + HD]);
-    float num = 0.f, den = 0.f;
-    for (int s = 0; s < nsplit; s++) {
-        const float* p = ph + (size_t)s * (HD + 2);
-        const float ls = p[HD + 1];
-        if (ls == 0.f) continue;
-        const float f = expf(p[HD] - M);
-        num = fmaf(f, p[d], num);
-        den = fmaf(f, ls, den);
+__global__ __launch_bounds__(256) void k_attn_combine(const float* __restrict__ part, int maxs,
+                                                      const int* __restrict__ state, int pos_host,
+                                                      int window, float* __restrict__ out) {
+    __shared__ float sf[64];
+    __shared__ float sden;
+    const int h = blockIdx.x, tid = threadIdx.x;
+    const int lp = state ? state[0] : pos_host;
+    const int L = min(lp + 1, window);
+    const int P = (L + ATT_BK - 1) / ATT_BK;
+    if (P <= 1) return;  // the attention blocks already wrote the output
+    const float* ph = part + (size_t)h * maxs * (HD + 2);
+    if (tid < 64) {
+        float mx = -INFINITY;
+        for (int i = tid; i < P; i += 64) mx = fmaxf(mx, ph[(size_t)i * (HD + 2) + HD]);
+        mx = wave_max(mx);
+        float den = 0.f;
+        for (int i = tid; i < P; i += 64) {
+            const float f = expf(ph[(size_t)i * (HD + 2) + HD] - mx);
+            sf[i] = f;
+            den = fmaf(f, ph[(size_t)i * (HD + 2) + HD + 1], den);
+        }
+        den = wave_sum(den);
+        if (tid == 0) sden = den;
     }
-    out[(size_t)h * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
+    __syncthreads();
+    for (int d = tid; d < HD; d += 256) {
+        float num = 0.f;
+        for (int i = 0; i < P; i++) num = fmaf(sf[i], ph[(size_t)i * (HD + 2) + d], num);
+        out[(size_t)h * HD + d] = sden > 0.f ? num * (1.0f / sden) : 0.f;
+    }
 }
 
 // ============================================================================
@@ -610,14 +791,21 @@ __global__ __launch_bounds__(256) void k_embed_rows(const float* __restrict__ ad
     for (int i = threadIdx.x; i < D; i += 256) x[(size_t)r * D + i] = a[i] + bf2f(e[i]);
 }
 
-// Final argmax over per-block partials; advance the device-side step state:
-// state = {logical kv pos, next adapter row, prev token, step index}
+// Final argmax over per-block partials; advance the device-side step state
+// state = {logical kv pos, next adapter row, prev token, step index} and, when adapter is
+// given, build the next step's input x = adapter[row] + tok_emb[token] (voxtral.c:
+// 1106-1113) so the next replay starts with its first GEMV.
 __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ pv,
                                                       const int* __restrict__ pi, int n,
                                                       int* __restrict__ state,
-                                                      int* __restrict__ tokens, int tokens_cap) {
+                                                      int* __restrict__ tokens, int tokens_cap,
+                                                      const float* __restrict__ adapter,
+                                                      int adapter_rows,
+                                                      const uint16_t* __restrict__ emb, int D,
+                                                      float* __restrict__ x) {
     __shared__ float sv[256];
     __shared__ int si[256];
+    __shared__ int stok, srow;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
     for (int i = threadIdx.x; i < n; i += 256) {
@@ -648,6 +836,14 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
         state[1] += 1;
         state[2] = tok;
         state[3] = step + 1;
+        stok = tok;
+        srow = state[1];
+    }
+    __syncthreads();
+    if (adapter && srow < adapter_rows) {
+        const float* a = adapter + (size_t)srow * D;
+        const uint16_t* e = emb + (size_t)stok * D;
+        for (int i = threadIdx.x; i < D; i += 256) x[i] = a[i] + bf2f(e[i]);
     }
 }
 
@@ -742,44 +938,75 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
     return hipSuccess;
 }
 
-int gemv_grid(int units) {
-    int g = (units + 3) / 4;
-    if (g > GEMV_MAX_BLOCKS) g = GEMV_MAX_BLOCKS;
-    return g < 1 ? 1 : g;
+static int gemv_rb(int rows) { return rows >= 4096 && rows % 8 == 0 ? 8 : 4; }
+
+int gemv_grid(int rows) {
+    // the largest divisor of the group count that fits 4 blocks per CU: every block then
+    // runs the same number of groups (no tail)
+    const int ng = rows / gemv_rb(rows);
+    int best = 1;
+    for (int gsz = 1; gsz <= GEMV_MAX_BLOCKS && gsz <= ng; gsz++)
+        if (ng % gsz == 0) best = gsz;
+    if (best < 256 && ng > GEMV_MAX_BLOCKS) best = GEMV_MAX_BLOCKS;  // no good divisor: accept a tail
+    return best;
+}
+
+template <int P, int E, int RB>
+static hipError_t gemv_k(const GemvArgs& a, int grid, hipStream_t st) {
+    const int kq = ((a.K >> 3) + 255) / 256;
+    switch (kq) {
+#define KQ_CASE(Q) case Q: hipLaunchKernelGGL((k_gemv<P, E, RB, Q>), dim3(grid), dim3(256), 0, st, a); break;
+        KQ_CASE(1) KQ_CASE(2) KQ_CASE(3) KQ_CASE(4) KQ_CASE(5)
+#undef KQ_CASE
+        default: return hipErrorInvalidValue;
+    }
+    LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
-    const int grid = gemv_grid(a.units);
-    const size_t lds = (size_t)a.K * sizeof(float);
-    if (a.K % 8) return hipErrorInvalidValue;
+    const int rb = gemv_rb(a.rows);
+    if (a.K % 8 || a.rows % rb) return hipErrorInvalidValue;
+    const int grid = gemv_grid(a.rows);
 #define GEMV_CASE(P, E) \
-    if (pro == P && epi == E) { hipLaunchKernelGGL((k_gemv<P, E>), dim3(grid), dim3(256), lds, st, a); LAUNCH_CHECK(); return hipSuccess; }
-    GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_STORE)
-    GEMV_CASE(PRO_NORM, EPI_QKV) GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_SWIGLU)
-    GEMV_CASE(PRO_NONE, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS) GEMV_CASE(PRO_NONE, EPI_LOGITS)
-    GEMV_CASE(PRO_NONE, EPI_QKV)
+    if (pro == P && epi == E) return rb == 8 ? gemv_k<P, E, 8>(a, grid, st) : gemv_k<P, E, 4>(a, grid, st);
+    GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_QKV)
+    GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS)
 #undef GEMV_CASE
     return hipErrorInvalidValue;
 }
 
+int attn_maxch(int window) { return (window + ATT_BK - 1) / ATT_BK; }
+
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
-                              int KVH, int nsplit, float* part, float* out, hipStream_t st) {
-    dim3 grid(nsplit, KVH);
-    if (H / KVH > 4) return hipErrorInvalidValue;
+                              int KVH, float* part, float* out, int with_combine, hipStream_t st) {
+    const int maxs = attn_maxch(window);
+    if (H / KVH > 4 || maxs > 64) return hipErrorInvalidValue;
+    dim3 grid(with_combine ? maxs : 1, KVH);
     if (hd == 128) {
-        hipLaunchKernelGGL(k_attn_decode<128>, grid, dim3(256), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, nsplit, part);
+        hipLaunchKernelGGL(k_attn_decode<128>, grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, maxs, part, out);
         LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_attn_combine<128>, dim3(H), dim3(128), 0, st, part, nsplit, out);
+        if (with_combine)
+            hipLaunchKernelGGL(k_attn_combine<128>, dim3(H), dim3(256), 0, st, part, maxs, state, pos_host, window, out);
     } else if (hd == 64) {
-        hipLaunchKernelGGL(k_attn_decode<64>, grid, dim3(256), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, nsplit, part);
+        hipLaunchKernelGGL(k_attn_decode<64>, grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, maxs, part, out);
         LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_attn_combine<64>, dim3(H), dim3(64), 0, st, part, nsplit, out);
+        if (with_combine)
+            hipLaunchKernelGGL(k_attn_combine<64>, dim3(H), dim3(256), 0, st, part, maxs, state, pos_host, window, out);
     } else {
         return hipErrorInvalidValue;
     }
     LAUNCH_CHECK();
     return hipSuccess;
+}
+
+hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
+                           const int* state, float* part, float* out, hipStream_t st) {
+    dim3 grid(1, 8);
+    if (dbg == 1) hipLaunchKernelGGL((k_attn_decode<128, 1>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
+    if (dbg == 3) hipLaunchKernelGGL((k_attn_decode<128, 3>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_embed_step(const float* adapter, const uint16_t* emb, const int* state, int D,
@@ -798,8 +1025,10 @@ hipError_t launch_embed_rows(const float* adapter, const uint16_t* emb, int row0
 }
 
 hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
-                               int cap, hipStream_t st) {
-    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, pv, pi, n, state, tokens, cap);
+                               int cap, const float* adapter, int adapter_rows,
+                               const uint16_t* emb, int D, float* x, hipStream_t st) {
+    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, pv, pi, n, state, tokens, cap,
+                       adapter, adapter_rows, emb, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -76,6 +76,10 @@ TINY = VoxConfig(enc_dim=256, enc_layers=2, enc_heads=4, enc_kv_heads=4, enc_hea
                  dec_kv_heads=2, dec_head_dim=128, dec_hidden=512, dec_window=48,
                  vocab=4096, ada_dim=32)
 
+# TINY with the real windows (750 / 8192): long streams exercise the multi-block decode
+# attention path (more than 256 visible keys) and the encoder window.
+TINY_LONG = dataclasses.replace(TINY, enc_window=750, dec_window=8192)
+
 ENC = "mm_streams_embeddings.embedding_module.whisper_encoder"
 EMB = "mm_streams_embeddings.embedding_module"
 

@@ -12,6 +12,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libvoxtral_hip.so)")
     config.addinivalue_line("markers", "slow: full-size Voxtral-4B shapes (minutes)")
+    config.addinivalue_line("markers", "cpu: runs without a GPU")
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,46 @@
+"""CPU: the multi-process harness of bench.py (one rank per GPU, replicas; gloo carries the
+barrier and the max/sum over ranks) with world_size 2."""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.cpu
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_dist_world2(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, sys, json
+        sys.path.insert(0, {ROOT!r})
+        from bench import Dist
+        d = Dist(2)
+        d.barrier()
+        mx = d.max(1.5 + d.rank)
+        sm = d.sum(10 * (d.rank + 1))
+        print(json.dumps({{"rank": d.rank, "world": d.world, "max": mx, "sum": sm}}))
+    """))
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(script)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+    outs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert sorted(o["rank"] for o in outs) == [0, 1]
+    for o in outs:
+        assert o["world"] == 2 and o["max"] == 2.5 and o["sum"] == 30.0

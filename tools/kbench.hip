@@ -85,14 +85,17 @@ int main(int argc, char** argv) {
     add("gemv wo   (3072x4096, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ * 2);
     add("gemv w13  (18432x3072, norm+swiglu)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
     add("gemv w2   (3072x9216, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH * 2);
+    add("gemv w13 same buffer (MALL-hot)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[0], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
+    add("gemv wo same buffer (MALL-hot)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[0], DQ, D); }, iters, st), (double)D * DQ * 2);
     add("gemv lm   (131072x3072, logits)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D * 2);
     for (int L : {64, 187, 256, 1000, 4096, 8192}) {
         int st4[4] = {L - 1, 0, 0, 0};
         CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
         char nm[64];
         snprintf(nm, sizeof nm, "attn decode L=%d", L);
-        const int comb = L > ATT_BLOCK_KEYS;
-        add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, comb, st)); }, iters, st),
+        int splits = 1;
+        while (splits * ATT_BLOCK_KEYS < L) splits *= 2;
+        add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, splits, st)); }, iters, st),
             (double)L * DKV * 2 * 4);
     }
     {
@@ -100,6 +103,44 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
         add("attn L=64 dbg1 (no merge)", timeit([&] { CK(launch_attn_dbg(1, x, Kc, Vc, cap, state, part, y, st)); }, iters, st), 1.0);
         add("attn L=64 dbg3 (loads+q only)", timeit([&] { CK(launch_attn_dbg(3, x, Kc, Vc, cap, state, part, y, st)); }, iters, st), 1.0);
+    }
+    {
+        int st4[4] = {186, 0, 0, 0};
+        CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
+        double acc[8] = {0}, cyc = 0, rt = 0, spread = 0, gstart = 0;
+        int nrun = 20;
+        for (int r = 0; r < nrun; r++) {
+            CK(launch_attn_dbg(4, x, Kc, Vc, cap, state, part, y, st));
+            CK(hipStreamSynchronize(st));
+            std::vector<unsigned long long> h(32 * 16 * 10);
+            CK(hipMemcpy(h.data(), part, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long g0 = ~0ull, g1 = 0;
+            for (int b = 0; b < 32; b++) {
+                unsigned long long mn = ~0ull, mx = 0;
+                for (int w = 0; w < 12; w++) {
+                    const unsigned long long* t = &h[(b * 16 + w) * 10];
+                    acc[0] += t[6] - t[0];  // issue K/V
+                    acc[1] += t[7] - t[6];  // q load + all loads landed
+                    acc[2] += t[1] - t[7];  // barrier wait
+                    acc[3] += t[2] - t[1];
+                    acc[4] += t[3] - t[2];
+                    acc[5] += t[4] - t[3];
+                    acc[6] += t[5] - t[4];
+                    cyc += t[5] - t[0];
+                    rt += t[9] - t[8];
+                    mn = std::min(mn, t[0]);
+                    mx = std::max(mx, t[0]);
+                    g0 = std::min(g0, t[8]);
+                    g1 = std::max(g1, t[8]);
+                }
+                spread += mx - mn;
+            }
+            gstart += g1 - g0;
+        }
+        const double n = nrun * 384.0;
+        printf("attn L=187 per-wave cycles: issue %.0f | loads land %.0f | barrier %.0f | QK/sm/PV %.0f | sO+sync %.0f | factors %.0f | merge %.0f ; total %.0f cyc = %.2f us (clk %.2f GHz); wave-start spread in block %.0f cyc; block start spread %.2f us\n",
+               acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, cyc / n, rt / n / 100.0,
+               cyc / (rt / 100.0) / 1000.0, spread / (nrun * 32.0), gstart / nrun / 100.0);
     }
     add("argmax+embed", timeit([&] { CK(launch_argmax_final(pv, pi, 1024, state, nullptr, 0, (float*)emb, 1024, emb, D, x, st)); }, iters, st), 1.0);
     add("empty-ish (embed step)", timeit([&] { CK(launch_embed_step((float*)emb, emb, state, D, x, st)); }, iters, st), 1.0);
@@ -109,7 +150,7 @@ int main(int argc, char** argv) {
     double t = timeit([&] {
         int l = layer++ % NL;
         gemv(PRO_NORM, EPI_QKV, wqkv[l], D, DQ + 2 * DKV);
-        CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, 0, st));
+        CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, 1, st));
         gemv(PRO_NONE, EPI_RESID, wo[l], DQ, D);
         gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[l], D, 2 * DH);
         gemv(PRO_NONE, EPI_RESID, w2[l], DH, D);

@@ -400,7 +400,7 @@ struct vox_hip_stream {
     float *xd, *xnd, *qkvd, *qd_, *attd, *gated, *part, *logits, *pval;
     int *pidx, *state, *tokens;
     int dec_rows_cap, tokens_cap;
-    hipGraphExec_t step_exec[2];  // [0]: context <= ATT_BLOCK_KEYS (no combine), [1]: any
+    hipGraphExec_t step_exec[STEP_GRAPHS];  // [g]: attention with 2^g key splits (g = 0: no combine)
     int graph_ready;              // bit mask of built graphs
     int started, eos_seen, n_generated;
     int h_state[4];
@@ -510,7 +510,7 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
 extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     if (!s) return;
     if (s->st) hipStreamSynchronize(s->st);
-    for (int g = 0; g < 2; g++)
+    for (int g = 0; g < STEP_GRAPHS; g++)
         if (s->step_exec[g]) hipGraphExecDestroy(s->step_exec[g]);
     dfree(s->ek); dfree(s->ev); dfree(s->dk); dfree(s->dv);
     dfree(s->mel_p); dfree(s->mel_tail); dfree(s->c0_p); dfree(s->c0_tail); dfree(s->c0_res);
@@ -716,7 +716,7 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
 // state != nullptr: positions come from device state (graph mode);
 // otherwise pos/rope_row are host values (boundary twin).
 static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row,
-                               int with_combine) {
+                               int splits) {
     vox_hip_model_t* m = s->m;
     const vox_hip_config_t& c = m->c;
     const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
@@ -739,7 +739,7 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
         // attention over the last min(pos+1, window) keys (decoder.c:724-733)
         CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
-                              s->part, s->attd, with_combine, st));
+                              s->part, s->attd, splits, st));
         // wo + residual (decoder.c:735-740)
         memset(&a, 0, sizeof a);
         a.x = s->attd; a.K = DQ; a.W = L.wo; a.rows = DD; a.y = s->xd;
@@ -767,9 +767,22 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
     return 0;
 }
 
-static int enqueue_graph_step(vox_hip_stream_t* s, int with_combine) {
+// Step graph g serves contexts of up to 2^g * ATT_BLOCK_KEYS keys (the last one: the whole
+// window); graph 0 runs one attention block per query head and no combine kernel.
+static int graph_splits(const vox_hip_stream_t* s, int g) {
+    return std::min(1 << g, attn_maxch(s->m->c.dec_window));
+}
+
+static int graph_index(const vox_hip_stream_t* s, int ctx) {
+    const int need = (ctx + ATT_BLOCK_KEYS - 1) / ATT_BLOCK_KEYS;
+    int g = 0;
+    while ((1 << g) < need && (1 << g) < attn_maxch(s->m->c.dec_window)) g++;
+    return g;
+}
+
+static int enqueue_graph_step(vox_hip_stream_t* s, int splits) {
     const vox_hip_config_t& c = s->m->c;
-    if (enqueue_step_layers(s, s->state, 0, nullptr, with_combine)) return -1;
+    if (enqueue_step_layers(s, s->state, 0, nullptr, splits)) return -1;
     CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), s->state, s->tokens, s->tokens_cap,
                            s->adapter, s->adapter_cap, s->m->tok_emb, c.dec_dim, s->xd, s->st));
     return 0;
@@ -787,7 +800,7 @@ static int build_step_graph(vox_hip_stream_t* s, int gi) {
     hipGraph_t g = nullptr;
     CK(hipStreamBeginCapture(s->st, hipStreamCaptureModeThreadLocal));
     s->capturing = 1;
-    int rc = enqueue_graph_step(s, gi);
+    int rc = enqueue_graph_step(s, graph_splits(s, gi));
     s->capturing = 0;
     hipError_t e = hipStreamEndCapture(s->st, &g);
     if (rc || e != hipSuccess) {
@@ -826,11 +839,12 @@ static int use_graphs() {
     return v;
 }
 
-// n steps starting at logical kv position pos0 (host mirror): while every step's context
-// fits one attention block the graph without the combine kernel is replayed.
+// n steps starting at logical kv position pos0 (host mirror): the replayed graph is the one
+// with the fewest attention key splits that covers the longest context of the n steps.
 static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
     const vox_hip_config_t& c = s->m->c;
-    const int gi = (std::min(pos0 + n, c.dec_window) <= ATT_BLOCK_KEYS) ? 0 : 1;
+    const int gi = graph_index(s, std::min(pos0 + n, c.dec_window));
+    const int splits = graph_splits(s, gi);
     if (!use_graphs()) {
         // eager launches of the same device-state kernels (profilers that cannot follow
         // graph replays; VOX_HIP_GRAPH=0)
@@ -840,7 +854,7 @@ static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
         }
         s->graph_prof = s->profiling;
         for (int i = 0; i < n; i++)
-            if (enqueue_graph_step(s, gi)) return -1;
+            if (enqueue_graph_step(s, splits)) return -1;
         return 0;
     }
     if (s->graph_ready && s->graph_prof != s->profiling) s->graph_ready = 0;
@@ -1118,7 +1132,9 @@ extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_
                                          float* logits) {
     const vox_hip_config_t& c = s->m->c;
     if (upload_rope_rows(s, rope_freqs, (size_t)c.dec_head_dim)) return -1;
-    if (enqueue_step_layers(s, nullptr, logical_pos, s->rope_rows, 1)) return -1;
+    const int ctx = std::min(logical_pos + 1, c.dec_window);
+    if (enqueue_step_layers(s, nullptr, logical_pos, s->rope_rows, (ctx + ATT_BLOCK_KEYS - 1) / ATT_BLOCK_KEYS))
+        return -1;
     // argmax into a scratch state so the graph-mode device state is untouched
     int* tmp_state = s->tokens + s->tokens_cap - 8;
     int st4[4] = {0, 0, 0, 0};

@@ -48,8 +48,9 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st);
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
-                              int KVH, float* part, float* out, int with_combine, hipStream_t st);
+                              int KVH, float* part, float* out, int splits, hipStream_t st);
 constexpr int ATT_BLOCK_KEYS = 256;  // keys one decode-attention block covers
+constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st);
 hipError_t launch_embed_step(const float* adapter, const uint16_t* emb, const int* state, int D,

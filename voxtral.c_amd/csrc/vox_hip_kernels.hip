@@ -572,18 +572,21 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 // ============================================================================
 // Decode attention (one query per head, GQA group of <= 4 heads per kv head).
 // Keys: the last min(lp+1, window) logical positions (voxtral_decoder.c:731-733 after
-// compaction; voxtral_kernels.c:554-560).  A block owns up to 256 consecutive keys of
-// one kv head; each wave walks 64 of them in 16-key chunks (lanes = key x quarter of
-// head_dim for Q.K, lanes = dims for P.V, every K/V load shared by the GQA heads) with an
-// online softmax; the 4 waves merge in LDS.  With one block per kv head (L <= 256) the
-// block writes the attention output directly; otherwise it writes an (o, m, l) partial
-// and k_attn_combine merges the blocks.
+// compaction; voxtral_kernels.c:554-560).  A block owns up to 256 consecutive keys and HPB
+// query heads of one kv head; each of its 16 waves takes 16 keys (lanes = key x quarter of
+// head_dim for Q.K, lanes = dims for P.V, every K/V load shared by the block's heads) and
+// the waves merge in LDS.  HPB = 1 (short contexts): one block per query head, so the
+// Q.K / P.V issue work of a kv head spreads over 4 CUs; the grid's y index is laid out so
+// that the 4 blocks of one kv head land on one XCD (blocks b and b+8 share an L2) and read
+// the K/V rows through the same L2.  HPB = 4 (long contexts): one block per kv head and
+// 256-key split, K/V read once.  With one split the block writes the attention output
+// directly; otherwise it writes an (o, m, l) partial and k_attn_combine merges the splits.
 // ============================================================================
 constexpr int ATT_CH = 16;      // keys per wave
 constexpr int ATT_WAVES = 16;   // waves per block (1024 threads)
 constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per block
 
-template <int HD, int DBG = 0>
+template <int HD, int HPB, int DBG = 0>
 __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ q,
                                                       const float* __restrict__ Kc,
                                                       const float* __restrict__ Vc, int cap,
@@ -593,36 +596,50 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ 
                                                       float* __restrict__ out) {
     constexpr int DQ = HD / 4;   // dims per lane for Q.K
     constexpr int DPL = HD / 64; // dims per lane for P.V
-    __shared__ __attribute__((aligned(16))) float sQ[4][HD];
+    __shared__ __attribute__((aligned(16))) float sQ[HPB][HD];
     __shared__ float sM[ATT_WAVES][4], sL[ATT_WAVES][4], sF[ATT_WAVES][4];
     __shared__ float sDen[4], sMax[4];
-    __shared__ __attribute__((aligned(16))) float sO[ATT_WAVES][4][HD];
-    const int kvh = blockIdx.y, sb = blockIdx.x;
+    __shared__ __attribute__((aligned(16))) float sO[ATT_WAVES][HPB][HD];
     const int hpk = H / KVH;
+    const int kvh = HPB == 1 ? (int)blockIdx.y % KVH : (int)blockIdx.y;
+    const int h0 = HPB == 1 ? kvh * hpk + (int)blockIdx.y / KVH : kvh * hpk;  // first query head
+    const int nh = HPB == 1 ? 1 : hpk;  // heads in this block (<= 4)
+    const int sb = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvd = KVH * HD;
+    unsigned long long ts[10];
+    if (DBG == 4) {
+        ts[0] = __builtin_amdgcn_s_memtime();
+        ts[8] = __builtin_amdgcn_s_memrealtime();
+    }
+    // the query does not depend on the step state: its load goes out first
+    float qreg = 0.f;
+    if (tid < nh * HD) qreg = q[(size_t)h0 * HD + tid];
     const int lp = state ? state[0] : pos_host;
     const int L = min(lp + 1, window);
     const int first = lp - L + 1;
     const int S = (L + ATT_BK - 1) / ATT_BK;
     if (sb >= S) return;  // uniform per block
-    const int k0 = first + sb * ATT_BK + wave * ATT_CH;
+    const int k0 = first + sb * ATT_BK + wave * ATT_CH;  // >= 0
     const int kn = min(ATT_CH, lp + 1 - k0);  // may be <= 0 for trailing waves
     const int kk = lane & 15, dq = lane >> 4;
+    // ring slots: one modulo per wave, then a wrap test per key
+    const int slot0 = k0 % cap;
 
-    // K quarter-rows and V dims for this wave's 16 keys: issued before anything else
+    // K quarter-rows and V dims for this wave's 16 keys
     float4 kv[DQ / 4];
     float vv[ATT_CH][DPL];
     {
-        const int key = k0 + (kk < kn ? kk : 0);
-        const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)((key < 0 ? 0 : key) % cap) * kvd + kvh * HD + dq * DQ);
+        int sk = slot0 + (kk < kn ? kk : 0);
+        sk = sk >= cap ? sk - cap : sk;
+        const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)sk * kvd + kvh * HD + dq * DQ);
 #pragma unroll
         for (int i = 0; i < DQ / 4; i++) kv[i] = kr[i];
 #pragma unroll
         for (int k = 0; k < ATT_CH; k++) {
-            int kp = k0 + (k < kn ? k : 0);
-            kp = kp < 0 ? 0 : kp;
-            const float* vr = Vc + (size_t)(kp % cap) * kvd + kvh * HD + lane * DPL;
+            int sv = slot0 + (k < kn ? k : 0);
+            sv = sv >= cap ? sv - cap : sv;
+            const float* vr = Vc + (size_t)sv * kvd + kvh * HD + lane * DPL;
             if (DPL == 2) {
                 const float2 t = *reinterpret_cast<const float2*>(vr);
                 vv[k][0] = t.x;
@@ -632,18 +649,24 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ 
             }
         }
     }
-    for (int e = tid; e < hpk * HD; e += 1024) sQ[e / HD][e % HD] = q[(size_t)(kvh * hpk) * HD + e];
+    if (DBG == 4) ts[6] = __builtin_amdgcn_s_memtime();
+    if (tid < nh * HD) sQ[tid / HD][tid % HD] = qreg;
+    if (DBG == 4) {
+        __builtin_amdgcn_s_waitcnt(0);
+        ts[7] = __builtin_amdgcn_s_memtime();
+    }
     __syncthreads();
+    if (DBG == 4) ts[1] = __builtin_amdgcn_s_memtime();
     if (DBG == 3) {
         if (lane == 0) out[wave] = kv[0].x + vv[3][0];
         return;
     }
 
-    float sc[4];
+    float sc[HPB];
 #pragma unroll
-    for (int h = 0; h < 4; h++) {
+    for (int h = 0; h < HPB; h++) {
         float acc = 0.f;
-        if (h < hpk) {
+        if (h < nh) {
 #pragma unroll
             for (int i = 0; i < DQ / 4; i++) {
                 const float4 qv = *reinterpret_cast<const float4*>(&sQ[h][dq * DQ + 4 * i]);
@@ -657,9 +680,9 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ 
         acc += __shfl_xor(acc, 32, 64);
         sc[h] = (kk < kn) ? acc * scale : -INFINITY;
     }
-    float m[4], l[4], p[4], o[4][DPL];
+    float m[HPB], l[HPB], p[HPB], o[HPB][DPL];
 #pragma unroll
-    for (int h = 0; h < 4; h++) {
+    for (int h = 0; h < HPB; h++) {
         const float mx = row_max16(sc[h]);
         m[h] = (kn > 0) ? mx : -1e30f;
         p[h] = (kk < kn) ? expf(sc[h] - mx) : 0.f;
@@ -670,7 +693,7 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ 
 #pragma unroll
     for (int k = 0; k < ATT_CH; k++) {
 #pragma unroll
-        for (int h = 0; h < 4; h++) {
+        for (int h = 0; h < HPB; h++) {
             // lane k holds key k's weight (zero past the valid keys): a scalar broadcast
             const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[h]), k));
 #pragma unroll
@@ -678,48 +701,53 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ 
         }
     }
     if (DBG == 1) {
-        out[tid] = o[0][0] + o[1][0] + m[0] + l[1];
+        out[tid] = o[0][0] + m[0] + l[0];
         return;
     }
+    if (DBG == 4) ts[2] = __builtin_amdgcn_s_memtime();
     // ---- merge the waves (in LDS): factors once per (wave, head), then a 16-term sum ----
     if (lane == 0) {
 #pragma unroll
-        for (int h = 0; h < 4; h++) {
+        for (int h = 0; h < HPB; h++) {
             sM[wave][h] = m[h];
             sL[wave][h] = l[h];
         }
     }
 #pragma unroll
-    for (int h = 0; h < 4; h++)
-        if (h < hpk)
+    for (int h = 0; h < HPB; h++)
+        if (h < nh)
 #pragma unroll
             for (int e = 0; e < DPL; e++) sO[wave][h][lane * DPL + e] = o[h][e];
     __syncthreads();
+    if (DBG == 4) ts[3] = __builtin_amdgcn_s_memtime();
     if (wave == 0) {
-        const int w = lane >> 2, h = lane & 3;  // 64 lanes = 16 waves x 4 heads
-        float M = -1e30f;
+        const int w = lane >> 2, h = lane & 3;  // 64 lanes = 16 waves x 4 head slots
+        if (h < HPB) {
+            float M = -1e30f;
 #pragma unroll
-        for (int i = 0; i < ATT_WAVES; i++) M = fmaxf(M, sM[i][h]);
-        const float f = expf(sM[w][h] - M);
-        float den = f * sL[w][h];
-        den += __shfl_xor(den, 4, 64);
-        den += __shfl_xor(den, 8, 64);
-        den += __shfl_xor(den, 16, 64);
-        den += __shfl_xor(den, 32, 64);
-        sF[w][h] = f;
-        if (w == 0) {
-            sDen[h] = den;
-            sMax[h] = M;
+            for (int i = 0; i < ATT_WAVES; i++) M = fmaxf(M, sM[i][h]);
+            const float f = expf(sM[w][h] - M);
+            float den = f * sL[w][h];
+            den += __shfl_xor(den, 4, 64);
+            den += __shfl_xor(den, 8, 64);
+            den += __shfl_xor(den, 16, 64);
+            den += __shfl_xor(den, 32, 64);
+            sF[w][h] = f;
+            if (w == 0) {
+                sDen[h] = den;
+                sMax[h] = M;
+            }
         }
     }
     __syncthreads();
-    for (int e = tid; e < hpk * HD; e += 1024) {
+    if (DBG == 4) ts[4] = __builtin_amdgcn_s_memtime();
+    for (int e = tid; e < nh * HD; e += 1024) {
         const int h = e / HD, d = e % HD;
         float num = 0.f;
 #pragma unroll
         for (int w = 0; w < ATT_WAVES; w++) num = fmaf(sF[w][h], sO[w][h][d], num);
         const float den = sDen[h];
-        const int hh = kvh * hpk + h;
+        const int hh = h0 + h;
         if (S == 1) {
             out[(size_t)hh * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
         } else {
@@ -729,6 +757,14 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ 
                 pp[HD] = sMax[h];
                 pp[HD + 1] = den;
             }
+        }
+    }
+    if (DBG == 4) {
+        ts[5] = __builtin_amdgcn_s_memtime();
+        ts[9] = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            unsigned long long* d = reinterpret_cast<unsigned long long*>(part) + (size_t)(blockIdx.y * 16 + wave) * 10;
+            for (int i = 0; i < 10; i++) d[i] = ts[i];
         }
     }
 }
@@ -978,34 +1014,42 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
 
 int attn_maxch(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 
+// splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
+// step the launch serves); 1 -> one block per query head, no combine kernel.
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
-                              int KVH, float* part, float* out, int with_combine, hipStream_t st) {
+                              int KVH, float* part, float* out, int splits, hipStream_t st) {
     const int maxs = attn_maxch(window);
-    if (H / KVH > 4 || maxs > 64) return hipErrorInvalidValue;
-    dim3 grid(with_combine ? maxs : 1, KVH);
+    if (H % KVH || H / KVH > 4 || maxs > 64 || splits < 1 || splits > maxs) return hipErrorInvalidValue;
+#define VOX_ATT(HD)                                                                                  \
+    if (splits == 1) {                                                                               \
+        hipLaunchKernelGGL((k_attn_decode<HD, 1>), dim3(1, H), dim3(1024), 0, st, q, Kc, Vc, cap,   \
+                           state, pos_host, window, scale, H, KVH, maxs, part, out);                 \
+    } else {                                                                                         \
+        hipLaunchKernelGGL((k_attn_decode<HD, 4>), dim3(splits, KVH), dim3(1024), 0, st, q, Kc, Vc, \
+                           cap, state, pos_host, window, scale, H, KVH, maxs, part, out);            \
+        LAUNCH_CHECK();                                                                              \
+        hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H), dim3(256), 0, st, part, maxs, state,        \
+                           pos_host, window, out);                                                   \
+    }
     if (hd == 128) {
-        hipLaunchKernelGGL(k_attn_decode<128>, grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, maxs, part, out);
-        LAUNCH_CHECK();
-        if (with_combine)
-            hipLaunchKernelGGL(k_attn_combine<128>, dim3(H), dim3(256), 0, st, part, maxs, state, pos_host, window, out);
+        VOX_ATT(128)
     } else if (hd == 64) {
-        hipLaunchKernelGGL(k_attn_decode<64>, grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, pos_host, window, scale, H, KVH, maxs, part, out);
-        LAUNCH_CHECK();
-        if (with_combine)
-            hipLaunchKernelGGL(k_attn_combine<64>, dim3(H), dim3(256), 0, st, part, maxs, state, pos_host, window, out);
+        VOX_ATT(64)
     } else {
         return hipErrorInvalidValue;
     }
+#undef VOX_ATT
     LAUNCH_CHECK();
     return hipSuccess;
 }
-
+// diagnostic variants for tools/kbench (not used by the engine)
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st) {
-    dim3 grid(1, 8);
-    if (dbg == 1) hipLaunchKernelGGL((k_attn_decode<128, 1>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
-    if (dbg == 3) hipLaunchKernelGGL((k_attn_decode<128, 3>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
+    dim3 grid(1, 32);
+    if (dbg == 1) hipLaunchKernelGGL((k_attn_decode<128, 1, 1>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
+    if (dbg == 3) hipLaunchKernelGGL((k_attn_decode<128, 1, 3>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
+    if (dbg == 4) hipLaunchKernelGGL((k_attn_decode<128, 1, 4>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
     return hipGetLastError();
 }
 

@@ -86,6 +86,54 @@ void vo_linear_bf16(float *y, const float *x, const uint16_t *W, const float *b,
     }
 }
 
+/* q8_matvec_fused, voxtral_kernels.c:277-318 (non-NEON path): sum of int8->f32 weight
+ * times x in k order from 0, then y = sum * scale + bias. */
+static void matvec_q8(float *y, const float *x, const int8_t *W, const float *scales,
+                      const float *bias, int in_dim, int out_dim) {
+#pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)
+    for (int o = 0; o < out_dim; o++) {
+        const int8_t *w = W + (size_t)o * in_dim;
+        float sum = 0.0f;
+#pragma omp simd reduction(+ : sum)
+        for (int k = 0; k < in_dim; k++) sum += (float)w[k] * x[k];
+        y[o] = sum * scales[o] + (bias ? bias[o] : 0.0f);
+    }
+}
+
+/* vox_linear_q8 / vox_linear_nobias_q8 / vox_matmul_t_q8 (voxtral_kernels.c:320-393):
+ * M==1 fused matvec; M>1 dequantises W[r][c] = (float)q * scale[r] into f32 scratch and
+ * takes the f32 sgemm path (vox_linear / vox_linear_nobias / vox_matmul_t). */
+void vo_linear_q8(float *y, const float *x, const int8_t *W, const float *scales, const float *b,
+                  int M, int in_dim, int out_dim) {
+    if (M <= 0) return;
+    if (M == 1) { matvec_q8(y, x, W, scales, b, in_dim, out_dim); return; }
+    size_t n = (size_t)out_dim * in_dim;
+    if (n > g_scratch_cap) {
+        free(g_scratch);
+        g_scratch = (float *)malloc(n * sizeof(float));
+        g_scratch_cap = g_scratch ? n : 0;
+    }
+#pragma omp parallel for schedule(static) num_threads(g_threads) if (g_threads > 1)
+    for (int r = 0; r < out_dim; r++) {
+        const float sc = scales[r];
+        for (int c = 0; c < in_dim; c++) g_scratch[(size_t)r * in_dim + c] = (float)W[(size_t)r * in_dim + c] * sc;
+    }
+    scipy_cblas_sgemm(RowMajor, NoTrans, Trans, M, out_dim, in_dim, 1.0f, x, in_dim,
+                      g_scratch, in_dim, 0.0f, y, out_dim);
+    if (b) {
+        for (int s = 0; s < M; s++)
+            for (int o = 0; o < out_dim; o++) y[(size_t)s * out_dim + o] += b[o];
+    }
+}
+
+/* bf16 or q8 by the presence of a scale array (the reference branches on *_weight_q8) */
+static void lin(float *y, const float *x, const uint16_t *W, const float *scales, const float *b,
+                int M, int in_dim, int out_dim) {
+    if (scales) vo_linear_q8(y, x, (const int8_t *)(const void *)W, scales, b, M, in_dim, out_dim);
+    else vo_linear_bf16(y, x, W, b, M, in_dim, out_dim);
+}
+#define SC(field, l) (w->field ? w->field[l] : NULL)
+
 /* ------------------------------------------------------------------------
  * Element-wise / normalisation (voxtral_kernels.c:475-513)
  * ------------------------------------------------------------------------ */
@@ -528,9 +576,9 @@ int vo_encoder_incremental(vo_stream_t *s, float *x, int new_len) {
 
     for (int l = 0; l < c->enc_layers; l++) {
         vo_rms_norm(xn, x, w->enc_attn_norm[l], new_len, dim, c->enc_eps);
-        vo_linear_bf16(q, xn, w->enc_wq[l], w->enc_wq_b[l], new_len, dim, qd);
-        vo_linear_bf16(k, xn, w->enc_wk[l], NULL, new_len, dim, kvd);
-        vo_linear_bf16(v, xn, w->enc_wv[l], w->enc_wv_b[l], new_len, dim, kvd);
+        lin(q, xn, w->enc_wq[l], SC(enc_wq_s, l), w->enc_wq_b[l], new_len, dim, qd);
+        lin(k, xn, w->enc_wk[l], SC(enc_wk_s, l), NULL, new_len, dim, kvd);
+        lin(v, xn, w->enc_wv[l], SC(enc_wv_s, l), w->enc_wv_b[l], new_len, dim, kvd);
         vo_apply_rope(q, rope, new_len, H, hd);
         vo_apply_rope(k, rope, new_len, KVH, hd);
         float *kc = s->ek + l * lstride, *vc = s->ev + l * lstride;
@@ -538,14 +586,14 @@ int vo_encoder_incremental(vo_stream_t *s, float *x, int new_len) {
         memcpy(vc + (size_t)cache_len * kvd, v, sizeof(float) * (size_t)new_len * kvd);
         vo_causal_attention(att, q, kc, vc, new_len, cache_len + new_len, H, KVH, hd, scale,
                             c->enc_window, cache_len);
-        vo_linear_bf16(proj, att, w->enc_wo[l], w->enc_wo_b[l], new_len, qd, dim);
+        lin(proj, att, w->enc_wo[l], SC(enc_wo_s, l), w->enc_wo_b[l], new_len, qd, dim);
         for (size_t i = 0; i < (size_t)new_len * dim; i++) x[i] += proj[i];
         vo_rms_norm(xn, x, w->enc_ffn_norm[l], new_len, dim, c->enc_eps);
-        vo_linear_bf16(gate, xn, w->enc_w1[l], NULL, new_len, dim, hidden);
+        lin(gate, xn, w->enc_w1[l], SC(enc_w1_s, l), NULL, new_len, dim, hidden);
         vo_silu(gate, new_len * hidden);
-        vo_linear_bf16(up, xn, w->enc_w3[l], NULL, new_len, dim, hidden);
+        lin(up, xn, w->enc_w3[l], SC(enc_w3_s, l), NULL, new_len, dim, hidden);
         for (size_t i = 0; i < (size_t)new_len * hidden; i++) gate[i] *= up[i];
-        vo_linear_bf16(proj, gate, w->enc_w2[l], w->enc_w2_b[l], new_len, hidden, dim);
+        lin(proj, gate, w->enc_w2[l], SC(enc_w2_s, l), w->enc_w2_b[l], new_len, hidden, dim);
         for (size_t i = 0; i < (size_t)new_len * dim; i++) x[i] += proj[i];
     }
     vo_rms_norm(x, x, w->enc_norm, new_len, dim, c->enc_eps);
@@ -562,9 +610,9 @@ int vo_adapter(vo_model_t *m, const float *enc, int enc_rows, float *out) {
     int ds = enc_rows / c->downsample, dsd = c->enc_dim * c->downsample, D = c->dec_dim;
     if (ds <= 0) return 0;
     float *mid = (float *)malloc(sizeof(float) * (size_t)ds * D);
-    vo_linear_bf16(mid, enc, m->w.ad0, NULL, ds, dsd, D);
+    lin(mid, enc, m->w.ad0, m->w.ad0_s, NULL, ds, dsd, D);
     gelu_m(m, mid, ds * D);
-    vo_linear_bf16(out, mid, m->w.ad1, NULL, ds, D, D);
+    lin(out, mid, m->w.ad1, m->w.ad1_s, NULL, ds, D, D);
     free(mid);
     return ds;
 }
@@ -696,9 +744,9 @@ static void dec_layers(vo_stream_t *s, float *x, int seq, int start_pos, const f
     size_t lstride = (size_t)s->d_max * kvd;
     for (int l = 0; l < c->dec_layers; l++) {
         vo_rms_norm(xn, x, w->dec_attn_norm[l], seq, D, c->dec_eps);
-        vo_linear_bf16(q, xn, w->dec_wq[l], NULL, seq, D, qd);
-        vo_linear_bf16(k, xn, w->dec_wk[l], NULL, seq, D, kvd);
-        vo_linear_bf16(v, xn, w->dec_wv[l], NULL, seq, D, kvd);
+        lin(q, xn, w->dec_wq[l], SC(dec_wq_s, l), NULL, seq, D, qd);
+        lin(k, xn, w->dec_wk[l], SC(dec_wk_s, l), NULL, seq, D, kvd);
+        lin(v, xn, w->dec_wv[l], SC(dec_wv_s, l), NULL, seq, D, kvd);
         vo_apply_rope(q, rope, seq, H, hd);
         vo_apply_rope(k, rope, seq, KVH, hd);
         float *kc = s->dk + l * lstride, *vc = s->dv + l * lstride;
@@ -706,17 +754,17 @@ static void dec_layers(vo_stream_t *s, float *x, int seq, int start_pos, const f
         memcpy(vc + (size_t)start_pos * kvd, v, sizeof(float) * (size_t)seq * kvd);
         vo_causal_attention(att, q, kc, vc, seq, start_pos + seq, H, KVH, hd, scale,
                             c->dec_window, start_pos);
-        vo_linear_bf16(proj, att, w->dec_wo[l], NULL, seq, qd, D);
+        lin(proj, att, w->dec_wo[l], SC(dec_wo_s, l), NULL, seq, qd, D);
         for (size_t i = 0; i < (size_t)seq * D; i++) x[i] += proj[i];
         vo_rms_norm(xn, x, w->dec_ffn_norm[l], seq, D, c->dec_eps);
         const float *ada = m->ada_scale + (size_t)l * D;
         for (int r = 0; r < seq; r++)
             for (int i = 0; i < D; i++) xn[(size_t)r * D + i] *= (1.0f + ada[i]);
-        vo_linear_bf16(gate, xn, w->dec_w1[l], NULL, seq, D, hidden);
+        lin(gate, xn, w->dec_w1[l], SC(dec_w1_s, l), NULL, seq, D, hidden);
         vo_silu(gate, seq * hidden);
-        vo_linear_bf16(up, xn, w->dec_w3[l], NULL, seq, D, hidden);
+        lin(up, xn, w->dec_w3[l], SC(dec_w3_s, l), NULL, seq, D, hidden);
         for (size_t i = 0; i < (size_t)seq * hidden; i++) gate[i] *= up[i];
-        vo_linear_bf16(proj, gate, w->dec_w2[l], NULL, seq, hidden, D);
+        lin(proj, gate, w->dec_w2[l], SC(dec_w2_s, l), NULL, seq, hidden, D);
         for (size_t i = 0; i < (size_t)seq * D; i++) x[i] += proj[i];
     }
     free(xn); free(q); free(k); free(v); free(att); free(proj); free(gate); free(up);
@@ -757,7 +805,7 @@ int vo_decoder_forward(vo_stream_t *s, const float *embed, float *logits) {
     dec_layers(s, x, 1, pos, rope);
     s->d_len = pos + 1;
     vo_rms_norm(x, x, m->w.dec_norm, 1, D, c->dec_eps);
-    vo_linear_bf16(logits, x, m->w.tok_emb, NULL, 1, D, c->vocab);
+    lin(logits, x, m->w.tok_emb, m->w.tok_emb_s, NULL, 1, D, c->vocab);
     int best = 0;
     float bv = logits[0];
     for (int i = 1; i < c->vocab; i++)
@@ -766,12 +814,19 @@ int vo_decoder_forward(vo_stream_t *s, const float *embed, float *logits) {
     return best;
 }
 
-/* tok_embed_bf16_to_f32 (voxtral.c:434-441) + adapter add (voxtral.c:1106-1113) */
+/* tok_embed_bf16_to_f32 / tok_embed_q8_to_f32 (voxtral.c:434-451) + adapter add
+ * (voxtral.c:1106-1113) */
 static void step_embed(vo_stream_t *s, float *dst, int adapter_row, int token) {
     const vo_config_t *c = &s->m->c;
     int D = c->dec_dim;
-    const uint16_t *e = s->m->w.tok_emb + (size_t)token * D;
     const float *a = s->adapter + (size_t)adapter_row * D;
+    if (s->m->w.tok_emb_s) {
+        const int8_t *e = (const int8_t *)(const void *)s->m->w.tok_emb + (size_t)token * D;
+        const float sc = s->m->w.tok_emb_s[token];
+        for (int j = 0; j < D; j++) dst[j] = a[j] + (float)e[j] * sc;
+        return;
+    }
+    const uint16_t *e = s->m->w.tok_emb + (size_t)token * D;
     for (int j = 0; j < D; j++) dst[j] = a[j] + bf16f(e[j]);
 }
 

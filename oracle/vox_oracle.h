@@ -48,6 +48,12 @@ typedef struct {
     const uint16_t **dec_wq, **dec_wk, **dec_wv, **dec_wo, **dec_w1, **dec_w2, **dec_w3;
     const float **dec_attn_norm, **dec_ffn_norm, **dec_ada_down, **dec_ada_up;
     const float *dec_norm;
+    /* Q8 checkpoints (quantize.py; voxtral_safetensors.c:393-408, 457-468): a non-NULL
+     * per-row scale array selects the q8 path for that matrix, whose pointer above then
+     * addresses its int8 [out, in] data.  ada_down/up arrive dequantized (load_f32). */
+    const float **enc_wq_s, **enc_wk_s, **enc_wv_s, **enc_wo_s, **enc_w1_s, **enc_w2_s, **enc_w3_s;
+    const float *ad0_s, *ad1_s, *tok_emb_s;
+    const float **dec_wq_s, **dec_wk_s, **dec_wv_s, **dec_wo_s, **dec_w1_s, **dec_w2_s, **dec_w3_s;
 } vo_weights_t;
 
 typedef struct vo_model vo_model_t;
@@ -57,6 +63,9 @@ typedef struct vo_stream vo_stream_t;
 void vo_set_threads(int n);
 void vo_linear_bf16(float *y, const float *x, const uint16_t *W, const float *b,
                     int M, int in_dim, int out_dim);
+/* vox_linear_q8 / vox_linear_nobias_q8 / vox_matmul_t_q8 (voxtral_kernels.c:277-393) */
+void vo_linear_q8(float *y, const float *x, const int8_t *W, const float *scales, const float *b,
+                  int M, int in_dim, int out_dim);
 void vo_rms_norm(float *out, const float *x, const float *w, int M, int hidden, float eps);
 void vo_gelu(float *x, int n, int erf_mode);
 void vo_silu(float *x, int n);

@@ -41,6 +41,7 @@ def lib():
         sig = {
             "vo_set_threads": (None, [I]),
             "vo_linear_bf16": (None, [fp, fp, P, fp, I, I, I]),
+            "vo_linear_q8": (None, [fp, fp, P, fp, fp, I, I, I]),
             "vo_rms_norm": (None, [fp, fp, fp, I, I, F]),
             "vo_gelu": (None, [fp, I, I]), "vo_silu": (None, [fp, I]),
             "vo_causal_conv1d": (None, [fp, fp, fp, fp, I, I, I, I, I]),
@@ -84,6 +85,17 @@ def linear_bf16(x, W_bf16, bias=None):
     b = None if bias is None else np.ascontiguousarray(bias, np.float32)
     lib().vo_linear_bf16(f(y), f(x), np.ascontiguousarray(W_bf16).ctypes.data,
                          None if b is None else f(b), M, K, N)
+    return y
+
+
+def linear_q8(x, W_q8, scales, bias=None):
+    x = np.ascontiguousarray(x, np.float32)
+    M, K = x.shape
+    N = W_q8.shape[0]
+    y = np.empty((M, N), np.float32)
+    b = None if bias is None else np.ascontiguousarray(bias, np.float32)
+    lib().vo_linear_q8(f(y), f(x), np.ascontiguousarray(W_q8, np.int8).ctypes.data,
+                       f(np.ascontiguousarray(scales, np.float32)), None if b is None else f(b), M, K, N)
     return y
 
 

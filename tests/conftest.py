@@ -7,6 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "voxtral.c_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, GOLDEN)  # fixture builders (gen_*.py) are importable; their main() is not run
 
 
 def pytest_configure(config):

@@ -28,7 +28,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "voxtral.c_amd"))
-from vox_weights import TINY, synth_weights  # noqa: E402
+from vox_weights import TINY, quantize_q8, synth_weights  # noqa: E402
 
 REF = "/root/reference/python_simple_implementation.py"
 PIPE_CFG = dataclasses.replace(TINY, gelu_erf=1)
@@ -53,6 +53,17 @@ class SF:
     def get_tensor(self, name):
         a = np.ascontiguousarray(self.w.bf16(name))
         return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16)
+
+
+class SFQ8:
+    """The same over a Q8 checkpoint: every tensor as the reference C code sees it after
+    safetensors_get_f32 (voxtral_safetensors.c:393-408: (float)q * scale per row)."""
+
+    def __init__(self, w):
+        self.w = w
+
+    def get_tensor(self, name):
+        return torch.from_numpy(np.ascontiguousarray(self.w.f32(name)).copy())
 
 
 def pipeline_mel():
@@ -113,26 +124,32 @@ def main():
                        ADA_NORM_DIM=c.ada_dim).items():
         setattr(pr, k_, v_)
     wts = synth_weights(c, seed=PIPE_SEED)
-    sf = SF(wts)
     mel = pipeline_mel()
-    with torch.no_grad():
-        enc = pr.encoder_forward(torch.from_numpy(mel.T.copy()), None, sf)
-        ad = pr.adapter_forward(enc, sf)
-        dec = pr.Decoder(sf)
-        t_cond = pr.compute_time_embedding(6.0, c.dec_dim)
-        prompt = [pr.TOKEN_BOS] + [pr.TOKEN_STREAMING_PAD] * (32 + 6)
-        L = len(prompt)
-        pe = ad[:L] + dec.embed_tokens(torch.tensor(prompt))
-        dec.prefill(pe[:-1], t_cond)
-        lg0 = dec.forward_one(pe[-1], pos=L - 1, t_cond=t_cond)
-        t0 = int(lg0.argmax())
-        lg1 = dec.forward_one(ad[L] + dec.embed_token(t0), pos=L, t_cond=t_cond)
-        t1 = int(lg1.argmax())
-    out.update({"pipe_mel": mel, "pipe_enc": enc.numpy(), "pipe_adapter": ad.numpy(),
-                "pipe_logits": np.stack([lg0.numpy(), lg1.numpy()]), "pipe_tokens": np.array([t0, t1]),
-                "pipe_seed": np.array(PIPE_SEED)})
+
+    def pipeline(sf):
+        with torch.no_grad():
+            enc = pr.encoder_forward(torch.from_numpy(mel.T.copy()), None, sf)
+            ad = pr.adapter_forward(enc, sf)
+            dec = pr.Decoder(sf)
+            t_cond = pr.compute_time_embedding(6.0, c.dec_dim)
+            prompt = [pr.TOKEN_BOS] + [pr.TOKEN_STREAMING_PAD] * (32 + 6)
+            L = len(prompt)
+            pe = ad[:L] + dec.embed_tokens(torch.tensor(prompt))
+            dec.prefill(pe[:-1], t_cond)
+            lg0 = dec.forward_one(pe[-1], pos=L - 1, t_cond=t_cond)
+            t0 = int(lg0.argmax())
+            lg1 = dec.forward_one(ad[L] + dec.embed_token(t0), pos=L, t_cond=t_cond)
+            t1 = int(lg1.argmax())
+        return enc.numpy(), ad.numpy(), np.stack([lg0.numpy(), lg1.numpy()]), np.array([t0, t1])
+
+    enc, ad, lg, tk = pipeline(SF(wts))
+    out.update({"pipe_mel": mel, "pipe_enc": enc, "pipe_adapter": ad, "pipe_logits": lg,
+                "pipe_tokens": tk, "pipe_seed": np.array(PIPE_SEED)})
+    # Q8 checkpoint of the same weights (quantize.py restatement, pinned by q8_ref.json)
+    enc, ad, lg, tk = pipeline(SFQ8(quantize_q8(wts)))
+    out.update({"pipeq8_enc": enc, "pipeq8_adapter": ad, "pipeq8_logits": lg, "pipeq8_tokens": tk})
     np.savez_compressed(os.path.join(HERE, "pyref.npz"), **out)
-    print("wrote", len(out), "arrays; enc", enc.shape, "adapter", ad.shape, "tokens", t0, t1)
+    print("wrote", len(out), "arrays; tokens", out["pipe_tokens"], "q8 tokens", out["pipeq8_tokens"])
 
 
 if __name__ == "__main__":

@@ -53,3 +53,47 @@ void vox_bf16_to_f32(float *out, const uint16_t *in, size_t n) {
         memcpy(&out[i], &u, 4);
     }
 }
+
+/* Per-row symmetric int8 quantisation of a bf16 [rows, cols] matrix, restating the
+ * reference's quantize.py:35-46 (quantize_q8_row) and :96-125: amax = max|row| in f32;
+ * scale = f32(amax / 127.0 in double); q = round-half-even(row / scale) in f32, clipped to
+ * [-128, 127]; an all-zero row gets scale 0 and zeros.  Output layout as quantize.py
+ * writes it (safetensors.c:393-408): scales [rows] f32, then q [rows, cols] int8. */
+void vox_quantize_q8_bf16(const uint16_t *in, long long rows, long long cols, float *scales,
+                          int8_t *q) {
+#pragma omp parallel for schedule(dynamic, 16)
+    for (long long r = 0; r < rows; r++) {
+        const uint16_t *src = in + r * cols;
+        int8_t *dst = q + r * cols;
+        float amax = 0.0f;
+        for (long long c = 0; c < cols; c++) {
+            uint32_t u = ((uint32_t)src[c]) << 16;
+            float v;
+            memcpy(&v, &u, 4);
+            v = fabsf(v);
+            if (v > amax) amax = v;
+        }
+        if (amax == 0.0f) {
+            scales[r] = 0.0f;
+            memset(dst, 0, (size_t)cols);
+            continue;
+        }
+        const float s = (float)((double)amax / 127.0);
+        scales[r] = s;
+        for (long long c = 0; c < cols; c++) {
+            uint32_t u = ((uint32_t)src[c]) << 16;
+            float v;
+            memcpy(&v, &u, 4);
+            float t = rintf(v / s);
+            t = t < -128.0f ? -128.0f : (t > 127.0f ? 127.0f : t);
+            dst[c] = (int8_t)t;
+        }
+    }
+}
+
+/* (float)q * scale per row: safetensors_get_f32 of a Q8 tensor (safetensors.c:393-408) */
+void vox_dequant_q8(float *out, const int8_t *q, const float *scales, long long rows, long long cols) {
+#pragma omp parallel for schedule(static)
+    for (long long r = 0; r < rows; r++)
+        for (long long c = 0; c < cols; c++) out[r * cols + c] = (float)q[r * cols + c] * scales[r];
+}

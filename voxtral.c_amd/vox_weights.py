@@ -9,6 +9,11 @@ norms, biases, conv and ada weights are converted to f32 exactly as `load_f32` d
 The real checkpoint is not available offline, so `synth_weights` builds seeded random
 weights of the exact architecture (same bytes and FLOPs) with a counter-based hash
 (libvox_synth.so), fast enough to make the full 8.86 GB model in a few seconds.
+
+Q8 checkpoints (config 5) are what the reference's quantize.py writes: every 2-D tensor
+becomes dtype "Q8" = f32 per-row scales followed by int8 [rows, cols]; everything else
+becomes F32 (quantize.py:96-150).  `quantize_q8` restates that quantiser (in C,
+libvox_synth.so) and `load_safetensors` reads such files.
 """
 from __future__ import annotations
 
@@ -142,6 +147,10 @@ def synth_lib():
         lib.vox_synth_f32.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
                                       ctypes.c_float, ctypes.c_float]
         lib.vox_bf16_to_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        lib.vox_quantize_q8_bf16.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+        lib.vox_dequant_q8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_longlong, ctypes.c_longlong]
         _synth = lib
     return _synth
 
@@ -161,28 +170,69 @@ def f32_to_bf16(a: np.ndarray) -> np.ndarray:
 
 
 class Weights:
-    """bf16 tensors by checkpoint name (views into one buffer or an mmap) plus the f32
-    conversions the reference makes at load time."""
+    """Checkpoint tensors by name: bf16 tensors (views into one buffer or an mmap), or for
+    a Q8 checkpoint (scales, int8) pairs for the matrices and f32 for the rest; plus the
+    f32 conversions the reference makes at load time (load_f32 / safetensors_get_f32)."""
 
-    F32_KINDS = ("conv", "bias", "norm", "ada")
-
-    def __init__(self, cfg: VoxConfig, tensors: dict, keep=None):
+    def __init__(self, cfg: VoxConfig, tensors: dict, keep=None, q8=None, f32=None):
         self.cfg = cfg
-        self.t = tensors
+        self.t = tensors          # name -> uint16 (bf16 bits)
+        self.q8 = q8 or {}        # name -> (scales f32 [rows], q int8 [rows, cols])
+        self._stored_f32 = dict(f32 or {})  # F32 tensors of a Q8 checkpoint
         self._keep = keep
         self._f32 = {}
+
+    @property
+    def is_q8(self):
+        return bool(self.q8)
 
     def bf16(self, name):
         return self.t[name]
 
+    def matrix(self, name):
+        """(data, scales): bf16 bits and None, or int8 and per-row f32 scales."""
+        if name in self.q8:
+            s, q = self.q8[name]
+            return q, s
+        return self.t[name], None
+
     def f32(self, name):
+        if name in self._stored_f32:
+            return self._stored_f32[name]
         if name not in self._f32:
-            self._f32[name] = bf16_to_f32(self.t[name])
+            if name in self.q8:
+                s, q = self.q8[name]
+                out = np.empty(q.shape, np.float32)
+                synth_lib().vox_dequant_q8(out.ctypes.data, np.ascontiguousarray(q).ctypes.data,
+                                           np.ascontiguousarray(s).ctypes.data, q.shape[0], q.shape[1])
+                self._f32[name] = out
+            else:
+                self._f32[name] = bf16_to_f32(self.t[name])
         return self._f32[name]
 
     @property
     def nbytes(self):
-        return sum(v.nbytes for v in self.t.values())
+        return (sum(v.nbytes for v in self.t.values())
+                + sum(s.nbytes + q.nbytes for s, q in self.q8.values())
+                + sum(v.nbytes for v in self._stored_f32.values()))
+
+
+def quantize_q8(w: Weights) -> Weights:
+    """quantize.py (main, :96-150) on a bf16 checkpoint: 2-D tensors -> per-row int8 with
+    f32 scales (quantize_q8_row, :35-46), other tensors -> f32."""
+    lib = synth_lib()
+    q8, f32 = {}, {}
+    for name, a in w.t.items():
+        if a.ndim == 2:
+            a = np.ascontiguousarray(a)
+            rows, cols = a.shape
+            s = np.empty(rows, np.float32)
+            q = np.empty((rows, cols), np.int8)
+            lib.vox_quantize_q8_bf16(a.ctypes.data, rows, cols, s.ctypes.data, q.ctypes.data)
+            q8[name] = (s, q)
+        else:
+            f32[name] = bf16_to_f32(a)
+    return Weights(w.cfg, {}, q8=q8, f32=f32)
 
 
 def synth_weights(cfg: VoxConfig, seed: int = 0) -> Weights:
@@ -210,36 +260,65 @@ def synth_weights(cfg: VoxConfig, seed: int = 0) -> Weights:
 
 
 def load_safetensors(path: str, cfg: VoxConfig = VOXTRAL_4B) -> Weights:
-    """mmap a BF16 consolidated.safetensors (voxtral_safetensors.c:205-285, 446-451)."""
+    """mmap a consolidated.safetensors: BF16 tensors (voxtral_safetensors.c:205-285,
+    446-451), or the Q8 / F32 tensors quantize.py writes (:393-408, 457-468)."""
     f = open(path, "rb")
     mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
     hlen = int.from_bytes(mm[:8], "little")
     hdr = json.loads(mm[8:8 + hlen])
     base = 8 + hlen
-    tensors = {}
+    tensors, q8, f32 = {}, {}, {}
     for name, meta in hdr.items():
         if name == "__metadata__":
             continue
-        if meta["dtype"] != "BF16":
-            raise ValueError(f"{name}: dtype {meta['dtype']} unsupported (BF16 only)")
         s, e = meta["data_offsets"]
-        tensors[name] = np.frombuffer(mm, dtype=np.uint16, count=(e - s) // 2,
-                                      offset=base + s).reshape(meta["shape"])
-    return Weights(cfg, tensors, keep=(f, mm))
+        shape = meta["shape"]
+        dt = meta["dtype"]
+        if dt == "BF16":
+            tensors[name] = np.frombuffer(mm, dtype=np.uint16, count=(e - s) // 2,
+                                          offset=base + s).reshape(shape)
+        elif dt == "F32":
+            f32[name] = np.frombuffer(mm, dtype=np.float32, count=(e - s) // 4,
+                                      offset=base + s).reshape(shape)
+        elif dt == "Q8":
+            rows, cols = shape
+            if e - s != rows * 4 + rows * cols:
+                raise ValueError(f"{name}: Q8 size {e - s} != {rows}*4 + {rows}*{cols}")
+            # quantize.py packs tensors back to back, so scales may be unaligned: copy them
+            sc = np.frombuffer(mm, dtype=np.uint8, count=rows * 4, offset=base + s).copy().view(np.float32)
+            q = np.frombuffer(mm, dtype=np.int8, count=rows * cols, offset=base + s + rows * 4).reshape(rows, cols)
+            q8[name] = (sc, q)
+        else:
+            raise ValueError(f"{name}: dtype {dt} unsupported (BF16, F32, Q8)")
+    if q8 and tensors:
+        raise ValueError("mixed BF16 and Q8 matrices are not a reference checkpoint layout")
+    return Weights(cfg, tensors, keep=(f, mm), q8=q8, f32=f32)
 
 
 def write_safetensors(w: Weights, path: str):
+    """BF16 checkpoint, or (Q8 weights) the layout quantize.py:152-186 writes."""
+    items = []
+    if w.is_q8:
+        for name, (sc, q) in w.q8.items():
+            items.append((name, "Q8", list(q.shape), [np.ascontiguousarray(sc), np.ascontiguousarray(q)]))
+        for name, a in w._stored_f32.items():
+            items.append((name, "F32", list(a.shape), [np.ascontiguousarray(a, np.float32)]))
+    else:
+        for name, a in w.t.items():
+            items.append((name, "BF16", list(a.shape), [np.ascontiguousarray(a)]))
     hdr, off = {}, 0
-    for name, a in w.t.items():
-        hdr[name] = {"dtype": "BF16", "shape": list(a.shape), "data_offsets": [off, off + a.nbytes]}
-        off += a.nbytes
+    for name, dt, shape, parts in items:
+        n = sum(p.nbytes for p in parts)
+        hdr[name] = {"dtype": dt, "shape": shape, "data_offsets": [off, off + n]}
+        off += n
     hj = json.dumps(hdr).encode()
     hj += b" " * ((8 - len(hj) % 8) % 8)
     with open(path, "wb") as f:
         f.write(len(hj).to_bytes(8, "little"))
         f.write(hj)
-        for a in w.t.values():
-            f.write(np.ascontiguousarray(a).tobytes())
+        for _, _, _, parts in items:
+            for p in parts:
+                f.write(p.tobytes())
 
 
 # ---------------------------------------------------------------------------
@@ -258,6 +337,12 @@ WEIGHT_FIELDS = [
     ("dec_w2", _PP), ("dec_w3", _PP),
     ("dec_attn_norm", _PP), ("dec_ffn_norm", _PP), ("dec_ada_down", _PP), ("dec_ada_up", _PP),
     ("dec_norm", _P),
+    # Q8 per-row scales (NULL for bf16 matrices)
+    ("enc_wq_s", _PP), ("enc_wk_s", _PP), ("enc_wv_s", _PP), ("enc_wo_s", _PP), ("enc_w1_s", _PP),
+    ("enc_w2_s", _PP), ("enc_w3_s", _PP),
+    ("ad0_s", _P), ("ad1_s", _P), ("tok_emb_s", _P),
+    ("dec_wq_s", _PP), ("dec_wk_s", _PP), ("dec_wv_s", _PP), ("dec_wo_s", _PP), ("dec_w1_s", _PP),
+    ("dec_w2_s", _PP), ("dec_w3_s", _PP),
 ]
 
 
@@ -292,24 +377,38 @@ def build_weights_struct(w: Weights, cls):
     s.conv0_b = p(w.f32(f"{ENC}.conv_layers.0.conv.bias"))
     s.conv1_w = p(w.f32(f"{ENC}.conv_layers.1.conv.weight"))
     s.conv1_b = p(w.f32(f"{ENC}.conv_layers.1.conv.bias"))
+    q8 = w.is_q8
+
+    def mats(fld, names):
+        data = [w.matrix(n) for n in names]
+        setattr(s, fld, arr([p(d) for d, _ in data]))
+        if q8:
+            setattr(s, fld + "_s", arr([p(sc) for _, sc in data]))
+
+    def mat(fld, name):
+        d, sc = w.matrix(name)
+        setattr(s, fld, p(d))
+        if q8:
+            setattr(s, fld + "_s", p(sc))
+
     for fld, suf in [("enc_wq", "attention.wq.weight"), ("enc_wk", "attention.wk.weight"),
                      ("enc_wv", "attention.wv.weight"), ("enc_wo", "attention.wo.weight"),
                      ("enc_w1", "feed_forward.w1.weight"), ("enc_w2", "feed_forward.w2.weight"),
                      ("enc_w3", "feed_forward.w3.weight")]:
-        setattr(s, fld, arr([p(w.bf16(enc(l, suf))) for l in L]))
+        mats(fld, [enc(l, suf) for l in L])
     for fld, suf in [("enc_wq_b", "attention.wq.bias"), ("enc_wv_b", "attention.wv.bias"),
                      ("enc_wo_b", "attention.wo.bias"), ("enc_w2_b", "feed_forward.w2.bias"),
                      ("enc_attn_norm", "attention_norm.weight"), ("enc_ffn_norm", "ffn_norm.weight")]:
         setattr(s, fld, arr([p(w.f32(enc(l, suf))) for l in L]))
     s.enc_norm = p(w.f32(f"{ENC}.transformer.norm.weight"))
-    s.ad0 = p(w.bf16(f"{EMB}.audio_language_projection.0.weight"))
-    s.ad1 = p(w.bf16(f"{EMB}.audio_language_projection.2.weight"))
-    s.tok_emb = p(w.bf16(f"{EMB}.tok_embeddings.weight"))
+    mat("ad0", f"{EMB}.audio_language_projection.0.weight")
+    mat("ad1", f"{EMB}.audio_language_projection.2.weight")
+    mat("tok_emb", f"{EMB}.tok_embeddings.weight")
     for fld, suf in [("dec_wq", "attention.wq.weight"), ("dec_wk", "attention.wk.weight"),
                      ("dec_wv", "attention.wv.weight"), ("dec_wo", "attention.wo.weight"),
                      ("dec_w1", "feed_forward.w1.weight"), ("dec_w2", "feed_forward.w2.weight"),
                      ("dec_w3", "feed_forward.w3.weight")]:
-        setattr(s, fld, arr([p(w.bf16(dec(l, suf))) for l in Ld]))
+        mats(fld, [dec(l, suf) for l in Ld])
     for fld, suf in [("dec_attn_norm", "attention_norm.weight"), ("dec_ffn_norm", "ffn_norm.weight"),
                      ("dec_ada_down", "ada_rms_norm_t_cond.0.weight"),
                      ("dec_ada_up", "ada_rms_norm_t_cond.2.weight")]:

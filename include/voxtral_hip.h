@@ -71,6 +71,15 @@ typedef struct {
     const uint16_t **dec_wq, **dec_wk, **dec_wv, **dec_wo, **dec_w1, **dec_w2, **dec_w3;
     const float **dec_attn_norm, **dec_ffn_norm, **dec_ada_down, **dec_ada_up;
     const float *dec_norm;
+    /* Q8 checkpoints (quantize.py output; voxtral_safetensors.c:393-408, 457-468).  A
+     * non-NULL per-row scale array (safetensors_get_q8_scales_direct) selects int8 for that
+     * matrix, whose pointer above then carries safetensors_get_q8_data_direct, cast
+     * (int8 [out, in]).  Q/K/V of a layer and its w1/w3 must agree.  ada_down/up and the
+     * conv weights stay f32 (load_f32 dequantises / quantize.py keeps 3-D tensors f32).
+     * Leave all NULL (zero-initialise the struct) for a bf16 checkpoint. */
+    const float **enc_wq_s, **enc_wk_s, **enc_wv_s, **enc_wo_s, **enc_w1_s, **enc_w2_s, **enc_w3_s;
+    const float *ad0_s, *ad1_s, *tok_emb_s;
+    const float **dec_wq_s, **dec_wk_s, **dec_wv_s, **dec_wo_s, **dec_w1_s, **dec_w2_s, **dec_w3_s;
 } vox_hip_weights_t;
 
 typedef struct vox_hip_model vox_hip_model_t;
@@ -130,6 +139,11 @@ int vox_hip_stream_state(vox_hip_stream_t *s, int *out6);
 /* voxtral_metal.h:38  C[M,N] = A[M,K] @ B[N,K]^T (B is a host bf16 weight pointer,
  * uploaded once and cached by pointer like voxtral_metal.m:165-201) */
 void vox_hip_sgemm_bf16(int M, int N, int K, const float *A, const uint16_t *B_bf16, float *C);
+/* voxtral_metal.h:262-265  C[M,N] = A[M,K] @ (scales[n] * B_q8[N,K])^T (vox_linear_q8 /
+ * vox_matmul_t_q8 under USE_HIP, voxtral_kernels.c:316-377); B and scales are host
+ * pointers, uploaded once and cached by pointer; bias is added by the caller. */
+void vox_hip_sgemm_q8(int M, int N, int K, const float *A, const int8_t *B_q8, const float *scales,
+                      float *C);
 /* voxtral_metal.h:59 */
 void vox_hip_fused_qkv_bf16(int M, int K, const float *input,
                             const uint16_t *wq_bf16, int Nq, const uint16_t *wk_bf16, int Nk,

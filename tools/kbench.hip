@@ -142,8 +142,8 @@ int main(int argc, char** argv) {
                acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, cyc / n, rt / n / 100.0,
                cyc / (rt / 100.0) / 1000.0, spread / (nrun * 32.0), gstart / nrun / 100.0);
     }
-    add("argmax+embed", timeit([&] { CK(launch_argmax_final(pv, pi, 1024, state, nullptr, 0, (float*)emb, 1024, emb, D, x, st)); }, iters, st), 1.0);
-    add("empty-ish (embed step)", timeit([&] { CK(launch_embed_step((float*)emb, emb, state, D, x, st)); }, iters, st), 1.0);
+    add("argmax+embed", timeit([&] { CK(launch_argmax_final(pv, pi, 1024, state, nullptr, 0, (float*)emb, 1024, emb, nullptr, D, x, st)); }, iters, st), 1.0);
+    add("empty-ish (embed step)", timeit([&] { CK(launch_embed_step((float*)emb, emb, nullptr, state, D, x, st)); }, iters, st), 1.0);
     // whole-layer sequence (no graph)
     int st4[4] = {186, 0, 0, 0};
     CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));

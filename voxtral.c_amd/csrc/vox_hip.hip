@@ -123,12 +123,16 @@ static void host_rope(float* out, int p0, int n, int dim, float theta) {
 // ---------------------------------------------------------------------------
 // Model
 // ---------------------------------------------------------------------------
+// Weight matrices are raw bytes: bf16 [rows, K], or int8 [rows, K] when the matching
+// scale array (Q8 per-row scales, quantize.py) is non-null.
 struct EncLayerD {
-    uint16_t *wqkv, *wo, *w13, *w2;
+    uint8_t *wqkv, *wo, *w13, *w2;
+    float *sqkv, *so, *s13, *s2;
     float *bqkv, *bo, *b2, *attn_norm, *ffn_norm;
 };
 struct DecLayerD {
-    uint16_t *wqkv, *wo, *w13, *w2;
+    uint8_t *wqkv, *wo, *w13, *w2;
+    float *sqkv, *so, *s13, *s2;
     float *attn_norm, *ffn_norm;
 };
 
@@ -139,7 +143,8 @@ struct vox_hip_model {
     float *conv0_b, *conv1_b, *enc_norm, *dec_norm;
     std::vector<EncLayerD> enc;
     std::vector<DecLayerD> dec;
-    uint16_t *ad0, *ad1, *tok_emb;
+    uint8_t *ad0, *ad1, *tok_emb;
+    float *ad0_s, *ad1_s, *tok_emb_s;  // Q8 scales (null: bf16)
     float* ada_scale;              // device [dec_layers][dec_dim]
     std::vector<float> ada_host;   // host copy
     std::vector<std::vector<float>> ada_down, ada_up;
@@ -165,13 +170,58 @@ static int upload_f32_as_bf16(uint16_t* dst, const float* src, size_t n) {
     return upload(dst, tmp.data(), n * 2);
 }
 
+// One device matrix (bf16, or int8 + per-row f32 scales) from a host pointer pair.
+static int upload_mat(uint8_t** dst, float** dscale, const void* src, const float* scale, size_t rows,
+                      size_t cols) {
+    const size_t esz = scale ? 1 : 2;
+    CK(dalloc(dst, rows * cols * esz));
+    if (upload(*dst, src, rows * cols * esz)) return -1;
+    *dscale = nullptr;
+    if (scale) {
+        CK(dalloc(dscale, rows));
+        if (upload(*dscale, scale, rows * 4)) return -1;
+    }
+    return 0;
+}
+
+// merged Q|K|V rows (voxtral_metal.m merged_3 warmup); all three bf16 or all three Q8
+static int upload_qkv(uint8_t** dst, float** dscale, const void* wq, const float* sq, const void* wk,
+                      const float* sk, const void* wv, const float* sv, int nq, int nkv, int K) {
+    if (!sq != !sk || !sq != !sv) return set_err("wq/wk/wv mix bf16 and Q8");
+    const size_t esz = sq ? 1 : 2, rows = (size_t)nq + 2 * nkv;
+    CK(dalloc(dst, rows * K * esz));
+    if (upload(*dst, wq, (size_t)nq * K * esz) || upload(*dst + (size_t)nq * K * esz, wk, (size_t)nkv * K * esz) ||
+        upload(*dst + (size_t)(nq + nkv) * K * esz, wv, (size_t)nkv * K * esz))
+        return -1;
+    *dscale = nullptr;
+    if (sq) {
+        CK(dalloc(dscale, rows));
+        if (upload(*dscale, sq, (size_t)nq * 4) || upload(*dscale + nq, sk, (size_t)nkv * 4) ||
+            upload(*dscale + nq + nkv, sv, (size_t)nkv * 4))
+            return -1;
+    }
+    return 0;
+}
+
 // rows 32g..32g+15 <- w1 rows 16g..16g+15, rows 32g+16..32g+31 <- w3 rows 16g..
-static int upload_w13(uint16_t* dst, const uint16_t* w1, const uint16_t* w3, int hidden, int K) {
+// (Q8: the row scales are interleaved the same way)
+static int upload_w13(uint8_t** dst, float** dscale, const void* w1, const float* s1, const void* w3,
+                      const float* s3, int hidden, int K) {
     if (!w1 || !w3) return set_err("null w1/w3");
+    if (!s1 != !s3) return set_err("w1/w3 mix bf16 and Q8");
     if (hidden % 16) return set_err("hidden %d not a multiple of 16", hidden);
-    size_t grp = (size_t)16 * K * 2;
-    CK(hipMemcpy2D(dst, 2 * grp, w1, grp, grp, hidden / 16, hipMemcpyHostToDevice));
-    CK(hipMemcpy2D((char*)dst + grp, 2 * grp, w3, grp, grp, hidden / 16, hipMemcpyHostToDevice));
+    const size_t esz = s1 ? 1 : 2;
+    CK(dalloc(dst, (size_t)2 * hidden * K * esz));
+    size_t grp = (size_t)16 * K * esz;
+    CK(hipMemcpy2D(*dst, 2 * grp, w1, grp, grp, hidden / 16, hipMemcpyHostToDevice));
+    CK(hipMemcpy2D(*dst + grp, 2 * grp, w3, grp, grp, hidden / 16, hipMemcpyHostToDevice));
+    *dscale = nullptr;
+    if (s1) {
+        CK(dalloc(dscale, (size_t)2 * hidden));
+        const size_t g4 = 16 * 4;
+        CK(hipMemcpy2D(*dscale, 2 * g4, s1, g4, g4, hidden / 16, hipMemcpyHostToDevice));
+        CK(hipMemcpy2D((char*)*dscale + g4, 2 * g4, s3, g4, g4, hidden / 16, hipMemcpyHostToDevice));
+    }
     return 0;
 }
 
@@ -251,7 +301,9 @@ extern "C" vox_hip_model_t* vox_hip_model_create(const vox_hip_config_t* cfg,
     memset(&m->c, 0, sizeof m->c);
     m->c = *cfg;
     m->delay_tokens = delay_tokens;
-    m->conv0_w = m->conv1_w = m->ad0 = m->ad1 = m->tok_emb = nullptr;
+    m->conv0_w = m->conv1_w = nullptr;
+    m->ad0 = m->ad1 = m->tok_emb = nullptr;
+    m->ad0_s = m->ad1_s = m->tok_emb_s = nullptr;
     m->conv0_b = m->conv1_b = m->enc_norm = m->dec_norm = m->ada_scale = nullptr;
     m->rope_enc = m->rope_dec = nullptr;
     const vox_hip_config_t& c = *cfg;
@@ -262,6 +314,7 @@ extern "C" vox_hip_model_t* vox_hip_model_create(const vox_hip_config_t* cfg,
     auto fail = [&]() -> vox_hip_model_t* { vox_hip_model_free(m); return nullptr; };
 #define TRY(x) do { if ((x) != 0) return fail(); } while (0)
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
+#define SCL(field, l) (w->field ? w->field[l] : nullptr)
     // conv stem
     TRYH(dalloc(&m->conv0_w, (size_t)ED * c.mel_bins * 3));
     TRY(upload_f32_as_bf16(m->conv0_w, w->conv0_w, (size_t)ED * c.mel_bins * 3));
@@ -276,21 +329,16 @@ extern "C" vox_hip_model_t* vox_hip_model_create(const vox_hip_config_t* cfg,
     for (int l = 0; l < c.enc_layers; l++) {
         EncLayerD& L = m->enc[l];
         memset(&L, 0, sizeof L);
-        TRYH(dalloc(&L.wqkv, (size_t)(EQ + 2 * EKV) * ED));
-        TRY(upload(L.wqkv, w->enc_wq[l], (size_t)EQ * ED * 2));
-        TRY(upload(L.wqkv + (size_t)EQ * ED, w->enc_wk[l], (size_t)EKV * ED * 2));
-        TRY(upload(L.wqkv + (size_t)(EQ + EKV) * ED, w->enc_wv[l], (size_t)EKV * ED * 2));
+        TRY(upload_qkv(&L.wqkv, &L.sqkv, w->enc_wq[l], SCL(enc_wq_s, l), w->enc_wk[l], SCL(enc_wk_s, l),
+                       w->enc_wv[l], SCL(enc_wv_s, l), EQ, EKV, ED));
         TRYH(dalloc(&L.bqkv, EQ + 2 * EKV));  // k part stays zero: wk has no bias
         TRY(upload(L.bqkv, w->enc_wq_b[l], EQ * 4));
         TRY(upload(L.bqkv + EQ + EKV, w->enc_wv_b[l], EKV * 4));
-        TRYH(dalloc(&L.wo, (size_t)ED * EQ));
-        TRY(upload(L.wo, w->enc_wo[l], (size_t)ED * EQ * 2));
+        TRY(upload_mat(&L.wo, &L.so, w->enc_wo[l], SCL(enc_wo_s, l), ED, EQ));
         TRYH(dalloc(&L.bo, ED));
         TRY(upload(L.bo, w->enc_wo_b[l], ED * 4));
-        TRYH(dalloc(&L.w13, (size_t)2 * EH * ED));
-        TRY(upload_w13(L.w13, w->enc_w1[l], w->enc_w3[l], EH, ED));
-        TRYH(dalloc(&L.w2, (size_t)ED * EH));
-        TRY(upload(L.w2, w->enc_w2[l], (size_t)ED * EH * 2));
+        TRY(upload_w13(&L.w13, &L.s13, w->enc_w1[l], SCL(enc_w1_s, l), w->enc_w3[l], SCL(enc_w3_s, l), EH, ED));
+        TRY(upload_mat(&L.w2, &L.s2, w->enc_w2[l], SCL(enc_w2_s, l), ED, EH));
         TRYH(dalloc(&L.b2, ED));
         TRY(upload(L.b2, w->enc_w2_b[l], ED * 4));
         TRYH(dalloc(&L.attn_norm, ED));
@@ -301,29 +349,21 @@ extern "C" vox_hip_model_t* vox_hip_model_create(const vox_hip_config_t* cfg,
     TRYH(dalloc(&m->enc_norm, ED));
     TRY(upload(m->enc_norm, w->enc_norm, ED * 4));
     // adapter
-    TRYH(dalloc(&m->ad0, (size_t)DD * ED * c.downsample));
-    TRY(upload(m->ad0, w->ad0, (size_t)DD * ED * c.downsample * 2));
-    TRYH(dalloc(&m->ad1, (size_t)DD * DD));
-    TRY(upload(m->ad1, w->ad1, (size_t)DD * DD * 2));
+    TRY(upload_mat(&m->ad0, &m->ad0_s, w->ad0, w->ad0_s, DD, (size_t)ED * c.downsample));
+    TRY(upload_mat(&m->ad1, &m->ad1_s, w->ad1, w->ad1_s, DD, DD));
     // decoder
-    TRYH(dalloc(&m->tok_emb, (size_t)c.vocab * DD));
-    TRY(upload(m->tok_emb, w->tok_emb, (size_t)c.vocab * DD * 2));
+    TRY(upload_mat(&m->tok_emb, &m->tok_emb_s, w->tok_emb, w->tok_emb_s, c.vocab, DD));
     m->dec.resize(c.dec_layers);
     m->ada_down.resize(c.dec_layers);
     m->ada_up.resize(c.dec_layers);
     for (int l = 0; l < c.dec_layers; l++) {
         DecLayerD& L = m->dec[l];
         memset(&L, 0, sizeof L);
-        TRYH(dalloc(&L.wqkv, (size_t)(DQ + 2 * DKV) * DD));
-        TRY(upload(L.wqkv, w->dec_wq[l], (size_t)DQ * DD * 2));
-        TRY(upload(L.wqkv + (size_t)DQ * DD, w->dec_wk[l], (size_t)DKV * DD * 2));
-        TRY(upload(L.wqkv + (size_t)(DQ + DKV) * DD, w->dec_wv[l], (size_t)DKV * DD * 2));
-        TRYH(dalloc(&L.wo, (size_t)DD * DQ));
-        TRY(upload(L.wo, w->dec_wo[l], (size_t)DD * DQ * 2));
-        TRYH(dalloc(&L.w13, (size_t)2 * DH * DD));
-        TRY(upload_w13(L.w13, w->dec_w1[l], w->dec_w3[l], DH, DD));
-        TRYH(dalloc(&L.w2, (size_t)DD * DH));
-        TRY(upload(L.w2, w->dec_w2[l], (size_t)DD * DH * 2));
+        TRY(upload_qkv(&L.wqkv, &L.sqkv, w->dec_wq[l], SCL(dec_wq_s, l), w->dec_wk[l], SCL(dec_wk_s, l),
+                       w->dec_wv[l], SCL(dec_wv_s, l), DQ, DKV, DD));
+        TRY(upload_mat(&L.wo, &L.so, w->dec_wo[l], SCL(dec_wo_s, l), DD, DQ));
+        TRY(upload_w13(&L.w13, &L.s13, w->dec_w1[l], SCL(dec_w1_s, l), w->dec_w3[l], SCL(dec_w3_s, l), DH, DD));
+        TRY(upload_mat(&L.w2, &L.s2, w->dec_w2[l], SCL(dec_w2_s, l), DD, DH));
         TRYH(dalloc(&L.attn_norm, DD));
         TRY(upload(L.attn_norm, w->dec_attn_norm[l], DD * 4));
         TRYH(dalloc(&L.ffn_norm, DD));
@@ -339,6 +379,7 @@ extern "C" vox_hip_model_t* vox_hip_model_create(const vox_hip_config_t* cfg,
     TRY(model_rope_tables(m, 32768));
 #undef TRY
 #undef TRYH
+#undef SCL
     return m;
 }
 
@@ -347,13 +388,16 @@ extern "C" void vox_hip_model_free(vox_hip_model_t* m) {
     dfree(m->conv0_w); dfree(m->conv1_w); dfree(m->conv0_b); dfree(m->conv1_b);
     for (auto& L : m->enc) {
         dfree(L.wqkv); dfree(L.wo); dfree(L.w13); dfree(L.w2);
+        dfree(L.sqkv); dfree(L.so); dfree(L.s13); dfree(L.s2);
         dfree(L.bqkv); dfree(L.bo); dfree(L.b2); dfree(L.attn_norm); dfree(L.ffn_norm);
     }
     for (auto& L : m->dec) {
         dfree(L.wqkv); dfree(L.wo); dfree(L.w13); dfree(L.w2);
+        dfree(L.sqkv); dfree(L.so); dfree(L.s13); dfree(L.s2);
         dfree(L.attn_norm); dfree(L.ffn_norm);
     }
     dfree(m->enc_norm); dfree(m->ad0); dfree(m->ad1); dfree(m->tok_emb); dfree(m->dec_norm);
+    dfree(m->ad0_s); dfree(m->ad1_s); dfree(m->tok_emb_s);
     dfree(m->ada_scale); dfree(m->rope_enc); dfree(m->rope_dec);
     delete m;
 }
@@ -472,6 +516,7 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     const vox_hip_config_t& c = m->c;
     auto fail = [&]() -> vox_hip_stream_t* { vox_hip_stream_free(s); return nullptr; };
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
+#define SCL(field, l) (w->field ? w->field[l] : nullptr)
     TRYH(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
     const int EKV = c.enc_kv_heads * c.enc_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
     const int EQ = c.enc_heads * c.enc_head_dim;
@@ -571,13 +616,13 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
         float* Kc = s->ek + (size_t)l * s->ecap * EKV;
         float* Vc = s->ev + (size_t)l * s->ecap * EKV;
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.attn_norm, nullptr, n, ED, c.enc_eps, st));
-        CK(launch_gemm(EPI_STORE, 3, s->xn, ED, L.wqkv, ED, n, EQ + 2 * EKV, L.bqkv, s->qkv, EQ + 2 * EKV, st));
+        CK(launch_gemm(EPI_STORE, 3, s->xn, ED, L.wqkv, L.sqkv, ED, n, EQ + 2 * EKV, L.bqkv, s->qkv, EQ + 2 * EKV, st));
         CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
         CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st));
-        CK(launch_gemm(EPI_RESID, 3, s->att, EQ, L.wo, EQ, n, ED, L.bo, x, ED, st));
+        CK(launch_gemm(EPI_RESID, 3, s->att, EQ, L.wo, L.so, EQ, n, ED, L.bo, x, ED, st));
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.ffn_norm, nullptr, n, ED, c.enc_eps, st));
-        CK(launch_gemm(EPI_SWIGLU, 3, s->xn, ED, L.w13, ED, n, 2 * EH, nullptr, s->gate, EH, st));
-        CK(launch_gemm(EPI_RESID, 3, s->gate, EH, L.w2, EH, n, ED, L.b2, x, ED, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, s->xn, ED, L.w13, L.s13, ED, n, 2 * EH, nullptr, s->gate, EH, st));
+        CK(launch_gemm(EPI_RESID, 3, s->gate, EH, L.w2, L.s2, EH, n, ED, L.b2, x, ED, st));
     }
     CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, n, ED, c.enc_eps, st));
     return 0;
@@ -612,7 +657,7 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
         CK(hipMemcpyAsync(s->c0_p + (size_t)2 * ED, s->c0_res, (size_t)ED * 4, hipMemcpyDeviceToDevice, st));
     float* c0_new = s->c0_p + (size_t)(2 + s->res_count) * ED;
     CK(launch_im2col3(s->mel_p, MB, n, 1, 0, s->im2col, st));
-    CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, MB * 3, m->conv0_w, MB * 3, n, ED,
+    CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, MB * 3, m->conv0_w, nullptr, MB * 3, n, ED,
                    m->conv0_b, c0_new, ED, st));
     // ---- stride alignment (voxtral.c:653-692) ----
     const int total = s->res_count + n;
@@ -630,7 +675,7 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
     const int T1 = feed / 2;
     float* xin = s->x_enc + (size_t)4 * ED;  // 4 spare rows in front for the downsample residual
     CK(launch_im2col3(s->c0_p, ED, T1, 2, 1, s->im2col, st));
-    CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, ED * 3, m->conv1_w, ED * 3, T1, ED,
+    CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, ED * 3, m->conv1_w, nullptr, ED * 3, T1, ED,
                    m->conv1_b, xin, ED, st));
     CK(hipMemcpyAsync(s->c0_tail, s->c0_p + (size_t)(2 + feed - 2) * ED, (size_t)2 * ED * 4,
                       hipMemcpyDeviceToDevice, st));
@@ -656,9 +701,9 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
         if (stream_alloc_adapter(s, s->total_adapter + n4)) return -1;
         for (int r0 = 0; r0 < n4; r0 += ENC_SUB / 4) {
             int nr = std::min(ENC_SUB / 4, n4 - r0);
-            CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, ain + (size_t)r0 * 4 * ED, 4 * ED, m->ad0,
+            CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, ain + (size_t)r0 * 4 * ED, 4 * ED, m->ad0, m->ad0_s,
                            4 * ED, nr, D, nullptr, s->ad_mid, D, st));
-            CK(launch_gemm(EPI_STORE, 3, s->ad_mid, D, m->ad1, D, nr, D, nullptr,
+            CK(launch_gemm(EPI_STORE, 3, s->ad_mid, D, m->ad1, m->ad1_s, D, nr, D, nullptr,
                            s->adapter + (size_t)(s->total_adapter + r0) * D, D, st));
         }
         s->total_adapter += n4;
@@ -701,13 +746,13 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
         float* Kc = s->dk + (size_t)l * s->dcap * DKV;
         float* Vc = s->dv + (size_t)l * s->dcap * DKV;
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.attn_norm, nullptr, n, DD, c.dec_eps, st));
-        CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st));
+        CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, L.sqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st));
         CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st));
         CK(launch_attn_tiled(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st));
-        CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, DQ, n, DD, nullptr, x, DD, st));
+        CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, L.so, DQ, n, DD, nullptr, x, DD, st));
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, n, DD, c.dec_eps, st));
-        CK(launch_gemm(EPI_SWIGLU, 3, s->xnd, DD, L.w13, DD, n, 2 * DH, nullptr, s->gated, DH, st));
-        CK(launch_gemm(EPI_RESID, 3, s->gated, DH, L.w2, DH, n, DD, nullptr, x, DD, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, s->xnd, DD, L.w13, L.s13, DD, n, 2 * DH, nullptr, s->gated, DH, st));
+        CK(launch_gemm(EPI_RESID, 3, s->gated, DH, L.w2, L.s2, DH, n, DD, nullptr, x, DD, st));
     }
     return 0;
 }
@@ -730,7 +775,7 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         GemvArgs a;
         memset(&a, 0, sizeof a);
         // norm -> QKV -> RoPE -> KV append (decoder.c:709-722)
-        a.x = s->xd; a.K = DD; a.W = L.wqkv; a.rows = DQ + 2 * DKV;
+        a.x = s->xd; a.K = DD; a.W = L.wqkv; a.wscale = L.sqkv; a.rows = DQ + 2 * DKV;
         a.norm_w = L.attn_norm; a.eps = c.dec_eps; a.y = s->qd_;
         a.qd = DQ; a.kvd = DKV; a.hd = hd;
         a.state = state; a.pos = pos;
@@ -742,11 +787,11 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
                               s->part, s->attd, splits, st));
         // wo + residual (decoder.c:735-740)
         memset(&a, 0, sizeof a);
-        a.x = s->attd; a.K = DQ; a.W = L.wo; a.rows = DD; a.y = s->xd;
+        a.x = s->attd; a.K = DQ; a.W = L.wo; a.wscale = L.so; a.rows = DD; a.y = s->xd;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
         // norm * (1 + ada) -> W1|W3 -> silu * up (decoder.c:742-758)
         memset(&a, 0, sizeof a);
-        a.x = s->xd; a.K = DD; a.W = L.w13; a.rows = 2 * DH; a.norm_w = L.ffn_norm;
+        a.x = s->xd; a.K = DD; a.W = L.w13; a.wscale = L.s13; a.rows = 2 * DH; a.norm_w = L.ffn_norm;
         a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
         const bool gprof = s->profiling && state && (int)s->pev.size() == 2 * c.dec_layers;
         const unsigned evflag = s->capturing ? hipEventRecordExternal : 0;
@@ -755,13 +800,13 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l + 1], st, evflag));
         // W2 + residual (decoder.c:758-760)
         memset(&a, 0, sizeof a);
-        a.x = s->gated; a.K = DH; a.W = L.w2; a.rows = DD; a.y = s->xd;
+        a.x = s->gated; a.K = DH; a.W = L.w2; a.wscale = L.s2; a.rows = DD; a.y = s->xd;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
     }
     // final norm + LM head (tied embeddings) + argmax (decoder.c:762-779)
     GemvArgs a;
     memset(&a, 0, sizeof a);
-    a.x = s->xd; a.K = DD; a.W = m->tok_emb; a.rows = c.vocab; a.norm_w = m->dec_norm;
+    a.x = s->xd; a.K = DD; a.W = m->tok_emb; a.wscale = m->tok_emb_s; a.rows = c.vocab; a.norm_w = m->dec_norm;
     a.eps = c.dec_eps; a.y = s->logits; a.part_val = s->pval; a.part_idx = s->pidx;
     CK(launch_gemv(PRO_NORM, EPI_LOGITS, a, st));
     return 0;
@@ -784,7 +829,7 @@ static int enqueue_graph_step(vox_hip_stream_t* s, int splits) {
     const vox_hip_config_t& c = s->m->c;
     if (enqueue_step_layers(s, s->state, 0, nullptr, splits)) return -1;
     CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), s->state, s->tokens, s->tokens_cap,
-                           s->adapter, s->adapter_cap, s->m->tok_emb, c.dec_dim, s->xd, s->st));
+                           s->adapter, s->adapter_cap, s->m->tok_emb, s->m->tok_emb_s, c.dec_dim, s->xd, s->st));
     return 0;
 }
 
@@ -877,7 +922,7 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
         const int np = prompt_len - 1;
         if (stream_alloc_dec_rows(s, np)) return -1;
         if (ensure_rope(s, prompt_len + 1)) return -1;
-        CK(launch_embed_rows(s->adapter, m->tok_emb, 0, np, TOKEN_BOS, TOKEN_STREAMING_PAD, D, s->xd, s->st));
+        CK(launch_embed_rows(s->adapter, m->tok_emb, m->tok_emb_s, 0, np, TOKEN_BOS, TOKEN_STREAMING_PAD, D, s->xd, s->st));
         if (run_decoder_rows(s, s->xd, np, 0, m->rope_dec)) return -1;
         int st4[4] = {np, np, TOKEN_STREAMING_PAD, s->n_generated};
         CK(hipMemcpyAsync(s->state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
@@ -897,7 +942,7 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
     if (ensure_rope(s, (long long)s->h_state[0] + avail + 1)) return -1;
     // step input for the first step of this call (later inputs are built by the previous
     // step's argmax kernel)
-    if (avail > 0) CK(launch_embed_step(s->adapter, m->tok_emb, s->state, D, s->xd, s->st));
+    if (avail > 0) CK(launch_embed_step(s->adapter, m->tok_emb, m->tok_emb_s, s->state, D, s->xd, s->st));
     if (s->n_generated + avail > s->tokens_cap) avail = s->tokens_cap - s->n_generated;
     int todo = std::min(max_steps, avail);
     std::vector<int> tok;
@@ -967,7 +1012,7 @@ extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
 // Reference-boundary twins (host pointers; voxtral_metal.h)
 // ---------------------------------------------------------------------------
 static std::mutex g_twin_mu;
-static std::unordered_map<const void*, uint16_t*> g_wcache;  // host weight ptr -> device copy
+static std::unordered_map<const void*, uint8_t*> g_wcache;  // host weight ptr -> device copy
 static hipStream_t g_twin_st = nullptr;
 static float *g_tA = nullptr, *g_tC = nullptr, *g_tQ = nullptr, *g_tK = nullptr, *g_tV = nullptr, *g_tO = nullptr;
 static size_t g_tA_n = 0, g_tC_n = 0, g_tQ_n = 0, g_tK_n = 0, g_tV_n = 0, g_tO_n = 0;
@@ -980,12 +1025,12 @@ static int twin_buf(float** p, size_t* cap, size_t n) {
     return 0;
 }
 
-static uint16_t* twin_weight(const uint16_t* host, size_t n) {
+static uint8_t* twin_weight(const void* host, size_t bytes) {
     auto it = g_wcache.find(host);
     if (it != g_wcache.end()) return it->second;
-    uint16_t* d = nullptr;
-    if (dalloc(&d, n) != hipSuccess) { set_err("weight alloc failed"); return nullptr; }
-    if (hipMemcpy(d, host, n * 2, hipMemcpyHostToDevice) != hipSuccess) { set_err("weight upload failed"); return nullptr; }
+    uint8_t* d = nullptr;
+    if (dalloc(&d, bytes) != hipSuccess) { set_err("weight alloc failed"); return nullptr; }
+    if (hipMemcpy(d, host, bytes, hipMemcpyHostToDevice) != hipSuccess) { set_err("weight upload failed"); return nullptr; }
     g_wcache[host] = d;
     return d;
 }
@@ -996,26 +1041,40 @@ static int twin_init() {
     return 0;
 }
 
-static int twin_gemm(int M, int N, int K, const float* dA, const uint16_t* dW, float* dC) {
-    if (M == 1 && N % GEMV_RB == 0 && K % 8 == 0 && K <= 5 * 2048) {
+static int twin_gemm(int M, int N, int K, const float* dA, const void* dW, const float* dS, float* dC) {
+    if (M == 1 && N % GEMV_RB == 0 && K % (dS ? 16 : 8) == 0 && K <= 5 * 2048) {
         GemvArgs a;
         memset(&a, 0, sizeof a);
-        a.x = dA; a.K = K; a.W = dW; a.rows = N; a.y = dC;
+        a.x = dA; a.K = K; a.W = dW; a.wscale = dS; a.rows = N; a.y = dC;
         CK(launch_gemv(PRO_NONE, EPI_STORE, a, g_twin_st));
         return 0;
     }
-    CK(launch_gemm(EPI_STORE, 3, dA, K, dW, K, M, N, nullptr, dC, N, g_twin_st));
+    CK(launch_gemm(EPI_STORE, 3, dA, K, dW, dS, K, M, N, nullptr, dC, N, g_twin_st));
     return 0;
 }
 
 extern "C" void vox_hip_sgemm_bf16(int M, int N, int K, const float* A, const uint16_t* B, float* C) {
     std::lock_guard<std::mutex> lk(g_twin_mu);
     if (twin_init()) return;
-    uint16_t* dW = twin_weight(B, (size_t)N * K);
+    uint8_t* dW = twin_weight(B, (size_t)N * K * 2);
     if (!dW) return;
     if (twin_buf(&g_tA, &g_tA_n, (size_t)M * K) || twin_buf(&g_tC, &g_tC_n, (size_t)M * N)) return;
     if (hipMemcpyAsync(g_tA, A, (size_t)M * K * 4, hipMemcpyHostToDevice, g_twin_st) != hipSuccess) { set_err("upload"); return; }
-    if (twin_gemm(M, N, K, g_tA, dW, g_tC)) return;
+    if (twin_gemm(M, N, K, g_tA, dW, nullptr, g_tC)) return;
+    if (hipMemcpyAsync(C, g_tC, (size_t)M * N * 4, hipMemcpyDeviceToHost, g_twin_st) != hipSuccess) { set_err("download"); return; }
+    hipStreamSynchronize(g_twin_st);
+}
+
+extern "C" void vox_hip_sgemm_q8(int M, int N, int K, const float* A, const int8_t* B, const float* scales,
+                                 float* C) {
+    std::lock_guard<std::mutex> lk(g_twin_mu);
+    if (twin_init()) return;
+    uint8_t* dW = twin_weight(B, (size_t)N * K);
+    uint8_t* dS = twin_weight(scales, (size_t)N * 4);
+    if (!dW || !dS) return;
+    if (twin_buf(&g_tA, &g_tA_n, (size_t)M * K) || twin_buf(&g_tC, &g_tC_n, (size_t)M * N)) return;
+    if (hipMemcpyAsync(g_tA, A, (size_t)M * K * 4, hipMemcpyHostToDevice, g_twin_st) != hipSuccess) { set_err("upload"); return; }
+    if (twin_gemm(M, N, K, g_tA, dW, reinterpret_cast<const float*>(dS), g_tC)) return;
     if (hipMemcpyAsync(C, g_tC, (size_t)M * N * 4, hipMemcpyDeviceToHost, g_twin_st) != hipSuccess) { set_err("download"); return; }
     hipStreamSynchronize(g_twin_st);
 }
@@ -1041,18 +1100,18 @@ extern "C" void vox_hip_fused_ffn_bf16(int M, int dim, int hidden, const float* 
                                        float* output) {
     std::lock_guard<std::mutex> lk(g_twin_mu);
     if (twin_init()) return;
-    uint16_t* d1 = twin_weight(w1, (size_t)hidden * dim);
-    uint16_t* d3 = twin_weight(w3, (size_t)hidden * dim);
-    uint16_t* d2 = twin_weight(w2, (size_t)dim * hidden);
+    uint8_t* d1 = twin_weight(w1, (size_t)hidden * dim * 2);
+    uint8_t* d3 = twin_weight(w3, (size_t)hidden * dim * 2);
+    uint8_t* d2 = twin_weight(w2, (size_t)dim * hidden * 2);
     if (!d1 || !d3 || !d2) return;
     if (twin_buf(&g_tA, &g_tA_n, (size_t)M * dim) || twin_buf(&g_tQ, &g_tQ_n, (size_t)M * hidden) ||
         twin_buf(&g_tK, &g_tK_n, (size_t)M * hidden) || twin_buf(&g_tC, &g_tC_n, (size_t)M * dim))
         return;
     hipMemcpyAsync(g_tA, input, (size_t)M * dim * 4, hipMemcpyHostToDevice, g_twin_st);
-    if (twin_gemm(M, hidden, dim, g_tA, d1, g_tQ) || twin_gemm(M, hidden, dim, g_tA, d3, g_tK)) return;
+    if (twin_gemm(M, hidden, dim, g_tA, d1, nullptr, g_tQ) || twin_gemm(M, hidden, dim, g_tA, d3, nullptr, g_tK)) return;
     size_t n = (size_t)M * hidden;
     hipLaunchKernelGGL(k_silu_mul, dim3((n + 255) / 256), dim3(256), 0, g_twin_st, g_tQ, g_tK, n);
-    if (twin_gemm(M, dim, hidden, g_tQ, d2, g_tC)) return;
+    if (twin_gemm(M, dim, hidden, g_tQ, d2, nullptr, g_tC)) return;
     hipMemcpyAsync(output, g_tC, (size_t)M * dim * 4, hipMemcpyDeviceToHost, g_twin_st);
     hipStreamSynchronize(g_twin_st);
 }
@@ -1140,7 +1199,7 @@ extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_
     int st4[4] = {0, 0, 0, 0};
     CK(hipMemcpyAsync(tmp_state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
     CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), tmp_state, nullptr, 0, nullptr, 0,
-                           nullptr, c.dec_dim, nullptr, s->st));
+                           nullptr, nullptr, c.dec_dim, nullptr, s->st));
     CK(hipMemcpyAsync(st4, tmp_state, sizeof st4, hipMemcpyDeviceToHost, s->st));
     if (logits) CK(hipMemcpyAsync(logits, s->logits, (size_t)c.vocab * 4, hipMemcpyDeviceToHost, s->st));
     CK(hipStreamSynchronize(s->st));

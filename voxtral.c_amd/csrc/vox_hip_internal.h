@@ -14,7 +14,8 @@ constexpr int GEMV_RB = 4;             // rows per block iteration (even: rope /
 struct GemvArgs {
     const float* x;        // input vector [K] (device)
     int K;
-    const uint16_t* W;     // bf16 [rows, K]
+    const void* W;         // bf16 [rows, K], or int8 [rows, K] when wscale is set
+    const float* wscale;   // Q8 per-row scales (null: bf16 weights)
     int rows;              // output rows streamed (2*hidden for SWIGLU)
     const float* norm_w;   // PRO_NORM*: RMSNorm weight [K]
     const float* ada;      // PRO_NORM_ADA: ada_scale row [K]
@@ -38,8 +39,9 @@ int gemv_grid(int rows);
 int attn_maxch(int window);
 hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,
                                const float* ada, int M, int D, float eps, hipStream_t st);
-hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const uint16_t* W, int K,
-                       int M, int N, const float* bias, float* C, int ldc, hipStream_t st);
+hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void* W,
+                       const float* wscale, int K, int M, int N, const float* bias, float* C,
+                       int ldc, hipStream_t st);
 hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, const float* rope,
                           int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st);
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
@@ -53,13 +55,13 @@ constexpr int ATT_BLOCK_KEYS = 256;  // keys one decode-attention block covers
 constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st);
-hipError_t launch_embed_step(const float* adapter, const uint16_t* emb, const int* state, int D,
-                             float* x, hipStream_t st);
-hipError_t launch_embed_rows(const float* adapter, const uint16_t* emb, int row0, int n,
+hipError_t launch_embed_step(const float* adapter, const void* emb, const float* esc, const int* state,
+                             int D, float* x, hipStream_t st);
+hipError_t launch_embed_rows(const float* adapter, const void* emb, const float* esc, int row0, int n,
                              int first_tok, int rest_tok, int D, float* x, hipStream_t st);
 hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
                                int cap, const float* adapter, int adapter_rows,
-                               const uint16_t* emb, int D, float* x, hipStream_t st);
+                               const void* emb, const float* esc, int D, float* x, hipStream_t st);
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

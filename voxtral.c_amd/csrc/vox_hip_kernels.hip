@@ -97,6 +97,21 @@ __device__ __forceinline__ float dot8(uint4 w, float4 a, float4 b, float acc) {
     return acc;
 }
 
+// dot of 16 int8 weights (one uint4, Q8 rows) with 16 f32 activations: each byte is
+// sign-extended and converted exactly (q8_matvec_fused, voxtral_kernels.c:277-318)
+__device__ __forceinline__ float i8f(uint32_t w, int b) { return (float)((int32_t)(w << (24 - 8 * b)) >> 24); }
+__device__ __forceinline__ float dot16q(uint4 w, const float4 (&x)[4], float acc) {
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        acc = fmaf(i8f(d[k], 0), x[k].x, acc);
+        acc = fmaf(i8f(d[k], 1), x[k].y, acc);
+        acc = fmaf(i8f(d[k], 2), x[k].z, acc);
+        acc = fmaf(i8f(d[k], 3), x[k].w, acc);
+    }
+    return acc;
+}
+
 // ============================================================================
 // Row-wise RMSNorm (+ optional ada scale), M>1 paths.  voxtral_kernels.c:475-492,
 // voxtral_decoder.c:564-570.  One block per row.
@@ -124,18 +139,22 @@ __global__ __launch_bounds__(256) void k_rmsnorm_rows(const float* __restrict__ 
 }
 
 // ============================================================================
-// MFMA GEMM for M>1:  C[M,N] (op)= A[M,K] (f32) * W[N,K]^T (bf16)
+// MFMA GEMM for M>1:  C[M,N] (op)= A[M,K] (f32) * W[N,K]^T (bf16, or int8 with per-row
+// scales: the Q8 "fused dequant -> bf16 MFMA" path, voxtral_kernels.c:320-393)
 // tile 64x64x32, 256 threads = 4 waves in 2x2, each wave 32x32 = 2x2 16x16 tiles,
-// v_mfma_f32_16x16x32_bf16.  A is split into NSPLIT bf16 terms in the staging pass.
+// v_mfma_f32_16x16x32_bf16.  A is split into NSPLIT bf16 terms in the staging pass; an
+// int8 weight is exact in bf16, so Q8 tiles are converted while staging and the row scale
+// is applied to the f32 result (s * sum(x q), where the reference sums x (q s)).
 // ============================================================================
 #define GB_M 64
 #define GB_N 64
 #define GB_K 32
 #define GB_LDS (GB_K + 8)  // padded bf16 row (80 B) to spread ds_read_b128 lanes
 
-template <int EPI, int NSPLIT>
+template <int EPI, int NSPLIT, int WQ8>
 __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int lda,
-                                              const uint16_t* __restrict__ W, int K, int M, int N,
+                                              const void* __restrict__ W, int K, int M, int N,
+                                              const float* __restrict__ wscale,
                                               const float* __restrict__ bias,
                                               float* __restrict__ C, int ldc) {
     __shared__ __attribute__((aligned(16))) uint16_t sA[NSPLIT][GB_M][GB_LDS];
@@ -153,7 +172,8 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
 
     const bool arow_ok = (m0 + srow) < M;
     const float* Ap = A + (size_t)(m0 + srow) * lda + skq;
-    const uint16_t* Wp = W + (size_t)(n0 + srow) * K + skq;
+    const uint16_t* Wp = static_cast<const uint16_t*>(W) + (size_t)(n0 + srow) * K + skq;
+    const int8_t* Wq = static_cast<const int8_t*>(W) + (size_t)(n0 + srow) * K + skq;
 
     for (int k0 = 0; k0 < K; k0 += GB_K) {
         float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
@@ -161,7 +181,22 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
             a0 = *reinterpret_cast<const float4*>(Ap + k0);
             a1 = *reinterpret_cast<const float4*>(Ap + k0 + 4);
         }
-        uint4 wv = *reinterpret_cast<const uint4*>(Wp + k0);
+        uint4 wv;
+        if (WQ8) {
+            const uint2 q = *reinterpret_cast<const uint2*>(Wq + k0);
+            uint32_t h[8];
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                h[b] = __float_as_uint(i8f(q.x, b)) >> 16;
+                h[4 + b] = __float_as_uint(i8f(q.y, b)) >> 16;
+            }
+            wv.x = h[0] | (h[1] << 16);
+            wv.y = h[2] | (h[3] << 16);
+            wv.z = h[4] | (h[5] << 16);
+            wv.w = h[6] | (h[7] << 16);
+        } else {
+            wv = *reinterpret_cast<const uint4*>(Wp + k0);
+        }
         __syncthreads();
         {
             float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
@@ -217,12 +252,18 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
                 // wave's 32 columns = one interleave group: tile 0 = w1 rows, tile 1 = w3 rows
                 const int g = (n0 + wc * 32) >> 5;
                 const int j = g * 16 + cc;
-                C[(size_t)m * ldc + j] = silu(acc[mi][0][r]) * acc[mi][1][r];
+                float gt = acc[mi][0][r], up = acc[mi][1][r];
+                if (WQ8) {
+                    gt *= wscale[n0 + wc * 32 + cc];
+                    up *= wscale[n0 + wc * 32 + 16 + cc];
+                }
+                C[(size_t)m * ldc + j] = silu(gt) * up;
             } else {
 #pragma unroll
                 for (int ni = 0; ni < 2; ni++) {
                     const int n = n0 + wc * 32 + ni * 16 + cc;
                     float v = acc[mi][ni][r];
+                    if (WQ8) v *= wscale[n];
                     if (bias) v += bias[n];
                     float* cp = C + (size_t)m * ldc + n;
                     if (EPI == EPI_STORE) *cp = v;
@@ -407,49 +448,62 @@ __device__ __forceinline__ void gemv_rows(int g, int (&rows)[RB]) {
     }
 }
 
+// KC = 16-B chunks per row (K/8 bf16, K/16 int8)
 template <int RB, int KQ>
-__device__ __forceinline__ void gemv_load(const uint16_t* __restrict__ W, int K, int K8,
+__device__ __forceinline__ void gemv_load(const void* __restrict__ W, int KC,
                                           const int (&rows)[RB], int wave, int lane,
                                           uint4 (&wv)[KQ][RB]) {
-    // Chunks past K (K not a multiple of 8*256) re-load chunk 0 and meet x = 0: every load
-    // is unconditional, so hipcc issues them all before the first wait (a guarded load
-    // makes it wait vmcnt(0) at each branch join).
+    // Chunks past K (K not a multiple of 16 B * 256) re-load chunk 0 and meet x = 0: every
+    // load is unconditional, so hipcc issues them all before the first wait (a guarded
+    // load makes it wait vmcnt(0) at each branch join).
+    const uint4* W4 = static_cast<const uint4*>(W);
 #pragma unroll
     for (int j = 0; j < KQ; j++) {
         const int c0 = (j * 4 + wave) * 64 + lane;
-        const int c = c0 < K8 ? c0 : 0;
+        const int c = c0 < KC ? c0 : 0;
 #pragma unroll
-        for (int i = 0; i < RB; i++) wv[j][i] = ldnt(reinterpret_cast<const uint4*>(W + (size_t)rows[i] * K) + c);
+        for (int i = 0; i < RB; i++) wv[j][i] = ldnt(W4 + (size_t)rows[i] * KC + c);
     }
 }
 
-template <int PRO, int EPI, int RB, int KQ>
+// Q8 rows (WQ8): 16-B chunks of 16 int8, so a lane holds 16 x values per chunk, and the
+// group's RB row scales are fetched with its weights (applied before the epilogue:
+// y = scale * sum + bias, voxtral_kernels.c:316).
+template <int PRO, int EPI, int RB, int KQ, int WQ8>
 __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
+    constexpr int XPC = WQ8 ? 4 : 2;  // float4 of x per 16-B chunk
     __shared__ float red[2][4][RB];
     __shared__ float sred[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int K = a.K, K8 = K >> 3;
+    const int K = a.K, KC = WQ8 ? K >> 4 : K >> 3;
     const int ngroups = a.rows / RB;
     int g = blockIdx.x;
     int rows[RB];
     uint4 wv[KQ][RB];
+    float wsc[RB];
     // first group's weights are independent of x: issue them before the prologue
     gemv_rows<EPI, RB>(g, rows);
-    gemv_load<RB, KQ>(a.W, K, K8, rows, wave, lane, wv);
+    gemv_load<RB, KQ>(a.W, KC, rows, wave, lane, wv);
+    if (WQ8 && wave == 0) {
+#pragma unroll
+        for (int i = 0; i < RB; i++) wsc[i] = a.wscale[rows[i]];
+    }
 
-    float4 xr[KQ][2];
+    float4 xr[KQ][XPC];
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < KQ; j++) {
         const int c = (j * 4 + wave) * 64 + lane;
-        const float4* xp = reinterpret_cast<const float4*>(a.x) + 2 * (c < K8 ? c : 0);
+        const float4* xp = reinterpret_cast<const float4*>(a.x) + XPC * (c < KC ? c : 0);
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 x0 = xp[0], x1 = xp[1];
-        xr[j][0] = c < K8 ? x0 : z;
-        xr[j][1] = c < K8 ? x1 : z;
+#pragma unroll
+        for (int h = 0; h < XPC; h++) {
+            const float4 xv = xp[h];
+            xr[j][h] = c < KC ? xv : z;
+        }
         if (PRO != PRO_NONE) {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
+            for (int h = 0; h < XPC; h++) {
                 const float4 v = xr[j][h];
                 ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, ss))));
             }
@@ -465,11 +519,11 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 #pragma unroll
         for (int j = 0; j < KQ; j++) {
             const int c0 = (j * 4 + wave) * 64 + lane;
-            const int c = c0 < K8 ? c0 : 0;
-            const float4* wp = reinterpret_cast<const float4*>(a.norm_w) + 2 * c;
-            const float4* ap = reinterpret_cast<const float4*>(PRO == PRO_NORM_ADA ? a.ada : a.norm_w) + 2 * c;
+            const int c = c0 < KC ? c0 : 0;
+            const float4* wp = reinterpret_cast<const float4*>(a.norm_w) + XPC * c;
+            const float4* ap = reinterpret_cast<const float4*>(PRO == PRO_NORM_ADA ? a.ada : a.norm_w) + XPC * c;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
+            for (int h = 0; h < XPC; h++) {
                 float4 v = xr[j][h];
                 const float4 nw = wp[h];
                 v.x = v.x * inv * nw.x; v.y = v.y * inv * nw.y;
@@ -496,15 +550,26 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 #pragma unroll
         for (int j = 0; j < KQ; j++)
 #pragma unroll
-            for (int i = 0; i < RB; i++) acc[i] = dot8(wv[j][i], xr[j][0], xr[j][1], acc[i]);
+            for (int i = 0; i < RB; i++) {
+                if (WQ8) acc[i] = dot16q(wv[j][i], reinterpret_cast<const float4(&)[4]>(xr[j]), acc[i]);
+                else acc[i] = dot8(wv[j][i], xr[j][0], xr[j][XPC - 1], acc[i]);
+            }
         const int gcur = g;
         int rcur[RB];
+        float scur[RB];
 #pragma unroll
-        for (int i = 0; i < RB; i++) rcur[i] = rows[i];
+        for (int i = 0; i < RB; i++) {
+            rcur[i] = rows[i];
+            scur[i] = WQ8 ? wsc[i] : 1.0f;
+        }
         g += gridDim.x;
         if (g < ngroups) {  // next group's loads go out before this group's reduction
             gemv_rows<EPI, RB>(g, rows);
-            gemv_load<RB, KQ>(a.W, K, K8, rows, wave, lane, wv);
+            gemv_load<RB, KQ>(a.W, KC, rows, wave, lane, wv);
+            if (WQ8 && wave == 0) {
+#pragma unroll
+                for (int i = 0; i < RB; i++) wsc[i] = a.wscale[rows[i]];
+            }
         }
 #pragma unroll
         for (int i = 0; i < RB; i++) acc[i] = wave_sum(acc[i]);
@@ -516,7 +581,10 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         if (wave == 0 && lane == 0) {
             float v[RB];
 #pragma unroll
-            for (int i = 0; i < RB; i++) v[i] = ((red[buf][0][i] + red[buf][1][i]) + red[buf][2][i]) + red[buf][3][i];
+            for (int i = 0; i < RB; i++) {
+                v[i] = ((red[buf][0][i] + red[buf][1][i]) + red[buf][2][i]) + red[buf][3][i];
+                if (WQ8) v[i] *= scur[i];
+            }
 #pragma unroll
             for (int i = 0; i < RB; i += 2) {
                 const int r0 = rcur[i], r1 = rcur[i + 1];
@@ -803,28 +871,35 @@ __global__ __launch_bounds__(256) void k_attn_combine(const float* __restrict__ 
 }
 
 // ============================================================================
-// Step input: x = adapter[gen] + bf16->f32(tok_emb[prev]) (voxtral.c:1106-1113)
+// Step input: x = adapter[gen] + tok_emb[prev] (voxtral.c:1106-1113); the embedding row
+// is bf16 (tok_embed_bf16_to_f32, voxtral.c:434-441) or, with esc, int8 times the row's
+// scale (tok_embed_q8_to_f32, voxtral.c:443-451).
 // ============================================================================
+__device__ __forceinline__ float emb_at(const void* emb, const float* esc, int tok, int D, int i) {
+    if (esc) return (float)static_cast<const int8_t*>(emb)[(size_t)tok * D + i] * esc[tok];
+    return bf2f(static_cast<const uint16_t*>(emb)[(size_t)tok * D + i]);
+}
+
 __global__ __launch_bounds__(256) void k_embed_step(const float* __restrict__ adapter,
-                                                    const uint16_t* __restrict__ emb,
+                                                    const void* __restrict__ emb,
+                                                    const float* __restrict__ esc,
                                                     const int* __restrict__ state, int D,
                                                     float* __restrict__ x) {
     const int gi = state[1], tok = state[2];
     const float* a = adapter + (size_t)gi * D;
-    const uint16_t* e = emb + (size_t)tok * D;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < D; i += gridDim.x * 256) x[i] = a[i] + bf2f(e[i]);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < D; i += gridDim.x * 256) x[i] = a[i] + emb_at(emb, esc, tok, D, i);
 }
 
 // prompt embeds for prefill rows (voxtral.c:1039-1048): token = BOS for logical row 0
 __global__ __launch_bounds__(256) void k_embed_rows(const float* __restrict__ adapter,
-                                                    const uint16_t* __restrict__ emb, int row0,
+                                                    const void* __restrict__ emb,
+                                                    const float* __restrict__ esc, int row0,
                                                     int first_tok, int rest_tok, int D,
                                                     float* __restrict__ x) {
     const int r = blockIdx.x;
     const int tok = (row0 + r == 0) ? first_tok : rest_tok;
     const float* a = adapter + (size_t)(row0 + r) * D;
-    const uint16_t* e = emb + (size_t)tok * D;
-    for (int i = threadIdx.x; i < D; i += 256) x[(size_t)r * D + i] = a[i] + bf2f(e[i]);
+    for (int i = threadIdx.x; i < D; i += 256) x[(size_t)r * D + i] = a[i] + emb_at(emb, esc, tok, D, i);
 }
 
 // Final argmax over per-block partials; advance the device-side step state
@@ -837,7 +912,8 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
                                                       int* __restrict__ tokens, int tokens_cap,
                                                       const float* __restrict__ adapter,
                                                       int adapter_rows,
-                                                      const uint16_t* __restrict__ emb, int D,
+                                                      const void* __restrict__ emb,
+                                                      const float* __restrict__ esc, int D,
                                                       float* __restrict__ x) {
     __shared__ float sv[256];
     __shared__ int si[256];
@@ -878,8 +954,7 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
     __syncthreads();
     if (adapter && srow < adapter_rows) {
         const float* a = adapter + (size_t)srow * D;
-        const uint16_t* e = emb + (size_t)stok * D;
-        for (int i = threadIdx.x; i < D; i += 256) x[i] = a[i] + bf2f(e[i]);
+        for (int i = threadIdx.x; i < D; i += 256) x[i] = a[i] + emb_at(emb, esc, stok, D, i);
     }
 }
 
@@ -928,20 +1003,24 @@ hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const
 }
 
 template <int EPI, int NS>
-static hipError_t gemm_t(const float* A, int lda, const uint16_t* W, int K, int M, int N,
-                         const float* bias, float* C, int ldc, hipStream_t st) {
+static hipError_t gemm_t(const float* A, int lda, const void* W, const float* wscale, int K, int M,
+                         int N, const float* bias, float* C, int ldc, hipStream_t st) {
     dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M);
-    hipLaunchKernelGGL((k_gemm<EPI, NS>), grid, dim3(256), 0, st, A, lda, W, K, M, N, bias, C, ldc);
+    if (wscale)
+        hipLaunchKernelGGL((k_gemm<EPI, NS, 1>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
+    else
+        hipLaunchKernelGGL((k_gemm<EPI, NS, 0>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
     LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const uint16_t* W, int K,
-                       int M, int N, const float* bias, float* C, int ldc, hipStream_t st) {
+hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void* W,
+                       const float* wscale, int K, int M, int N, const float* bias, float* C,
+                       int ldc, hipStream_t st) {
     if (M <= 0) return hipSuccess;
     if (N % GB_N || K % GB_K || lda % 4) return hipErrorInvalidValue;
 #define GEMM_CASE(E, S) \
-    if (epi == E && nsplit == S) return gemm_t<E, S>(A, lda, W, K, M, N, bias, C, ldc, st);
+    if (epi == E && nsplit == S) return gemm_t<E, S>(A, lda, W, wscale, K, M, N, bias, C, ldc, st);
     GEMM_CASE(EPI_STORE, 1) GEMM_CASE(EPI_STORE, 2) GEMM_CASE(EPI_STORE, 3)
     GEMM_CASE(EPI_RESID, 1) GEMM_CASE(EPI_RESID, 2) GEMM_CASE(EPI_RESID, 3)
     GEMM_CASE(EPI_GELU, 1) GEMM_CASE(EPI_GELU, 2) GEMM_CASE(EPI_GELU, 3)
@@ -987,11 +1066,11 @@ int gemv_grid(int rows) {
     return best;
 }
 
-template <int P, int E, int RB>
+template <int P, int E, int RB, int Q8>
 static hipError_t gemv_k(const GemvArgs& a, int grid, hipStream_t st) {
-    const int kq = ((a.K >> 3) + 255) / 256;
+    const int kq = ((Q8 ? a.K >> 4 : a.K >> 3) + 255) / 256;
     switch (kq) {
-#define KQ_CASE(Q) case Q: hipLaunchKernelGGL((k_gemv<P, E, RB, Q>), dim3(grid), dim3(256), 0, st, a); break;
+#define KQ_CASE(Q) case Q: hipLaunchKernelGGL((k_gemv<P, E, RB, Q, Q8>), dim3(grid), dim3(256), 0, st, a); break;
         KQ_CASE(1) KQ_CASE(2) KQ_CASE(3) KQ_CASE(4) KQ_CASE(5)
 #undef KQ_CASE
         default: return hipErrorInvalidValue;
@@ -1000,12 +1079,17 @@ static hipError_t gemv_k(const GemvArgs& a, int grid, hipStream_t st) {
     return hipSuccess;
 }
 
+template <int P, int E, int RB>
+static hipError_t gemv_q(const GemvArgs& a, int grid, hipStream_t st) {
+    return a.wscale ? gemv_k<P, E, RB, 1>(a, grid, st) : gemv_k<P, E, RB, 0>(a, grid, st);
+}
+
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     const int rb = gemv_rb(a.rows);
-    if (a.K % 8 || a.rows % rb) return hipErrorInvalidValue;
+    if (a.K % (a.wscale ? 16 : 8) || a.rows % rb) return hipErrorInvalidValue;
     const int grid = gemv_grid(a.rows);
 #define GEMV_CASE(P, E) \
-    if (pro == P && epi == E) return rb == 8 ? gemv_k<P, E, 8>(a, grid, st) : gemv_k<P, E, 4>(a, grid, st);
+    if (pro == P && epi == E) return rb == 8 ? gemv_q<P, E, 8>(a, grid, st) : gemv_q<P, E, 4>(a, grid, st);
     GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_QKV)
     GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS)
 #undef GEMV_CASE
@@ -1053,26 +1137,26 @@ hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float
     return hipGetLastError();
 }
 
-hipError_t launch_embed_step(const float* adapter, const uint16_t* emb, const int* state, int D,
-                             float* x, hipStream_t st) {
-    hipLaunchKernelGGL(k_embed_step, dim3((D + 255) / 256), dim3(256), 0, st, adapter, emb, state, D, x);
+hipError_t launch_embed_step(const float* adapter, const void* emb, const float* esc, const int* state,
+                             int D, float* x, hipStream_t st) {
+    hipLaunchKernelGGL(k_embed_step, dim3((D + 255) / 256), dim3(256), 0, st, adapter, emb, esc, state, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t launch_embed_rows(const float* adapter, const uint16_t* emb, int row0, int n,
+hipError_t launch_embed_rows(const float* adapter, const void* emb, const float* esc, int row0, int n,
                              int first_tok, int rest_tok, int D, float* x, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_embed_rows, dim3(n), dim3(256), 0, st, adapter, emb, row0, first_tok, rest_tok, D, x);
+    hipLaunchKernelGGL(k_embed_rows, dim3(n), dim3(256), 0, st, adapter, emb, esc, row0, first_tok, rest_tok, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
 }
 
 hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
                                int cap, const float* adapter, int adapter_rows,
-                               const uint16_t* emb, int D, float* x, hipStream_t st) {
+                               const void* emb, const float* esc, int D, float* x, hipStream_t st) {
     hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, pv, pi, n, state, tokens, cap,
-                       adapter, adapter_rows, emb, D, x);
+                       adapter, adapter_rows, emb, esc, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -38,7 +38,7 @@ EXPORTS = [
     "vox_hip_model_ada_scale", "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
-    "vox_hip_stream_state", "vox_hip_sgemm_bf16", "vox_hip_fused_qkv_bf16",
+    "vox_hip_stream_state", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
     "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
@@ -73,6 +73,7 @@ def lib():
         "vox_hip_stream_decode": (I, [P, I, I, ip, fp]),
         "vox_hip_stream_state": (I, [P, ip]),
         "vox_hip_sgemm_bf16": (None, [I, I, I, fp, P, fp]),
+        "vox_hip_sgemm_q8": (None, [I, I, I, fp, P, fp, fp]),
         "vox_hip_fused_qkv_bf16": (None, [I, I, fp, P, I, P, I, P, I, fp, fp, fp]),
         "vox_hip_fused_ffn_bf16": (None, [I, I, I, fp, P, P, P, fp]),
         "vox_hip_encoder_attention": (None, [fp, fp, fp, fp, I, I, I, I, I, F, I, I]),
@@ -297,6 +298,17 @@ def sgemm_bf16(A: np.ndarray, B_bf16: np.ndarray) -> np.ndarray:
     N = B_bf16.shape[0]
     C = np.empty((M, N), np.float32)
     lib().vox_hip_sgemm_bf16(M, N, K, fptr(A), B_bf16.ctypes.data, fptr(C))
+    return C
+
+
+def sgemm_q8(A: np.ndarray, B_q8: np.ndarray, scales: np.ndarray) -> np.ndarray:
+    """C = A @ (scales[:, None] * B_q8)^T (vox_metal_sgemm_q8 twin); B/scales are cached
+    on the device by host pointer, so keep them alive and unmodified."""
+    A = np.ascontiguousarray(A, np.float32)
+    M, K = A.shape
+    N = B_q8.shape[0]
+    C = np.empty((M, N), np.float32)
+    lib().vox_hip_sgemm_q8(M, N, K, fptr(A), B_q8.ctypes.data, fptr(scales), fptr(C))
     return C
 
 

@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=8, help="oracle decode steps in the CPU sample")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--q8", action="store_true",
+                    help="config 5: Q8 weights (the quantize.py layout, quantised from the seeded bf16 set)")
     return ap.parse_args()
 
 
@@ -95,7 +97,7 @@ def transcribe(st, mel_dev, n_mel):
             "tokens": np.concatenate([first, rest])}
 
 
-def cpu_baseline(cfg, weights, mel, n_steps):
+def cpu_baseline(cfg, weights, mel, n_steps, q8=False):
     """The CPU restatement (oracle/, the reference's algorithm) timed on this host on a
     bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -120,9 +122,9 @@ def cpu_baseline(cfg, weights, mel, n_steps):
     ms_step = (t3 - t2) * 1000.0 / n_steps
     return {"value": round(1000.0 / ms_step, 3), "unit": "tokens/s", "cores": 1, "kind": "port",
             "sample": (f"oracle/ CPU restatement, full Voxtral-4B shapes: {n_steps} greedy decode "
-                       f"steps after the 38-row prefill (single-threaded bf16 GEMV as "
-                       f"voxtral_kernels.c:154-195); encoder = the 3 jfk chunks with "
-                       f"{threads}-thread OpenBLAS sgemm"),
+                       f"steps after the 38-row prefill (single-threaded "
+                       + ("q8 GEMV as voxtral_kernels.c:277-318" if q8 else "bf16 GEMV as voxtral_kernels.c:154-195")
+                       + f"); encoder = the 3 jfk chunks with {threads}-thread OpenBLAS sgemm"),
             "ms_per_token": round(ms_step, 2),
             "encoder_rtf": round((t1 - t0) / AUDIO_SECONDS, 4),
             "encoder_threads": threads}
@@ -132,11 +134,13 @@ def main():
     args = parse()
     d = Dist(args.gpus)
     import vox_hip
-    from vox_weights import VOXTRAL_4B, synth_weights
+    from vox_weights import VOXTRAL_4B, quantize_q8, synth_weights
     vox_hip.init(device=d.local)
     cfg = VOXTRAL_4B
 
     w = synth_weights(cfg, seed=args.seed)
+    if args.q8:
+        w = quantize_q8(w)
     model = vox_hip.Model(cfg, w)
     keep_host = d.rank == 0 and d.world == 1 and not args.no_cpu_baseline
     if not keep_host:
@@ -174,7 +178,9 @@ def main():
     # roofline of the dominant kernel: the fused RMSNorm*(1+ada) -> W1|W3 GEMV -> SiLU*up
     # (26 launches per token, 43% of the decode bytes; DESIGN.md "Roofline")
     D, H = cfg.dec_dim, cfg.dec_hidden
-    w13_bytes = 2 * H * D * 2 + D * 4 * 3 + H * 4   # bf16 W1|W3 + x, norm w, ada in + gate out
+    wb = 1 if args.q8 else 2
+    # W1|W3 (+ Q8 row scales) + x, norm w, ada in + gate out
+    w13_bytes = 2 * H * D * wb + (2 * H * 4 if args.q8 else 0) + D * 4 * 3 + H * 4
     avg_ms = prof["avg_ms"] if prof["launches"] else float("nan")
     achieved = w13_bytes / (avg_ms * 1e-3) / 1e9 if prof["launches"] else None
     traffic = None
@@ -183,7 +189,8 @@ def main():
         traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
 
     out = {
-        "metric": "decoder tokens/sec + encoder RTF, Voxtral-4B bf16 at 1/2/4/8 MI355X",
+        "metric": ("decoder tokens/sec + encoder RTF, Voxtral-4B q8 (config 5) at 1/2/4/8 MI355X" if args.q8
+                   else "decoder tokens/sec + encoder RTF, Voxtral-4B bf16 at 1/2/4/8 MI355X"),
         "value": round(tok_s, 2),
         "unit": "tokens/s",
         "n_gpus": d.world,
@@ -195,7 +202,7 @@ def main():
         "vs_baseline": round(tok_s / d.world / MPS_TOK_S, 2),
         "vs_baseline_ref": "per-GPU tok/s vs 42.6 tok/s, Apple M3 Max MPS, README.md:323 (BASELINE.md 1)",
         "dtype": "f32",
-        "weights_dtype": "bf16",
+        "weights_dtype": "q8 (int8 + f32 row scales, quantize.py)" if args.q8 else "bf16",
         "data": "synthetic (seeded random weights of the exact architecture; synthetic log-mel)",
         "config": {"workload": "jfk.wav one-shot transcription shape: 1355/140/1-frame encoder "
                                "chunks, 38-row prefill, 148 greedy steps",
@@ -212,7 +219,7 @@ def main():
                      "launches_timed": prof["launches"]},
     }
     if keep_host:
-        out["cpu_baseline"] = cpu_baseline(cfg, w, mel, args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(cfg, w, mel, args.cpu_steps, q8=args.q8)
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     mel_dev.free()

@@ -127,6 +127,15 @@ int vox_hip_stream_read_adapter(vox_hip_stream_t *s, int first, int n, float *ou
  * [n, vocab] logits.  Returns the number of tokens generated (<0 on error). */
 int vox_hip_stream_decode(vox_hip_stream_t *s, int max_steps, int stop_at_eos,
                           int *tokens_out, float *logits_out);
+/* Alternative tokens (--alt, voxtral.h:294-304).  vox_stream_set_alt (voxtral.c:1329-1337):
+ * n_alt clamped to 1..VOX_HIP_MAX_ALT, cutoff to [0,1]; n_alt > 1 makes every later step
+ * also keep the softmax candidates of stream_fill_alts (voxtral.c:955-1010) on the device
+ * (no logits download).  read_alts returns, for generated steps [first, first+n), the
+ * chosen id and the accepted alternatives ([n][VOX_HIP_MAX_ALT], -1 = none) and optionally
+ * their probabilities.  Callers apply it to text tokens only, as the reference does. */
+#define VOX_HIP_MAX_ALT 4
+int vox_hip_stream_set_alt(vox_hip_stream_t *s, int n_alt, float cutoff);
+int vox_hip_stream_read_alts(vox_hip_stream_t *s, int first, int n, int *ids_out, float *probs_out);
 /* Decoder state snapshot: [0]=kv logical length, [1]=next adapter row, [2]=prev token,
  * [3]=started, [4]=eos_seen, [5]=tokens generated. */
 int vox_hip_stream_state(vox_hip_stream_t *s, int *out6);

@@ -237,6 +237,37 @@ class OracleStream:
             self.h = None
 
 
+def fill_alts(logits, best_token, n_alt, cutoff, text_min=1000, max_alt=4):
+    """stream_fill_alts (voxtral.c:955-1010) on one step's logits: softmax in f32 (max,
+    exp(l - max), sum, * 1/sum), then repeated scans over ids >= TOKEN_TEXT_MIN for the most
+    probable unused id, accepted while 1 - p / p_best <= cutoff.  Returns (ids, probs),
+    length max_alt, -1 / 0 padded."""
+    ids = [-1] * max_alt
+    probs = [0.0] * max_alt
+    ids[0] = int(best_token)
+    if n_alt <= 1:
+        return ids, probs
+    lg = np.asarray(logits, np.float32)
+    e = np.exp(lg - lg.max()).astype(np.float32)
+    p = e * np.float32(np.float32(1.0) / e.sum(dtype=np.float32))
+    best_prob = float(p[best_token])
+    probs[0] = best_prob
+    if best_prob <= 0:
+        return ids, probs
+    cand = p.copy()
+    cand[:text_min] = -1.0
+    cand[best_token] = -1.0
+    for k in range(1, n_alt):
+        i = int(np.argmax(cand))          # first index of the maximum, as the strict '>' scan
+        if cand[i] < 0:
+            break
+        if 1.0 - float(cand[i]) / best_prob > cutoff:
+            break
+        ids[k], probs[k] = i, float(cand[i])
+        cand[i] = -1.0
+    return ids, probs
+
+
 class OracleMel:
     """Incremental log-mel (voxtral_audio.c:405-633)."""
 

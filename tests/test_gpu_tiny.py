@@ -123,3 +123,37 @@ def test_long_stream_multiblock_attention(tiny_weights):
     # logits of a late step (window > 256 keys)
     assert hs.state()["kv_pos"] == os_.state()["dec_len"]
     hs.close(); os_.close(); hm.close(); om.close()
+
+
+def test_alternatives_match_stream_fill_alts(models, jfk_samples):
+    """--alt (voxtral.c:955-1010): candidates kept on the device per step agree with the
+    reference's softmax + repeated scan applied to the oracle's logits (ids exact, probs
+    1e-5 relative), for several n_alt / cutoff settings."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    events = vox_oracle.transcribe_mel_schedule(jfk_samples)
+    for n_alt, cutoff in ((3, 1.0), (4, 0.5), (2, 0.0), (1, 1.0)):
+        hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+        hs.set_alt(n_alt, cutoff)
+        ht, ol = [], []
+        done = 0
+        for kind, mel in events:
+            hs.encode_mel(mel[done:])
+            os_.encode_mel(mel[done:])
+            done = mel.shape[0]
+            ht += hs.decode(stop_at_eos=False).tolist()
+            t, lg = os_.decode(stop_at_eos=False, want_logits=True)
+            ol.append(lg)
+        ol = np.concatenate(ol)
+        ids, pr = hs.read_alts(0, len(ht))
+        n_with_alts = 0
+        for i, tok in enumerate(ht):
+            rid, rpr = vox_oracle.fill_alts(ol[i], tok, n_alt, cutoff)
+            assert ids[i].tolist() == rid, (i, ids[i], rid)
+            np.testing.assert_allclose(pr[i], rpr, rtol=1e-5, atol=1e-9)
+            n_with_alts += ids[i][1] >= 0
+        if n_alt > 1 and cutoff >= 0.5:
+            assert n_with_alts > 0
+        hs.close()
+        os_.close()

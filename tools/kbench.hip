@@ -66,10 +66,12 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&state, 16));
 
     int layer = 0;
+    float* wsc = (float*)dmalloc((size_t)V * 4, 1);  // Q8 row scales (any finite values)
+    const float* qs = nullptr;  // set: the weight buffers are read as int8 rows
     auto gemv = [&](int pro, int epi, const uint16_t* W, int K, int rows) {
         GemvArgs a;
         memset(&a, 0, sizeof a);
-        a.x = x; a.K = K; a.W = W; a.rows = rows; a.norm_w = normw; a.ada = ada; a.eps = 1e-5f;
+        a.x = x; a.K = K; a.W = W; a.wscale = qs; a.rows = rows; a.norm_w = normw; a.ada = ada; a.eps = 1e-5f;
         a.y = y; a.qd = DQ; a.kvd = DKV; a.hd = HD; a.rope = rope; a.state = state; a.Kc = Kc; a.Vc = Vc;
         a.cap = cap; a.part_val = pv; a.part_idx = pi;
         CK(launch_gemv(pro, epi, a, st));
@@ -88,6 +90,13 @@ int main(int argc, char** argv) {
     add("gemv w13 same buffer (MALL-hot)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[0], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
     add("gemv wo same buffer (MALL-hot)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[0], DQ, D); }, iters, st), (double)D * DQ * 2);
     add("gemv lm   (131072x3072, logits)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D * 2);
+    qs = wsc;
+    add("q8 gemv qkv  (6144x3072)", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D);
+    add("q8 gemv wo   (3072x4096)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ);
+    add("q8 gemv w13  (18432x3072)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D);
+    add("q8 gemv w2   (3072x9216)", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH);
+    add("q8 gemv lm   (131072x3072)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D);
+    qs = nullptr;
     for (int L : {64, 187, 256, 1000, 4096, 8192}) {
         int st4[4] = {L - 1, 0, 0, 0};
         CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));

@@ -442,6 +442,10 @@ struct vox_hip_stream {
     int adapter_cap, total_adapter;
     // decoder
     float *xd, *xnd, *qkvd, *qd_, *attd, *gated, *part, *logits, *pval;
+    float *part_alt, *alts;  // stream_fill_alts partials / per-step records [tokens_cap][ALT_REC]
+    int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
+    float alt_cutoff;
+    int graph_alt;           // alt mode the step graphs were captured with
     int *pidx, *state, *tokens;
     int dec_rows_cap, tokens_cap;
     hipGraphExec_t step_exec[STEP_GRAPHS];  // [g]: attention with 2^g key splits (g = 0: no combine)
@@ -537,12 +541,16 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->gate, (size_t)ENC_SUB * c.enc_hidden));
     TRYH(dalloc(&s->ad_mid, (size_t)(ENC_SUB / 4 + 4) * c.dec_dim));
     TRYH(dalloc(&s->part, (size_t)c.dec_heads * attn_maxch(c.dec_window) * (c.dec_head_dim + 2)));
+    TRYH(dalloc(&s->part_alt, (size_t)GEMV_MAX_BLOCKS * ALT_PART));
     TRYH(dalloc(&s->logits, (size_t)c.vocab));
     TRYH(dalloc(&s->pval, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->state, 4));
     s->tokens_cap = 1 << 16;
     TRYH(dalloc(&s->tokens, s->tokens_cap));
+    TRYH(dalloc(&s->alts, (size_t)s->tokens_cap * ALT_REC));
+    s->n_alt = 1;
+    s->alt_cutoff = 0.f;
     TRYH(hipEventCreate(&s->evt[0]));
     TRYH(hipEventCreate(&s->evt[1]));
 #undef TRYH
@@ -563,6 +571,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->tokens);
+    dfree(s->part_alt); dfree(s->alts);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
     for (hipEvent_t e : s->pev) hipEventDestroy(e);
@@ -808,7 +817,8 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
     memset(&a, 0, sizeof a);
     a.x = s->xd; a.K = DD; a.W = m->tok_emb; a.wscale = m->tok_emb_s; a.rows = c.vocab; a.norm_w = m->dec_norm;
     a.eps = c.dec_eps; a.y = s->logits; a.part_val = s->pval; a.part_idx = s->pidx;
-    CK(launch_gemv(PRO_NORM, EPI_LOGITS, a, st));
+    a.part_alt = s->part_alt;
+    CK(launch_gemv(PRO_NORM, (state && s->n_alt > 1) ? EPI_LOGITS_ALT : EPI_LOGITS, a, st));
     return 0;
 }
 
@@ -829,7 +839,8 @@ static int enqueue_graph_step(vox_hip_stream_t* s, int splits) {
     const vox_hip_config_t& c = s->m->c;
     if (enqueue_step_layers(s, s->state, 0, nullptr, splits)) return -1;
     CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), s->state, s->tokens, s->tokens_cap,
-                           s->adapter, s->adapter_cap, s->m->tok_emb, s->m->tok_emb_s, c.dec_dim, s->xd, s->st));
+                           s->adapter, s->adapter_cap, s->m->tok_emb, s->m->tok_emb_s, c.dec_dim, s->xd,
+                           s->part_alt, s->n_alt > 1 ? s->alts : nullptr, s->st));
     return 0;
 }
 
@@ -857,6 +868,7 @@ static int build_step_graph(vox_hip_stream_t* s, int gi) {
     if (e != hipSuccess) return set_err("graph instantiate failed: %s", hipGetErrorString(e));
     s->graph_ready |= 1 << gi;
     s->graph_prof = s->profiling;
+    s->graph_alt = s->n_alt > 1;
     return 0;
 }
 
@@ -902,7 +914,7 @@ static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
             if (enqueue_graph_step(s, splits)) return -1;
         return 0;
     }
-    if (s->graph_ready && s->graph_prof != s->profiling) s->graph_ready = 0;
+    if (s->graph_ready && (s->graph_prof != s->profiling || s->graph_alt != (s->n_alt > 1))) s->graph_ready = 0;
     if (!(s->graph_ready & (1 << gi)) && build_step_graph(s, gi)) return -1;
     for (int i = 0; i < n; i++) CK(hipGraphLaunch(s->step_exec[gi], s->st));
     return 0;
@@ -978,6 +990,59 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
     s->h_state[3] = s->n_generated;
     (void)hd;
     return produced;
+}
+
+// vox_stream_set_alt (voxtral.c:1329-1337)
+extern "C" int vox_hip_stream_set_alt(vox_hip_stream_t* s, int n_alt, float cutoff) {
+    if (!s) return -1;
+    if (n_alt < 1) n_alt = 1;
+    if (n_alt > VOX_HIP_MAX_ALT) n_alt = VOX_HIP_MAX_ALT;
+    if (cutoff < 0) cutoff = 0;
+    if (cutoff > 1) cutoff = 1;
+    s->n_alt = n_alt;
+    s->alt_cutoff = cutoff;
+    return 0;
+}
+
+// stream_fill_alts (voxtral.c:955-1010) for generated steps [first, first+n): the device
+// left, per step, p_best and the three most probable text tokens other than the chosen
+// one; the reference's acceptance rule is applied here.  ids_out [n][VOX_HIP_MAX_ALT]:
+// [0] = the chosen token, then accepted alternatives, -1 after the first rejection (or
+// beyond n_alt).  probs_out (optional) holds the matching softmax probabilities.
+extern "C" int vox_hip_stream_read_alts(vox_hip_stream_t* s, int first, int n, int* ids_out,
+                                        float* probs_out) {
+    if (!s || first < 0 || n < 0 || first + n > s->n_generated) return set_err("alt range out of bounds");
+    if (n == 0) return 0;
+    std::vector<float> rec((size_t)n * ALT_REC);
+    std::vector<int> tok(n);
+    CK(hipMemcpyAsync(rec.data(), s->alts + (size_t)first * ALT_REC, rec.size() * 4, hipMemcpyDeviceToHost, s->st));
+    CK(hipMemcpyAsync(tok.data(), s->tokens + first, (size_t)n * 4, hipMemcpyDeviceToHost, s->st));
+    CK(hipStreamSynchronize(s->st));
+    for (int i = 0; i < n; i++) {
+        int* ids = ids_out + (size_t)i * VOX_HIP_MAX_ALT;
+        float* pr = probs_out ? probs_out + (size_t)i * VOX_HIP_MAX_ALT : nullptr;
+        const float* r = rec.data() + (size_t)i * ALT_REC;
+        for (int k = 0; k < VOX_HIP_MAX_ALT; k++) {
+            ids[k] = -1;
+            if (pr) pr[k] = 0.f;
+        }
+        ids[0] = tok[i];
+        if (s->n_alt <= 1) continue;
+        const float best_prob = r[0];
+        if (pr) pr[0] = best_prob;
+        if (best_prob <= 0) continue;
+        for (int k = 1; k < s->n_alt; k++) {
+            int id;
+            memcpy(&id, &r[1 + 2 * (k - 1)], 4);
+            const float p = r[2 + 2 * (k - 1)];
+            if (id < 0) break;
+            const float rr = 1.0f - p / best_prob;
+            if (rr > s->alt_cutoff) break;
+            ids[k] = id;
+            if (pr) pr[k] = p;
+        }
+    }
+    return 0;
 }
 
 extern "C" int vox_hip_stream_state(vox_hip_stream_t* s, int* out6) {
@@ -1199,7 +1264,7 @@ extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_
     int st4[4] = {0, 0, 0, 0};
     CK(hipMemcpyAsync(tmp_state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
     CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), tmp_state, nullptr, 0, nullptr, 0,
-                           nullptr, nullptr, c.dec_dim, nullptr, s->st));
+                           nullptr, nullptr, c.dec_dim, nullptr, nullptr, nullptr, s->st));
     CK(hipMemcpyAsync(st4, tmp_state, sizeof st4, hipMemcpyDeviceToHost, s->st));
     if (logits) CK(hipMemcpyAsync(logits, s->logits, (size_t)c.vocab * 4, hipMemcpyDeviceToHost, s->st));
     CK(hipStreamSynchronize(s->st));

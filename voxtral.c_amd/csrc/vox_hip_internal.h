@@ -5,7 +5,11 @@
 
 namespace vox {
 
-enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_GELU_ERF = 3, EPI_SWIGLU = 4, EPI_QKV = 5, EPI_LOGITS = 6 };
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_GELU_ERF = 3, EPI_SWIGLU = 4, EPI_QKV = 5, EPI_LOGITS = 6,
+       EPI_LOGITS_ALT = 7 };  // + softmax partials and top-4 text candidates (stream_fill_alts)
+constexpr int ALT_TEXT_MIN = 1000;   // TOKEN_TEXT_MIN (voxtral.c:399)
+constexpr int ALT_PART = 10;         // per-block alt partial: m, s, 4 values, 4 ids
+constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3, pad
 enum { PRO_NONE = 0, PRO_NORM = 1, PRO_NORM_ADA = 2 };
 
 constexpr int GEMV_MAX_BLOCKS = 1024;  // 4 blocks of 256 threads per CU on 256 CUs
@@ -30,9 +34,10 @@ struct GemvArgs {
     float* Kc;
     float* Vc;
     int cap;
-    // EPI_LOGITS
+    // EPI_LOGITS(_ALT)
     float* part_val;
     int* part_idx;
+    float* part_alt;       // EPI_LOGITS_ALT: [blocks][ALT_PART]
 };
 
 int gemv_grid(int rows);
@@ -61,7 +66,8 @@ hipError_t launch_embed_rows(const float* adapter, const void* emb, const float*
                              int first_tok, int rest_tok, int D, float* x, hipStream_t st);
 hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
                                int cap, const float* adapter, int adapter_rows,
-                               const void* emb, const float* esc, int D, float* x, hipStream_t st);
+                               const void* emb, const float* esc, int D, float* x,
+                               const float* part_alt, float* alts, hipStream_t st);
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

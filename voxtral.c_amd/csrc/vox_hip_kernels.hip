@@ -434,6 +434,28 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
 // VGPRs (cdna_hip_programming.md "GEMV / M <= 16" row).  Partial sums meet in LDS; wave
 // 0 applies the epilogue.  Summation order is fixed (deterministic).
 // ============================================================================
+// stream_fill_alts (voxtral.c:955-1010) partials for one logit: running max / sum of
+// exp for the softmax, and an ascending-id-stable top-4 of ids >= TOKEN_TEXT_MIN (rows
+// arrive in ascending order, so a strict '>' keeps the lower id first on ties).
+__device__ __forceinline__ void alt_row(float v, int r, float& am, float& as, float (&tv)[4], int (&ti)[4]) {
+    if (v > am) {
+        as = as * expf(am - v) + 1.0f;
+        am = v;
+    } else {
+        as += expf(v - am);
+    }
+    if (r >= ALT_TEXT_MIN && v > tv[3]) {
+        int k = 3;
+        while (k > 0 && v > tv[k - 1]) {
+            tv[k] = tv[k - 1];
+            ti[k] = ti[k - 1];
+            k--;
+        }
+        tv[k] = v;
+        ti[k] = r;
+    }
+}
+
 template <int EPI, int RB>
 __device__ __forceinline__ void gemv_rows(int g, int (&rows)[RB]) {
 #pragma unroll
@@ -542,6 +564,9 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     if (EPI == EPI_QKV) lp = a.state ? a.state[0] : a.pos;
     float best = -INFINITY;
     int besti = 0x7fffffff;
+    // EPI_LOGITS_ALT: online softmax partial (max, sum exp) and the 4 largest text logits
+    float am = -INFINITY, as = 0.f, tv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int ti[4] = {-1, -1, -1, -1};
     int buf = 0;
     for (;;) {
         float acc[RB];
@@ -595,12 +620,16 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 } else if (EPI == EPI_RESID) {
                     a.y[r0] += acc0 + (a.bias ? a.bias[r0] : 0.f);
                     a.y[r1] += acc1 + (a.bias ? a.bias[r1] : 0.f);
-                } else if (EPI == EPI_LOGITS) {
+                } else if (EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT) {
                     a.y[r0] = acc0;
                     a.y[r1] = acc1;
                     // first max wins (voxtral_decoder.c:771-779): rows ascend within a block
                     if (acc0 > best) { best = acc0; besti = r0; }
                     if (acc1 > best) { best = acc1; besti = r1; }
+                    if (EPI == EPI_LOGITS_ALT) {
+                        alt_row(acc0, r0, am, as, tv, ti);
+                        alt_row(acc1, r1, am, as, tv, ti);
+                    }
                 } else if (EPI == EPI_SWIGLU) {
                     a.y[gcur * (RB / 2) + (i >> 1)] = silu(acc0) * acc1;
                 } else if (EPI == EPI_QKV) {
@@ -631,9 +660,19 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         buf ^= 1;
         if (g >= ngroups) break;
     }
-    if (EPI == EPI_LOGITS && wave == 0 && lane == 0) {
+    if ((EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT) && wave == 0 && lane == 0) {
         a.part_val[blockIdx.x] = best;
         a.part_idx[blockIdx.x] = besti;
+        if (EPI == EPI_LOGITS_ALT) {
+            float* pa = a.part_alt + (size_t)blockIdx.x * ALT_PART;
+            pa[0] = am;
+            pa[1] = as;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                pa[2 + k] = tv[k];
+                pa[6 + k] = __int_as_float(ti[k]);
+            }
+        }
     }
 }
 
@@ -902,6 +941,98 @@ __global__ __launch_bounds__(256) void k_embed_rows(const float* __restrict__ ad
     for (int i = threadIdx.x; i < D; i += 256) x[(size_t)r * D + i] = a[i] + emb_at(emb, esc, tok, D, i);
 }
 
+// stream_fill_alts candidates (voxtral.c:955-1010) from the LM head's per-block partials:
+// the softmax denominator S = sum_b s_b exp(m_b - M) and the 3 largest logits with id >=
+// TOKEN_TEXT_MIN other than the chosen token (ties: lower id).  Writes the step's record
+// {p_best, id1, p1, id2, p2, id3, p3, 0}, p = exp(l - M) * (1 / S); the host applies n_alt
+// and the cutoff.  Called by all 256 threads of k_argmax_final after its barrier.
+__device__ __forceinline__ bool alt_before(float va, int ia, float vb, int ib) {
+    return va > vb || (va == vb && ia >= 0 && (ib < 0 || ia < ib));
+}
+
+__device__ void alt_merge(const float* __restrict__ pa, int n, int best, float bestv, int step,
+                          float* __restrict__ alts) {
+    __shared__ float sm[256], ss[256], stv[256][4];
+    __shared__ int sti[256][4];
+    const int t = threadIdx.x;
+    float m = -INFINITY, su = 0.f, tv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int ti[4] = {-1, -1, -1, -1};
+    for (int b = t; b < n; b += 256) {
+        const float* p = pa + (size_t)b * ALT_PART;
+        const float bm = p[0], bs = p[1];
+        if (bm > m) {
+            su = su * expf(m - bm) + bs;
+            m = bm;
+        } else if (bs > 0.f) {
+            su += bs * expf(bm - m);
+        }
+        for (int k = 0; k < 4; k++) {
+            const float v = p[2 + k];
+            const int id = __float_as_int(p[6 + k]);
+            if (id < 0 || id == best || !alt_before(v, id, tv[3], ti[3])) continue;
+            int j = 3;
+            while (j > 0 && alt_before(v, id, tv[j - 1], ti[j - 1])) {
+                tv[j] = tv[j - 1];
+                ti[j] = ti[j - 1];
+                j--;
+            }
+            tv[j] = v;
+            ti[j] = id;
+        }
+    }
+    sm[t] = m;
+    ss[t] = su;
+    for (int k = 0; k < 4; k++) {
+        stv[t][k] = tv[k];
+        sti[t][k] = ti[k];
+    }
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) {
+            const float m2 = sm[t + h], s2 = ss[t + h];
+            float m1 = sm[t], s1 = ss[t];
+            if (m2 > m1) {
+                s1 = s1 * expf(m1 - m2) + s2;
+                m1 = m2;
+            } else if (s2 > 0.f) {
+                s1 += s2 * expf(m2 - m1);
+            }
+            sm[t] = m1;
+            ss[t] = s1;
+            float ov[4];
+            int oi[4];
+            int a = 0, b = 0;
+            for (int k = 0; k < 4; k++) {
+                if (alt_before(stv[t][a], sti[t][a], stv[t + h][b], sti[t + h][b])) {
+                    ov[k] = stv[t][a];
+                    oi[k] = sti[t][a];
+                    a++;
+                } else {
+                    ov[k] = stv[t + h][b];
+                    oi[k] = sti[t + h][b];
+                    b++;
+                }
+            }
+            for (int k = 0; k < 4; k++) {
+                stv[t][k] = ov[k];
+                sti[t][k] = oi[k];
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const float M = sm[0], inv = 1.0f / ss[0];
+        float* r = alts + (size_t)step * ALT_REC;
+        r[0] = expf(bestv - M) * inv;
+        for (int k = 0; k < 3; k++) {
+            const int id = sti[0][k];
+            r[1 + 2 * k] = __int_as_float(id);
+            r[2 + 2 * k] = id >= 0 ? expf(stv[0][k] - M) * inv : 0.f;
+        }
+        r[7] = 0.f;
+    }
+}
+
 // Final argmax over per-block partials; advance the device-side step state
 // state = {logical kv pos, next adapter row, prev token, step index} and, when adapter is
 // given, build the next step's input x = adapter[row] + tok_emb[token] (voxtral.c:
@@ -914,10 +1045,12 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
                                                       int adapter_rows,
                                                       const void* __restrict__ emb,
                                                       const float* __restrict__ esc, int D,
-                                                      float* __restrict__ x) {
+                                                      float* __restrict__ x,
+                                                      const float* __restrict__ part_alt,
+                                                      float* __restrict__ alts) {
     __shared__ float sv[256];
     __shared__ int si[256];
-    __shared__ int stok, srow;
+    __shared__ int stok, srow, sstep;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
     for (int i = threadIdx.x; i < n; i += 256) {
@@ -949,6 +1082,7 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
         state[2] = tok;
         state[3] = step + 1;
         stok = tok;
+        sstep = step;
         srow = state[1];
     }
     __syncthreads();
@@ -956,6 +1090,7 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
         const float* a = adapter + (size_t)srow * D;
         for (int i = threadIdx.x; i < D; i += 256) x[i] = a[i] + emb_at(emb, esc, stok, D, i);
     }
+    if (alts && sstep < tokens_cap) alt_merge(part_alt, n, stok, sv[0], sstep, alts);
 }
 
 // im2col for the causal conv stem (voxtral_kernels.c:430-447):
@@ -1091,7 +1226,7 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
 #define GEMV_CASE(P, E) \
     if (pro == P && epi == E) return rb == 8 ? gemv_q<P, E, 8>(a, grid, st) : gemv_q<P, E, 4>(a, grid, st);
     GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_QKV)
-    GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS)
+    GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS) GEMV_CASE(PRO_NORM, EPI_LOGITS_ALT)
 #undef GEMV_CASE
     return hipErrorInvalidValue;
 }
@@ -1154,9 +1289,10 @@ hipError_t launch_embed_rows(const float* adapter, const void* emb, const float*
 
 hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state, int* tokens,
                                int cap, const float* adapter, int adapter_rows,
-                               const void* emb, const float* esc, int D, float* x, hipStream_t st) {
+                               const void* emb, const float* esc, int D, float* x,
+                               const float* part_alt, float* alts, hipStream_t st) {
     hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, pv, pi, n, state, tokens, cap,
-                       adapter, adapter_rows, emb, esc, D, x);
+                       adapter, adapter_rows, emb, esc, D, x, part_alt, alts);
     LAUNCH_CHECK();
     return hipSuccess;
 }

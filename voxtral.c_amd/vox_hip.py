@@ -38,7 +38,7 @@ EXPORTS = [
     "vox_hip_model_ada_scale", "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
-    "vox_hip_stream_state", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
+    "vox_hip_stream_state", "vox_hip_stream_set_alt", "vox_hip_stream_read_alts", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
     "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
@@ -72,6 +72,8 @@ def lib():
         "vox_hip_stream_read_adapter": (I, [P, I, I, fp]),
         "vox_hip_stream_decode": (I, [P, I, I, ip, fp]),
         "vox_hip_stream_state": (I, [P, ip]),
+        "vox_hip_stream_set_alt": (I, [P, I, F]),
+        "vox_hip_stream_read_alts": (I, [P, I, I, ip, fp]),
         "vox_hip_sgemm_bf16": (None, [I, I, I, fp, P, fp]),
         "vox_hip_sgemm_q8": (None, [I, I, I, fp, P, fp, fp]),
         "vox_hip_fused_qkv_bf16": (None, [I, I, fp, P, I, P, I, P, I, fp, fp, fp]),
@@ -201,6 +203,20 @@ class Stream:
         o = np.zeros(6, np.int32)
         lib().vox_hip_stream_state(self.h, o.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
         return dict(zip(["kv_pos", "gen_pos", "prev_token", "started", "eos_seen", "generated"], o.tolist()))
+
+    def set_alt(self, n_alt: int, cutoff: float):
+        """vox_stream_set_alt: keep up to n_alt candidates per step (1 = off)."""
+        if lib().vox_hip_stream_set_alt(self.h, n_alt, cutoff) != 0:
+            _err("set_alt")
+
+    def read_alts(self, first: int, n: int):
+        """(ids [n, 4] with -1 for none, probs [n, 4]) for generated steps [first, first+n)."""
+        ids = np.empty((n, 4), np.int32)
+        pr = np.empty((n, 4), np.float32)
+        if lib().vox_hip_stream_read_alts(self.h, first, n, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                          fptr(pr)) != 0:
+            _err("read_alts")
+        return ids, pr
 
     def set_profiling(self, on: bool):
         lib().vox_hip_stream_set_profiling(self.h, int(on))

@@ -1,3 +1,4 @@
+#include <algorithm>
 // kbench.hip -- isolated timing of the decode-step kernels (HIP events, back-to-back
 // launches on one stream).  Build: make -C tools; run: tools/kbench [iters]
 // Shapes: Voxtral-4B decoder (voxtral.h:37-48).
@@ -10,6 +11,9 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
+#ifdef VOX_GEMV_STAMPS
+namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
+#endif
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -65,6 +69,22 @@ int main(int argc, char** argv) {
     int* state;
     CK(hipMalloc(&state, 16));
 
+    {
+        hipDeviceProp_t prop;
+        CK(hipGetDeviceProperties(&prop, 0));
+        printf("device %s: %d CUs, clock %d MHz, L2 %d KB\n", prop.name, prop.multiProcessorCount, prop.clockRate / 1000, prop.l2CacheSize / 1024);
+        struct O { const char* n; int pro, epi, K, rows; int q8; };
+        for (O o : {O{"qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 0}, O{"wo", PRO_NONE, EPI_RESID, DQ, D, 0},
+                    O{"w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 0}, O{"w2", PRO_NONE, EPI_RESID, DH, D, 0},
+                    O{"lm", PRO_NORM, EPI_LOGITS, D, V, 0}, O{"qkv q8", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 1},
+                    O{"wo q8", PRO_NONE, EPI_RESID, DQ, D, 1}, O{"w13 q8", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 1},
+                    O{"w2 q8", PRO_NONE, EPI_RESID, DH, D, 1}}) {
+            GemvArgs a;
+            memset(&a, 0, sizeof a);
+            a.K = o.K; a.rows = o.rows; a.wscale = o.q8 ? (const float*)1 : nullptr;
+            printf("occupancy %-7s %d blocks/CU, grid %d\n", o.n, gemv_occupancy(gemv_kernel(o.pro, o.epi, a)), gemv_grid(o.rows));
+        }
+    }
     int layer = 0;
     float* wsc = (float*)dmalloc((size_t)V * 4, 1);  // Q8 row scales (any finite values)
     const float* qs = nullptr;  // set: the weight buffers are read as int8 rows
@@ -151,7 +171,59 @@ int main(int argc, char** argv) {
                acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, cyc / n, rt / n / 100.0,
                cyc / (rt / 100.0) / 1000.0, spread / (nrun * 32.0), gstart / nrun / 100.0);
     }
-    add("argmax+embed", timeit([&] { CK(launch_argmax_final(pv, pi, 1024, state, nullptr, 0, (float*)emb, 1024, emb, nullptr, D, x, st)); }, iters, st), 1.0);
+#ifdef VOX_GEMV_STAMPS
+    {
+        // per-block timeline of one launch of each big GEMV (s_memrealtime, 10 ns ticks)
+        const int maxb = 4096;
+        unsigned long long* dst;
+        CK(hipMalloc(&dst, (size_t)maxb * 4 * 8));
+        CK(gemv_set_stamps(dst));
+        struct T { const char* n; int pro, epi, K, rows; const float* q; };
+        for (T t : {T{"w13 bf16", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, nullptr}, T{"w2 bf16", PRO_NONE, EPI_RESID, DH, D, nullptr},
+                    T{"qkv bf16", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, nullptr}, T{"wo bf16", PRO_NONE, EPI_RESID, DQ, D, nullptr},
+                    T{"w13 q8", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, wsc}}) {
+            const uint16_t* W = t.epi == EPI_SWIGLU ? w13[5] : t.epi == EPI_QKV ? wqkv[5] : t.K == DH ? w2[5] : wo[5];
+            qs = t.q;
+            for (int r = 0; r < 3; r++) {  // last run is measured; earlier ones flush other layers' buffers
+                gemv(PRO_NONE, EPI_RESID, w2[(r + 7) % NL], DH, D);
+                CK(hipMemset(dst, 0, (size_t)maxb * 32));
+                gemv(t.pro, t.epi, W, t.K, t.rows);
+                CK(hipStreamSynchronize(st));
+            }
+            qs = nullptr;
+            const int nb = gemv_grid(t.rows);
+            std::vector<unsigned long long> h((size_t)nb * 4);
+            CK(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull;
+            for (int b = 0; b < nb; b++) t0 = std::min(t0, h[b * 4]);
+            std::vector<double> st_, fd, en;
+            for (int b = 0; b < nb; b++) {
+                st_.push_back((h[b * 4] - t0) * 0.01);
+                fd.push_back((h[b * 4 + 1] - t0) * 0.01);
+                en.push_back((h[b * 4 + 2] - t0) * 0.01);
+            }
+            auto pct = [](std::vector<double> v, double p) { std::sort(v.begin(), v.end()); return v[(size_t)(p * (v.size() - 1))]; };
+            printf("stamps %-9s blocks %4d | start p50 %.2f max %.2f | first data p10 %.2f p50 %.2f p90 %.2f | end p10 %.2f p50 %.2f p90 %.2f max %.2f us\n",
+                   t.n, nb, pct(st_, 0.5), pct(st_, 1.0), pct(fd, 0.1), pct(fd, 0.5), pct(fd, 0.9), pct(en, 0.1), pct(en, 0.5),
+                   pct(en, 0.9), pct(en, 1.0));
+            printf("   end by blockIdx%%8:");
+            for (int x = 0; x < 8; x++) {
+                std::vector<double> v;
+                for (int b = x; b < nb; b += 8) v.push_back(en[b]);
+                printf(" [%d] p10 %.1f p50 %.1f max %.1f", x, pct(v, 0.1), pct(v, 0.5), pct(v, 1.0));
+            }
+            printf("\n   end by blockIdx/256:");
+            for (int x = 0; x * 256 < nb; x++) {
+                std::vector<double> v;
+                for (int b = x * 256; b < std::min(nb, x * 256 + 256); b++) v.push_back(en[b]);
+                printf(" [%d] p10 %.1f p50 %.1f max %.1f", x, pct(v, 0.1), pct(v, 0.5), pct(v, 1.0));
+            }
+            printf("\n");
+        }
+        CK(gemv_set_stamps(nullptr));
+    }
+#endif
+    add("argmax+embed", timeit([&] { CK(launch_argmax_final(pv, pi, 1024, state, nullptr, 0, (float*)emb, 1024, emb, nullptr, D, x, nullptr, nullptr, st)); }, iters, st), 1.0);
     add("empty-ish (embed step)", timeit([&] { CK(launch_embed_step((float*)emb, emb, nullptr, state, D, x, st)); }, iters, st), 1.0);
     // whole-layer sequence (no graph)
     int st4[4] = {186, 0, 0, 0};

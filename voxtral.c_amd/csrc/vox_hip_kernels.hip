@@ -470,27 +470,36 @@ __device__ __forceinline__ void gemv_rows(int g, int (&rows)[RB]) {
     }
 }
 
-// KC = 16-B chunks per row (K/8 bf16, K/16 int8)
+// Weight rows come in through a buffer descriptor: the row offset is wave-uniform (an SGPR
+// soffset) and each lane keeps one 32-bit chunk offset per K round (voff), instead of a
+// 64-bit address per (row, round) -- the register count sets how many blocks stay resident.
+// Non-temporal (aux = 2: nt): every weight byte is read once per step.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 template <int RB, int KQ>
-__device__ __forceinline__ void gemv_load(const void* __restrict__ W, int KC,
-                                          const int (&rows)[RB], int wave, int lane,
-                                          uint4 (&wv)[KQ][RB]) {
-    // Chunks past K (K not a multiple of 16 B * 256) re-load chunk 0 and meet x = 0: every
-    // load is unconditional, so hipcc issues them all before the first wait (a guarded
-    // load makes it wait vmcnt(0) at each branch join).
-    const uint4* W4 = static_cast<const uint4*>(W);
+__device__ __forceinline__ void gemv_load(__amdgpu_buffer_rsrc_t W, int rowbytes, const int (&rows)[RB],
+                                          const int (&voff)[KQ], uint4 (&wv)[KQ][RB]) {
 #pragma unroll
-    for (int j = 0; j < KQ; j++) {
-        const int c0 = (j * 4 + wave) * 64 + lane;
-        const int c = c0 < KC ? c0 : 0;
+    for (int j = 0; j < KQ; j++)
 #pragma unroll
-        for (int i = 0; i < RB; i++) wv[j][i] = ldnt(W4 + (size_t)rows[i] * KC + c);
-    }
+        for (int i = 0; i < RB; i++) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(W, voff[j], rows[i] * rowbytes, 2);
+            wv[j][i] = make_uint4(v.x, v.y, v.z, v.w);
+        }
 }
 
 // Q8 rows (WQ8): 16-B chunks of 16 int8, so a lane holds 16 x values per chunk, and the
 // group's RB row scales are fetched with its weights (applied before the epilogue:
 // y = scale * sum + bias, voxtral_kernels.c:316).
+#ifdef VOX_GEMV_STAMPS
+// diagnostic build only (tools/kbench_stamps): per block s_memrealtime at entry, when the
+// first group's weights have been consumed, and at exit
+__device__ unsigned long long* g_gemv_stamps;
+#define GEMV_STAMP(k) \
+    do { if (g_gemv_stamps && tid == 0) g_gemv_stamps[(size_t)blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define GEMV_STAMP(k) do {} while (0)
+#endif
+
 template <int PRO, int EPI, int RB, int KQ, int WQ8>
 __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     constexpr int XPC = WQ8 ? 4 : 2;  // float4 of x per 16-B chunk
@@ -503,10 +512,25 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     int rows[RB];
     uint4 wv[KQ][RB];
     float wsc[RB];
+    GEMV_STAMP(0);
+    bool first_group = true;
+    const int rowbytes = K * (WQ8 ? 1 : 2);
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), 0, a.rows * rowbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wnone = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.W), 0, 0, 0x00020000);
+    // chunk offsets per K round; chunks past K (K not a multiple of 16 B * 256) re-load
+    // chunk 0 and meet x = 0: every load is unconditional, so hipcc issues them all before
+    // the first wait (a guarded load makes it wait vmcnt(0) at each branch join)
+    int voff[KQ];
+#pragma unroll
+    for (int j = 0; j < KQ; j++) {
+        const int c0 = (j * 4 + wave) * 64 + lane;
+        voff[j] = (c0 < KC ? c0 : 0) * 16;
+    }
     // first group's weights are independent of x: issue them before the prologue
     gemv_rows<EPI, RB>(g, rows);
-    gemv_load<RB, KQ>(a.W, KC, rows, wave, lane, wv);
-    if (WQ8 && wave == 0) {
+    gemv_load<RB, KQ>(wrs, rowbytes, rows, voff, wv);
+    if ((EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT) && WQ8 && wave == 0) {
 #pragma unroll
         for (int i = 0; i < RB; i++) wsc[i] = a.wscale[rows[i]];
     }
@@ -567,8 +591,43 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     // EPI_LOGITS_ALT: online softmax partial (max, sum exp) and the 4 largest text logits
     float am = -INFINITY, as = 0.f, tv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int ti[4] = {-1, -1, -1, -1};
+    // Epilogue ownership: lane l of wave 0 finishes row l (STORE / RESID) or row pair
+    // (2l, 2l+1) (QKV rope pairs, SWIGLU w1/w3 pairs), so the epilogue's reads (residual,
+    // bias, rope, Q8 scales) go out in parallel at the top of the iteration instead of one
+    // dependent round trip per row after the reduction.  The LM head keeps one lane (its
+    // running argmax is sequential over ascending rows).
+    constexpr bool LOGIT = (EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT);
+    constexpr bool PAIRED = (EPI == EPI_QKV || EPI == EPI_SWIGLU);
+    constexpr int NL = LOGIT ? 1 : (PAIRED ? RB / 2 : RB);
+    const bool owner = wave == 0 && lane < NL;
+    const int i0 = PAIRED ? 2 * lane : lane;
     int buf = 0;
     for (;;) {
+        const int gcur = g;
+        // epilogue inputs of this group (independent of the dot products)
+        int er0 = 0, er1 = 0;
+        float ein0 = 0.f, ein1 = 0.f, esc0 = 1.f, esc1 = 1.f;
+        if (!LOGIT && owner) {
+            int rr[RB];
+            gemv_rows<EPI, RB>(gcur, rr);
+#pragma unroll
+            for (int i = 0; i < RB; i++) {
+                if (i == i0) er0 = rr[i];
+                if (i == i0 + 1) er1 = rr[i];
+            }
+            if (WQ8) {
+                esc0 = a.wscale[er0];
+                if (PAIRED) esc1 = a.wscale[er1];
+            }
+            if (EPI == EPI_RESID) ein0 = a.y[er0] + (a.bias ? a.bias[er0] : 0.f);
+            if (EPI == EPI_STORE) ein0 = a.bias ? a.bias[er0] : 0.f;
+            if (EPI == EPI_QKV && er0 < a.qd + a.kvd) {
+                const int col = er0 < a.qd ? er0 : er0 - a.qd;
+                const float* rp = a.rope + (size_t)lp * a.hd + ((col % a.hd) & ~1);
+                ein0 = rp[0];
+                ein1 = rp[1];
+            }
+        }
         float acc[RB];
 #pragma unroll
         for (int i = 0; i < RB; i++) acc[i] = 0.f;
@@ -579,19 +638,29 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 if (WQ8) acc[i] = dot16q(wv[j][i], reinterpret_cast<const float4(&)[4]>(xr[j]), acc[i]);
                 else acc[i] = dot8(wv[j][i], xr[j][0], xr[j][XPC - 1], acc[i]);
             }
-        const int gcur = g;
+        if (first_group) {
+            GEMV_STAMP(1);
+            first_group = false;
+        }
         int rcur[RB];
         float scur[RB];
+        if (LOGIT) {
 #pragma unroll
-        for (int i = 0; i < RB; i++) {
-            rcur[i] = rows[i];
-            scur[i] = WQ8 ? wsc[i] : 1.0f;
+            for (int i = 0; i < RB; i++) {
+                rcur[i] = rows[i];
+                scur[i] = WQ8 ? wsc[i] : 1.0f;
+            }
         }
         g += gridDim.x;
-        if (g < ngroups) {  // next group's loads go out before this group's reduction
-            gemv_rows<EPI, RB>(g, rows);
-            gemv_load<RB, KQ>(a.W, KC, rows, wave, lane, wv);
-            if (WQ8 && wave == 0) {
+        // The next group's loads go out before this group's reduction, unconditionally: a
+        // load under `if (more)` keeps the old weight registers alive across the branch and
+        // doubles the weight register set (fewer resident blocks).  Past the last group they
+        // go through a zero-length descriptor: the range check returns zeros, no traffic.
+        {
+            const bool more = g < ngroups;
+            gemv_rows<EPI, RB>(more ? g : 0, rows);
+            gemv_load<RB, KQ>(more ? wrs : wnone, rowbytes, rows, voff, wv);
+            if (LOGIT && WQ8 && wave == 0) {
 #pragma unroll
                 for (int i = 0; i < RB; i++) wsc[i] = a.wscale[rows[i]];
             }
@@ -603,7 +672,37 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             for (int i = 0; i < RB; i++) red[buf][wave][i] = acc[i];
         }
         __syncthreads();
-        if (wave == 0 && lane == 0) {
+        if (!LOGIT && owner) {
+            float v0 = ((red[buf][0][i0] + red[buf][1][i0]) + red[buf][2][i0]) + red[buf][3][i0];
+            float v1 = 0.f;
+            if (PAIRED) v1 = ((red[buf][0][i0 + 1] + red[buf][1][i0 + 1]) + red[buf][2][i0 + 1]) + red[buf][3][i0 + 1];
+            if (WQ8) {
+                v0 *= esc0;
+                v1 *= esc1;
+            }
+            if (EPI == EPI_STORE || EPI == EPI_RESID) {
+                a.y[er0] = ein0 + v0;  // RESID: residual + bias were read at the top
+            } else if (EPI == EPI_SWIGLU) {
+                a.y[gcur * (RB / 2) + lane] = silu(v0) * v1;
+            } else if (EPI == EPI_QKV) {
+                if (er0 < a.qd + a.kvd) {
+                    const float o0 = v0 * ein0 - v1 * ein1, o1 = v0 * ein1 + v1 * ein0;
+                    if (er0 < a.qd) {
+                        a.y[er0] = o0;
+                        a.y[er1] = o1;
+                    } else {
+                        float* kr = a.Kc + (size_t)(lp % a.cap) * a.kvd + (er0 - a.qd);
+                        kr[0] = o0;
+                        kr[1] = o1;
+                    }
+                } else {
+                    float* vr = a.Vc + (size_t)(lp % a.cap) * a.kvd + (er0 - a.qd - a.kvd);
+                    vr[0] = v0;
+                    vr[1] = v1;
+                }
+            }
+        }
+        if (LOGIT && wave == 0 && lane == 0) {
             float v[RB];
 #pragma unroll
             for (int i = 0; i < RB; i++) {
@@ -611,55 +710,17 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 if (WQ8) v[i] *= scur[i];
             }
 #pragma unroll
-            for (int i = 0; i < RB; i += 2) {
-                const int r0 = rcur[i], r1 = rcur[i + 1];
-                const float acc0 = v[i], acc1 = v[i + 1];
-                if (EPI == EPI_STORE) {
-                    a.y[r0] = acc0 + (a.bias ? a.bias[r0] : 0.f);
-                    a.y[r1] = acc1 + (a.bias ? a.bias[r1] : 0.f);
-                } else if (EPI == EPI_RESID) {
-                    a.y[r0] += acc0 + (a.bias ? a.bias[r0] : 0.f);
-                    a.y[r1] += acc1 + (a.bias ? a.bias[r1] : 0.f);
-                } else if (EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT) {
-                    a.y[r0] = acc0;
-                    a.y[r1] = acc1;
-                    // first max wins (voxtral_decoder.c:771-779): rows ascend within a block
-                    if (acc0 > best) { best = acc0; besti = r0; }
-                    if (acc1 > best) { best = acc1; besti = r1; }
-                    if (EPI == EPI_LOGITS_ALT) {
-                        alt_row(acc0, r0, am, as, tv, ti);
-                        alt_row(acc1, r1, am, as, tv, ti);
-                    }
-                } else if (EPI == EPI_SWIGLU) {
-                    a.y[gcur * (RB / 2) + (i >> 1)] = silu(acc0) * acc1;
-                } else if (EPI == EPI_QKV) {
-                    const int hd = a.hd;
-                    if (r0 < a.qd + a.kvd) {
-                        const int col = r0 < a.qd ? r0 : r0 - a.qd;
-                        const int d = (col % hd) >> 1;
-                        const float* rp = a.rope + (size_t)lp * hd;
-                        const float cs = rp[2 * d], sn = rp[2 * d + 1];
-                        const float o0 = acc0 * cs - acc1 * sn, o1 = acc0 * sn + acc1 * cs;
-                        if (r0 < a.qd) {
-                            a.y[r0] = o0;
-                            a.y[r1] = o1;
-                        } else {
-                            float* kr = a.Kc + (size_t)(lp % a.cap) * a.kvd;
-                            kr[col] = o0;
-                            kr[col + 1] = o1;
-                        }
-                    } else {
-                        const int col = r0 - a.qd - a.kvd;
-                        float* vr = a.Vc + (size_t)(lp % a.cap) * a.kvd;
-                        vr[col] = acc0;
-                        vr[col + 1] = acc1;
-                    }
-                }
+            for (int i = 0; i < RB; i++) {
+                a.y[rcur[i]] = v[i];
+                // first max wins (voxtral_decoder.c:771-779): rows ascend within a block
+                if (v[i] > best) { best = v[i]; besti = rcur[i]; }
+                if (EPI == EPI_LOGITS_ALT) alt_row(v[i], rcur[i], am, as, tv, ti);
             }
         }
         buf ^= 1;
         if (g >= ngroups) break;
     }
+    GEMV_STAMP(2);
     if ((EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT) && wave == 0 && lane == 0) {
         a.part_val[blockIdx.x] = best;
         a.part_idx[blockIdx.x] = besti;
@@ -1202,6 +1263,24 @@ int gemv_grid(int rows) {
 }
 
 template <int P, int E, int RB, int Q8>
+static const void* gemv_fn(int kq) {
+    switch (kq) {
+        case 1: return reinterpret_cast<const void*>(&k_gemv<P, E, RB, 1, Q8>);
+        case 2: return reinterpret_cast<const void*>(&k_gemv<P, E, RB, 2, Q8>);
+        case 3: return reinterpret_cast<const void*>(&k_gemv<P, E, RB, 3, Q8>);
+        case 4: return reinterpret_cast<const void*>(&k_gemv<P, E, RB, 4, Q8>);
+        case 5: return reinterpret_cast<const void*>(&k_gemv<P, E, RB, 5, Q8>);
+        default: return nullptr;
+    }
+}
+
+int gemv_occupancy(const void* fn) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 256, 0) != hipSuccess) occ = 0;
+    return occ;
+}
+
+template <int P, int E, int RB, int Q8>
 static hipError_t gemv_k(const GemvArgs& a, int grid, hipStream_t st) {
     const int kq = ((Q8 ? a.K >> 4 : a.K >> 3) + 255) / 256;
     switch (kq) {
@@ -1212,6 +1291,20 @@ static hipError_t gemv_k(const GemvArgs& a, int grid, hipStream_t st) {
     }
     LAUNCH_CHECK();
     return hipSuccess;
+}
+
+// kernel instance launch_gemv would use (tools, occupancy queries)
+const void* gemv_kernel(int pro, int epi, const GemvArgs& a) {
+    const int rb = gemv_rb(a.rows);
+    const int kq = ((a.wscale ? a.K >> 4 : a.K >> 3) + 255) / 256;
+#define GEMV_FN(P, E)                                                                     \
+    if (pro == P && epi == E)                                                             \
+        return rb == 8 ? (a.wscale ? gemv_fn<P, E, 8, 1>(kq) : gemv_fn<P, E, 8, 0>(kq))   \
+                       : (a.wscale ? gemv_fn<P, E, 4, 1>(kq) : gemv_fn<P, E, 4, 0>(kq));
+    GEMV_FN(PRO_NONE, EPI_STORE) GEMV_FN(PRO_NONE, EPI_RESID) GEMV_FN(PRO_NORM, EPI_QKV)
+    GEMV_FN(PRO_NORM_ADA, EPI_SWIGLU) GEMV_FN(PRO_NORM, EPI_LOGITS) GEMV_FN(PRO_NORM, EPI_LOGITS_ALT)
+#undef GEMV_FN
+    return nullptr;
 }
 
 template <int P, int E, int RB>
@@ -1262,6 +1355,9 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
     LAUNCH_CHECK();
     return hipSuccess;
 }
+#ifdef VOX_GEMV_STAMPS
+hipError_t gemv_set_stamps(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_gemv_stamps), &p, sizeof p); }
+#endif
 // diagnostic variants for tools/kbench (not used by the engine)
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st) {

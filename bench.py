@@ -154,7 +154,10 @@ def main():
     for _ in range(args.warmup):
         transcribe(st, mel_dev, cfg.mel_bins)
 
-    st.set_profiling(True)   # HIP events around the W1|W3 GEMV on the stream's own queue
+    # HIP events recorded by each W1|W3 launch's own dispatch packet (hipExtLaunchKernel) on
+    # the stream's queue; profiled decode steps are launched eagerly (a graph cannot carry
+    # dispatch events), which runs as fast as the graph replay
+    st.set_profiling(True)
     runs = []
     d.barrier()
     st.sync()

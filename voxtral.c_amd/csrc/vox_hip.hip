@@ -454,10 +454,10 @@ struct vox_hip_stream {
     int h_state[4];
     // profiling
     int profiling;
-    int graph_prof;               // the captured step graph carries event-record nodes
+    int graph_prof;               // the last (eager, profiled) steps recorded W1|W3 events
     int capturing;
     hipEvent_t evt[2];
-    std::vector<hipEvent_t> pev;  // [2*dec_layers] around each W1|W3 GEMV in the graph
+    std::vector<hipEvent_t> pev;  // [2*dec_layers] start/stop of each layer's W1|W3 GEMV
     double prof_ms, prof_bytes;
     long long prof_launches;
 };
@@ -802,11 +802,10 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         memset(&a, 0, sizeof a);
         a.x = s->xd; a.K = DD; a.W = L.w13; a.wscale = L.s13; a.rows = 2 * DH; a.norm_w = L.ffn_norm;
         a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
-        const bool gprof = s->profiling && state && (int)s->pev.size() == 2 * c.dec_layers;
-        const unsigned evflag = s->capturing ? hipEventRecordExternal : 0;
-        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l], st, evflag));
-        CK(launch_gemv(PRO_NORM_ADA, EPI_SWIGLU, a, st));
-        if (gprof) CK(hipEventRecordWithFlags(s->pev[2 * l + 1], st, evflag));
+        // profiling: HIP events recorded by the W1|W3 launch's own dispatch (eager steps)
+        const bool gprof = s->profiling && state && !s->capturing && (int)s->pev.size() == 2 * c.dec_layers;
+        if (gprof) CK(launch_gemv_timed(PRO_NORM_ADA, EPI_SWIGLU, a, s->pev[2 * l], s->pev[2 * l + 1], st));
+        else CK(launch_gemv(PRO_NORM_ADA, EPI_SWIGLU, a, st));
         // W2 + residual (decoder.c:758-760)
         memset(&a, 0, sizeof a);
         a.x = s->gated; a.K = DH; a.W = L.w2; a.wscale = L.s2; a.rows = DD; a.y = s->xd;
@@ -845,10 +844,6 @@ static int enqueue_graph_step(vox_hip_stream_t* s, int splits) {
 }
 
 static int build_step_graph(vox_hip_stream_t* s, int gi) {
-    if (s->profiling && s->pev.empty()) {
-        s->pev.resize(2 * s->m->c.dec_layers);
-        for (auto& e : s->pev) CK(hipEventCreate(&e));
-    }
     if (s->step_exec[gi]) {
         hipGraphExecDestroy(s->step_exec[gi]);
         s->step_exec[gi] = nullptr;
@@ -867,13 +862,12 @@ static int build_step_graph(vox_hip_stream_t* s, int gi) {
     hipGraphDestroy(g);
     if (e != hipSuccess) return set_err("graph instantiate failed: %s", hipGetErrorString(e));
     s->graph_ready |= 1 << gi;
-    s->graph_prof = s->profiling;
     s->graph_alt = s->n_alt > 1;
     return 0;
 }
 
-// Sampled kernel timing: after a batch of replays, the event pair around each layer's
-// W1|W3 GEMV holds the last replay's duration on the stream the kernel ran on.
+// Sampled kernel timing: after a batch of profiled steps, each layer's W1|W3 event pair
+// (recorded by the kernel's dispatch packet) holds the last step's kernel duration.
 static int collect_graph_profile(vox_hip_stream_t* s) {
     if (!s->profiling || !s->graph_prof) return 0;
     const vox_hip_config_t& c = s->m->c;
@@ -902,9 +896,11 @@ static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
     const vox_hip_config_t& c = s->m->c;
     const int gi = graph_index(s, std::min(pos0 + n, c.dec_window));
     const int splits = graph_splits(s, gi);
-    if (!use_graphs()) {
-        // eager launches of the same device-state kernels (profilers that cannot follow
-        // graph replays; VOX_HIP_GRAPH=0)
+    if (!use_graphs() || s->profiling) {
+        // eager launches of the same device-state kernels: profiling (the W1|W3 launches
+        // carry dispatch-recorded HIP events, which a graph cannot hold), profilers that
+        // cannot follow graph replays (VOX_HIP_GRAPH=0).  Measured as fast as the graph
+        // replay on MI355X (kernels are long enough for the host to stay ahead).
         if (s->profiling && s->pev.empty()) {
             s->pev.resize(2 * c.dec_layers);
             for (auto& e : s->pev) CK(hipEventCreate(&e));
@@ -914,7 +910,7 @@ static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
             if (enqueue_graph_step(s, splits)) return -1;
         return 0;
     }
-    if (s->graph_ready && (s->graph_prof != s->profiling || s->graph_alt != (s->n_alt > 1))) s->graph_ready = 0;
+    if (s->graph_ready && s->graph_alt != (s->n_alt > 1)) s->graph_ready = 0;
     if (!(s->graph_ready & (1 << gi)) && build_step_graph(s, gi)) return -1;
     for (int i = 0; i < n; i++) CK(hipGraphLaunch(s->step_exec[gi], s->st));
     return 0;
@@ -1056,7 +1052,6 @@ extern "C" int vox_hip_stream_state(vox_hip_stream_t* s, int* out6) {
 }
 
 extern "C" int vox_hip_stream_set_profiling(vox_hip_stream_t* s, int enable) {
-    if (s->profiling != enable) s->graph_ready = 0;
     s->profiling = enable;
     s->prof_ms = 0;
     s->prof_bytes = 0;

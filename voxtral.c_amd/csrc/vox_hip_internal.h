@@ -54,6 +54,8 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
                              int k_first, int window, float scale, hipStream_t st);
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st);
 const void* gemv_kernel(int pro, int epi, const GemvArgs& a);
+hipError_t launch_gemv_timed(int pro, int epi, const GemvArgs& a, hipEvent_t start, hipEvent_t stop,
+                             hipStream_t st);
 int gemv_occupancy(const void* fn);
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,

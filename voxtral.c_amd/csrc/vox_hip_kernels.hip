@@ -17,6 +17,7 @@
 #include "vox_hip_internal.h"
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace vox {
@@ -1310,6 +1311,18 @@ const void* gemv_kernel(int pro, int epi, const GemvArgs& a) {
 template <int P, int E, int RB>
 static hipError_t gemv_q(const GemvArgs& a, int grid, hipStream_t st) {
     return a.wscale ? gemv_k<P, E, RB, 1>(a, grid, st) : gemv_k<P, E, RB, 0>(a, grid, st);
+}
+
+// The same launch with HIP events recorded by the kernel's own dispatch packet
+// (hipExtLaunchKernel): they bracket the kernel itself, not the marker packets an
+// event-record node adds.  Eager launches only (not capturable into a graph).
+hipError_t launch_gemv_timed(int pro, int epi, const GemvArgs& a, hipEvent_t start, hipEvent_t stop,
+                             hipStream_t st) {
+    const void* fn = gemv_kernel(pro, epi, a);
+    if (!fn) return hipErrorInvalidValue;
+    GemvArgs args = a;
+    void* kargs[] = {&args};
+    return hipExtLaunchKernel(fn, dim3(gemv_grid(a.rows)), dim3(256), kargs, 0, st, start, stop, 0);
 }
 
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {

@@ -418,6 +418,7 @@ extern "C" int vox_hip_model_ada_scale(vox_hip_model_t* m, float* out) {
 static const int ENC_SUB = 1024;      // encoder rows per pass through the 32 layers
 static const int DEC_SLACK = 64;      // decoder ring capacity = window + slack
 static const int STEP_BATCH = 16;     // graph replays between EOS checks
+static const size_t GEMM_WS_ELEMS = (size_t)8 << 20;  // split-K workspace (32 MB)
 
 struct vox_hip_stream {
     vox_hip_stream() { memset((void*)this, 0, offsetof(vox_hip_stream, pev)); }
@@ -443,6 +444,8 @@ struct vox_hip_stream {
     // decoder
     float *xd, *xnd, *qkvd, *qd_, *attd, *gated, *part, *logits, *pval;
     float *part_alt, *alts;  // stream_fill_alts partials / per-step records [tokens_cap][ALT_REC]
+    float* gws;              // split-K GEMM partials (encoder / prefill / adapter)
+    size_t gws_n;
     int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
     float alt_cutoff;
     int graph_alt;           // alt mode the step graphs were captured with
@@ -542,6 +545,8 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->ad_mid, (size_t)(ENC_SUB / 4 + 4) * c.dec_dim));
     TRYH(dalloc(&s->part, (size_t)c.dec_heads * attn_maxch(c.dec_window) * (c.dec_head_dim + 2)));
     TRYH(dalloc(&s->part_alt, (size_t)GEMV_MAX_BLOCKS * ALT_PART));
+    s->gws_n = GEMM_WS_ELEMS;
+    TRYH(dalloc(&s->gws, s->gws_n));
     TRYH(dalloc(&s->logits, (size_t)c.vocab));
     TRYH(dalloc(&s->pval, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
@@ -571,7 +576,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->tokens);
-    dfree(s->part_alt); dfree(s->alts);
+    dfree(s->part_alt); dfree(s->alts); dfree(s->gws);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
     for (hipEvent_t e : s->pev) hipEventDestroy(e);
@@ -625,13 +630,13 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
         float* Kc = s->ek + (size_t)l * s->ecap * EKV;
         float* Vc = s->ev + (size_t)l * s->ecap * EKV;
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.attn_norm, nullptr, n, ED, c.enc_eps, st));
-        CK(launch_gemm(EPI_STORE, 3, s->xn, ED, L.wqkv, L.sqkv, ED, n, EQ + 2 * EKV, L.bqkv, s->qkv, EQ + 2 * EKV, st));
+        CK(launch_gemm(EPI_STORE, 3, s->xn, ED, L.wqkv, L.sqkv, ED, n, EQ + 2 * EKV, L.bqkv, s->qkv, EQ + 2 * EKV, st, s->gws, s->gws_n));
         CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
         CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st));
-        CK(launch_gemm(EPI_RESID, 3, s->att, EQ, L.wo, L.so, EQ, n, ED, L.bo, x, ED, st));
+        CK(launch_gemm(EPI_RESID, 3, s->att, EQ, L.wo, L.so, EQ, n, ED, L.bo, x, ED, st, s->gws, s->gws_n));
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.ffn_norm, nullptr, n, ED, c.enc_eps, st));
-        CK(launch_gemm(EPI_SWIGLU, 3, s->xn, ED, L.w13, L.s13, ED, n, 2 * EH, nullptr, s->gate, EH, st));
-        CK(launch_gemm(EPI_RESID, 3, s->gate, EH, L.w2, L.s2, EH, n, ED, L.b2, x, ED, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, s->xn, ED, L.w13, L.s13, ED, n, 2 * EH, nullptr, s->gate, EH, st, s->gws, s->gws_n));
+        CK(launch_gemm(EPI_RESID, 3, s->gate, EH, L.w2, L.s2, EH, n, ED, L.b2, x, ED, st, s->gws, s->gws_n));
     }
     CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, n, ED, c.enc_eps, st));
     return 0;
@@ -667,7 +672,7 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
     float* c0_new = s->c0_p + (size_t)(2 + s->res_count) * ED;
     CK(launch_im2col3(s->mel_p, MB, n, 1, 0, s->im2col, st));
     CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, MB * 3, m->conv0_w, nullptr, MB * 3, n, ED,
-                   m->conv0_b, c0_new, ED, st));
+                   m->conv0_b, c0_new, ED, st, s->gws, s->gws_n));
     // ---- stride alignment (voxtral.c:653-692) ----
     const int total = s->res_count + n;
     const int new_res = total & 1;
@@ -685,7 +690,7 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
     float* xin = s->x_enc + (size_t)4 * ED;  // 4 spare rows in front for the downsample residual
     CK(launch_im2col3(s->c0_p, ED, T1, 2, 1, s->im2col, st));
     CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, s->im2col, ED * 3, m->conv1_w, nullptr, ED * 3, T1, ED,
-                   m->conv1_b, xin, ED, st));
+                   m->conv1_b, xin, ED, st, s->gws, s->gws_n));
     CK(hipMemcpyAsync(s->c0_tail, s->c0_p + (size_t)(2 + feed - 2) * ED, (size_t)2 * ED * 4,
                       hipMemcpyDeviceToDevice, st));
     // ---- encoder (voxtral_encoder.c:495-693), sub-chunks through all layers ----
@@ -711,9 +716,9 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
         for (int r0 = 0; r0 < n4; r0 += ENC_SUB / 4) {
             int nr = std::min(ENC_SUB / 4, n4 - r0);
             CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, ain + (size_t)r0 * 4 * ED, 4 * ED, m->ad0, m->ad0_s,
-                           4 * ED, nr, D, nullptr, s->ad_mid, D, st));
+                           4 * ED, nr, D, nullptr, s->ad_mid, D, st, s->gws, s->gws_n));
             CK(launch_gemm(EPI_STORE, 3, s->ad_mid, D, m->ad1, m->ad1_s, D, nr, D, nullptr,
-                           s->adapter + (size_t)(s->total_adapter + r0) * D, D, st));
+                           s->adapter + (size_t)(s->total_adapter + r0) * D, D, st, s->gws, s->gws_n));
         }
         s->total_adapter += n4;
         added = n4;
@@ -755,13 +760,13 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
         float* Kc = s->dk + (size_t)l * s->dcap * DKV;
         float* Vc = s->dv + (size_t)l * s->dcap * DKV;
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.attn_norm, nullptr, n, DD, c.dec_eps, st));
-        CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, L.sqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st));
+        CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, L.sqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st, s->gws, s->gws_n));
         CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st));
         CK(launch_attn_tiled(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st));
-        CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, L.so, DQ, n, DD, nullptr, x, DD, st));
+        CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, L.so, DQ, n, DD, nullptr, x, DD, st, s->gws, s->gws_n));
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, n, DD, c.dec_eps, st));
-        CK(launch_gemm(EPI_SWIGLU, 3, s->xnd, DD, L.w13, L.s13, DD, n, 2 * DH, nullptr, s->gated, DH, st));
-        CK(launch_gemm(EPI_RESID, 3, s->gated, DH, L.w2, L.s2, DH, n, DD, nullptr, x, DD, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, s->xnd, DD, L.w13, L.s13, DD, n, 2 * DH, nullptr, s->gated, DH, st, s->gws, s->gws_n));
+        CK(launch_gemm(EPI_RESID, 3, s->gated, DH, L.w2, L.s2, DH, n, DD, nullptr, x, DD, st, s->gws, s->gws_n));
     }
     return 0;
 }
@@ -1074,6 +1079,7 @@ extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
 static std::mutex g_twin_mu;
 static std::unordered_map<const void*, uint8_t*> g_wcache;  // host weight ptr -> device copy
 static hipStream_t g_twin_st = nullptr;
+static float* g_twin_ws = nullptr;  // split-K partials of the twin GEMMs
 static float *g_tA = nullptr, *g_tC = nullptr, *g_tQ = nullptr, *g_tK = nullptr, *g_tV = nullptr, *g_tO = nullptr;
 static size_t g_tA_n = 0, g_tC_n = 0, g_tQ_n = 0, g_tK_n = 0, g_tV_n = 0, g_tO_n = 0;
 
@@ -1109,7 +1115,8 @@ static int twin_gemm(int M, int N, int K, const float* dA, const void* dW, const
         CK(launch_gemv(PRO_NONE, EPI_STORE, a, g_twin_st));
         return 0;
     }
-    CK(launch_gemm(EPI_STORE, 3, dA, K, dW, dS, K, M, N, nullptr, dC, N, g_twin_st));
+    if (!g_twin_ws) CK(dalloc(&g_twin_ws, GEMM_WS_ELEMS));
+    CK(launch_gemm(EPI_STORE, 3, dA, K, dW, dS, K, M, N, nullptr, dC, N, g_twin_st, g_twin_ws, GEMM_WS_ELEMS));
     return 0;
 }
 

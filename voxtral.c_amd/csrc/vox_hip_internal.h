@@ -6,7 +6,8 @@
 namespace vox {
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_GELU_ERF = 3, EPI_SWIGLU = 4, EPI_QKV = 5, EPI_LOGITS = 6,
-       EPI_LOGITS_ALT = 7 };  // + softmax partials and top-4 text candidates (stream_fill_alts)
+       EPI_LOGITS_ALT = 7,
+       EPI_PARTIAL = 8 };  // split-K GEMM slice: raw f32 tile into a workspace, epilogue in k_splitk_reduce  // + softmax partials and top-4 text candidates (stream_fill_alts)
 constexpr int ALT_TEXT_MIN = 1000;   // TOKEN_TEXT_MIN (voxtral.c:399)
 constexpr int ALT_PART = 10;         // per-block alt partial: m, s, 4 values, 4 ids
 constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3, pad
@@ -44,9 +45,11 @@ int gemv_grid(int rows);
 int attn_maxch(int window);
 hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,
                                const float* ada, int M, int D, float eps, hipStream_t st);
+// ws: f32 workspace for split-K partials (ws_elems floats; nullptr = no split)
 hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void* W,
                        const float* wscale, int K, int M, int N, const float* bias, float* C,
-                       int ldc, hipStream_t st);
+                       int ldc, hipStream_t st, float* ws = nullptr, size_t ws_elems = 0);
+int gemm_ksplit(int M, int N, int K, size_t ws_elems);
 hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, const float* rope,
                           int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st);
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,

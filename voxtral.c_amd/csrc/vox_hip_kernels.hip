@@ -171,12 +171,14 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // split-K: slice z of gridDim.z covers K range [kb, kb + Ks) (EPI_PARTIAL only)
+    const int Ks = K / gridDim.z, kb = blockIdx.z * Ks;
     const bool arow_ok = (m0 + srow) < M;
     const float* Ap = A + (size_t)(m0 + srow) * lda + skq;
     const uint16_t* Wp = static_cast<const uint16_t*>(W) + (size_t)(n0 + srow) * K + skq;
     const int8_t* Wq = static_cast<const int8_t*>(W) + (size_t)(n0 + srow) * K + skq;
 
-    for (int k0 = 0; k0 < K; k0 += GB_K) {
+    for (int k0 = kb; k0 < kb + Ks; k0 += GB_K) {
         float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
         if (arow_ok) {
             a0 = *reinterpret_cast<const float4*>(Ap + k0);
@@ -249,7 +251,11 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
         for (int r = 0; r < 4; r++) {
             const int m = m0 + wr * 32 + mi * 16 + rq + r;
             if (m >= M) continue;
-            if (EPI == EPI_SWIGLU) {
+            if (EPI == EPI_PARTIAL) {
+#pragma unroll
+                for (int ni = 0; ni < 2; ni++)
+                    C[((size_t)blockIdx.z * M + m) * N + n0 + wc * 32 + ni * 16 + cc] = acc[mi][ni][r];
+            } else if (EPI == EPI_SWIGLU) {
                 // wave's 32 columns = one interleave group: tile 0 = w1 rows, tile 1 = w3 rows
                 const int g = (n0 + wc * 32) >> 5;
                 const int j = g * 16 + cc;
@@ -275,6 +281,46 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
             }
         }
     }
+}
+
+// ============================================================================
+// Split-K finish: sum the S partial tiles in slice order (deterministic), then the GEMM
+// epilogue (Q8 row scale, bias, residual / GELU / SwiGLU pairing) as in k_gemm.
+// One thread per output element; part is [S][M][N].
+// ============================================================================
+template <int EPI>
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ part, int S, int M, int N,
+                                                       const float* __restrict__ wscale,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ C, int ldc) {
+    const int NO = EPI == EPI_SWIGLU ? N / 2 : N;  // output columns
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)M * NO) return;
+    const int m = (int)(idx / NO), j = (int)(idx % NO);
+    const size_t MN = (size_t)M * N;
+    if (EPI == EPI_SWIGLU) {
+        const int n1 = (j >> 4) * 32 + (j & 15), n3 = n1 + 16;  // w1 / w3 rows of unit j
+        float g = 0.f, u = 0.f;
+        for (int z = 0; z < S; z++) {
+            g += part[z * MN + (size_t)m * N + n1];
+            u += part[z * MN + (size_t)m * N + n3];
+        }
+        if (wscale) {
+            g *= wscale[n1];
+            u *= wscale[n3];
+        }
+        C[(size_t)m * ldc + j] = silu(g) * u;
+        return;
+    }
+    float v = 0.f;
+    for (int z = 0; z < S; z++) v += part[z * MN + (size_t)m * N + j];
+    if (wscale) v *= wscale[j];
+    if (bias) v += bias[j];
+    float* cp = C + (size_t)m * ldc + j;
+    if (EPI == EPI_STORE) *cp = v;
+    else if (EPI == EPI_RESID) *cp += v;
+    else if (EPI == EPI_GELU) *cp = gelu_tanh(v);
+    else if (EPI == EPI_GELU_ERF) *cp = gelu_erf(v);
 }
 
 // ============================================================================
@@ -1199,9 +1245,36 @@ hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const
     return hipSuccess;
 }
 
+// K slices for a GEMM: enough blocks to cover the CUs twice when the (M, N) tiles alone do
+// not (prefill M = 38, the N = 1280 encoder projections), each slice >= 4 K steps, the
+// partials within the workspace.
+int gemm_ksplit(int M, int N, int K, size_t ws_elems) {
+    const int tiles = (N / GB_N) * ((M + GB_M - 1) / GB_M);
+    int s = 1;
+    while (tiles * s < 512 && K % (2 * s * GB_K) == 0 && K / (2 * s) >= 4 * GB_K &&
+           (size_t)(2 * s) * M * N <= ws_elems)
+        s *= 2;
+    return s;
+}
+
 template <int EPI, int NS>
 static hipError_t gemm_t(const float* A, int lda, const void* W, const float* wscale, int K, int M,
-                         int N, const float* bias, float* C, int ldc, hipStream_t st) {
+                         int N, const float* bias, float* C, int ldc, hipStream_t st, float* ws,
+                         size_t ws_elems) {
+    const int S = ws ? gemm_ksplit(M, N, K, ws_elems) : 1;
+    if (S > 1) {
+        dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M, S);
+        if (wscale)
+            hipLaunchKernelGGL((k_gemm<EPI_PARTIAL, NS, 1>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, nullptr, ws, N);
+        else
+            hipLaunchKernelGGL((k_gemm<EPI_PARTIAL, NS, 0>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, nullptr, ws, N);
+        LAUNCH_CHECK();
+        const size_t outs = (size_t)M * (EPI == EPI_SWIGLU ? N / 2 : N);
+        hipLaunchKernelGGL(k_splitk_reduce<EPI>, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, ws, S, M, N,
+                           wscale, bias, C, ldc);
+        LAUNCH_CHECK();
+        return hipSuccess;
+    }
     dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M);
     if (wscale)
         hipLaunchKernelGGL((k_gemm<EPI, NS, 1>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
@@ -1213,11 +1286,11 @@ static hipError_t gemm_t(const float* A, int lda, const void* W, const float* ws
 
 hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void* W,
                        const float* wscale, int K, int M, int N, const float* bias, float* C,
-                       int ldc, hipStream_t st) {
+                       int ldc, hipStream_t st, float* ws, size_t ws_elems) {
     if (M <= 0) return hipSuccess;
     if (N % GB_N || K % GB_K || lda % 4) return hipErrorInvalidValue;
 #define GEMM_CASE(E, S) \
-    if (epi == E && nsplit == S) return gemm_t<E, S>(A, lda, W, wscale, K, M, N, bias, C, ldc, st);
+    if (epi == E && nsplit == S) return gemm_t<E, S>(A, lda, W, wscale, K, M, N, bias, C, ldc, st, ws, ws_elems);
     GEMM_CASE(EPI_STORE, 1) GEMM_CASE(EPI_STORE, 2) GEMM_CASE(EPI_STORE, 3)
     GEMM_CASE(EPI_RESID, 1) GEMM_CASE(EPI_RESID, 2) GEMM_CASE(EPI_RESID, 3)
     GEMM_CASE(EPI_GELU, 1) GEMM_CASE(EPI_GELU, 2) GEMM_CASE(EPI_GELU, 3)

@@ -117,6 +117,25 @@ int main(int argc, char** argv) {
     add("q8 gemv w2   (3072x9216)", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH);
     add("q8 gemv lm   (131072x3072)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D);
     qs = nullptr;
+    {
+        // M>1 GEMMs of the encoder / prefill (useful TFLOP/s = 2 M N K / t)
+        float* ws = (float*)dmalloc((size_t)8 << 22, 0);
+        float* Am = (float*)dmalloc((size_t)1024 * 9216 * 4, 1);
+        float* Cm = (float*)dmalloc((size_t)1024 * 18432 * 4, 0);
+        struct G { const char* n; int epi, M, N, K; const uint16_t* W; };
+        for (G g : {G{"enc qkv  677x6144x1280", EPI_STORE, 677, 6144, 1280, wqkv[1]},
+                    G{"enc w13  677x10240x1280", EPI_SWIGLU, 677, 10240, 1280, w13[1]},
+                    G{"enc wo   677x1280x2048", EPI_RESID, 677, 1280, 2048, wo[1]},
+                    G{"enc w2   677x1280x5120", EPI_RESID, 677, 1280, 5120, w2[1]},
+                    G{"pre w2   38x3072x9216", EPI_RESID, 38, 3072, 9216, w2[2]},
+                    G{"pre w13  38x18432x3072", EPI_SWIGLU, 38, 18432, 3072, w13[2]}}) {
+            const int ldc = g.epi == EPI_SWIGLU ? g.N / 2 : g.N;
+            double us = timeit([&] { CK(launch_gemm(g.epi, 3, Am, g.K, g.W, nullptr, g.K, g.M, g.N, nullptr, Cm, ldc, st, ws, (size_t)8 << 20)); }, 20, st);
+            char nm[80];
+            snprintf(nm, sizeof nm, "gemm %s", g.n);
+            printf("%-34s %9.2f us  %8.1f TFLOP/s (useful)\n", nm, us, 2.0 * g.M * g.N * g.K / us / 1e6);
+        }
+    }
     for (int L : {64, 187, 256, 1000, 4096, 8192}) {
         int st4[4] = {L - 1, 0, 0, 0};
         CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));

@@ -36,11 +36,11 @@ __device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(
 __device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// round-to-nearest-even f32 -> bf16 bits (inputs are finite activations)
+// round-to-nearest-even f32 -> bf16 bits: the native conversion (hipcc emits
+// v_cvt_pk_bf16_f32 on gfx950, two values per instruction)
 __device__ __forceinline__ uint32_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return u >> 16;
+    const __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(unsigned short, b);
 }
 
 // Cross-lane reductions: DPP inside each 16-lane row (quad_perm xor1 / xor2, row half
@@ -282,6 +282,203 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
         }
     }
 }
+
+// ============================================================================
+// Pipelined MFMA GEMM (the production M>1 path): C[M,N] (op)= A[M,K] * W[N,K]^T.
+// Block tile 128x128, 4 waves in 2x2, each wave 64x64 = 4x4 v_mfma_f32_16x16x32_bf16
+// tiles (the large wave tile keeps the LDS fragment traffic of the 3 A planes under the
+// LDS rate).  K advances in 64-deep stages: the stage's A (f32) and W tiles are loaded to
+// registers one stage ahead (issued before the current stage's MFMAs), split into the three
+// bf16 planes hi/mid/lo (A = hi + mid + lo exactly; Q8 weights -> exact bf16) and written
+// to one of two LDS buffers, so one barrier per stage suffices.  Epilogues as k_gemm
+// (incl. EPI_PARTIAL for split-K slices over blockIdx.z).
+// ============================================================================
+#define G2_M 128
+#define G2_N 128
+#define G2_K 64
+#define G2_LDS (G2_K + 8)  // padded bf16 row (144 B)
+#ifndef VOX_G2_DIAG
+#define VOX_G2_DIAG 0  // kbench diagnostics only: 1 = no MFMA, 2 = no staging
+#endif
+
+// k_gemm2 staging: 32 A floats and 32 W elements per thread (row t/2, k half (t&1)*32)
+struct G2Regs {  // one stage's staging registers (named members: kept in VGPRs)
+    float4 a0, a1, a2, a3, a4, a5, a6, a7;
+    uint4 w0, w1, w2, w3;
+};
+
+template <int WQ8>
+__device__ __forceinline__ void g2_load(G2Regs& r, const float* __restrict__ Ap, const uint16_t* __restrict__ Wp,
+                                        const int8_t* __restrict__ Wq, int ko) {
+    const float4* a = reinterpret_cast<const float4*>(Ap + ko);
+    r.a0 = a[0]; r.a1 = a[1]; r.a2 = a[2]; r.a3 = a[3];
+    r.a4 = a[4]; r.a5 = a[5]; r.a6 = a[6]; r.a7 = a[7];
+    if (WQ8) {
+        const uint4* q = reinterpret_cast<const uint4*>(Wq + ko);
+        r.w0 = q[0];
+        r.w1 = q[1];
+    } else {
+        const uint4* w = reinterpret_cast<const uint4*>(Wp + ko);
+        r.w0 = w[0]; r.w1 = w[1]; r.w2 = w[2]; r.w3 = w[3];
+    }
+}
+
+// split A into the hi/mid/lo bf16 planes (exact), W to bf16 (Q8: exact), into one LDS buffer
+template <int WQ8>
+__device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int srow, int sk, float amask) {
+    constexpr int PLANE = 128 * (64 + 8);
+    const float4 ra[8] = {r.a0, r.a1, r.a2, r.a3, r.a4, r.a5, r.a6, r.a7};
+    const uint4 rw[4] = {r.w0, r.w1, r.w2, r.w3};
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        float v[8] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w, ra[i + 1].x, ra[i + 1].y, ra[i + 1].z, ra[i + 1].w};
+        uint32_t t[3][8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            float r = v[e] * amask;
+#pragma unroll
+            for (int p = 0; p < 3; p++) {
+                const uint32_t bb = f2bf(r);
+                t[p][e] = bb;
+                r = r - __uint_as_float(bb << 16);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+            uint4 pk;
+            pk.x = t[p][0] | (t[p][1] << 16);
+            pk.y = t[p][2] | (t[p][3] << 16);
+            pk.z = t[p][4] | (t[p][5] << 16);
+            pk.w = t[p][6] | (t[p][7] << 16);
+            *reinterpret_cast<uint4*>(base + p * PLANE + srow * 72 + sk + 4 * i) = pk;
+        }
+    }
+    uint16_t* wb = base + 3 * PLANE + srow * 72 + sk;
+    if (WQ8) {
+        const uint32_t d[8] = {rw[0].x, rw[0].y, rw[0].z, rw[0].w, rw[1].x, rw[1].y, rw[1].z, rw[1].w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t h[8];
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) {
+                h[bb] = __float_as_uint(i8f(d[2 * i], bb)) >> 16;
+                h[4 + bb] = __float_as_uint(i8f(d[2 * i + 1], bb)) >> 16;
+            }
+            uint4 pk;
+            pk.x = h[0] | (h[1] << 16);
+            pk.y = h[2] | (h[3] << 16);
+            pk.z = h[4] | (h[5] << 16);
+            pk.w = h[6] | (h[7] << 16);
+            *reinterpret_cast<uint4*>(wb + 8 * i) = pk;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) *reinterpret_cast<uint4*>(wb + 8 * i) = rw[i];
+    }
+}
+
+template <int EPI, int WQ8>
+__global__ __launch_bounds__(256, 2) void k_gemm2(const float* __restrict__ A, int lda,
+                                                  const void* __restrict__ W, int K, int M, int N,
+                                                  const float* __restrict__ wscale,
+                                                  const float* __restrict__ bias,
+                                                  float* __restrict__ C, int ldc) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t g2_lds[];
+    // [buf][plane 0..2 = A hi/mid/lo, 3 = W][128][G2_LDS]
+    constexpr int PLANE = G2_M * G2_LDS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int m0 = blockIdx.y * G2_M, n0 = blockIdx.x * G2_N;
+    const int Ks = K / gridDim.z, kb = blockIdx.z * Ks;
+    const int nst = Ks / G2_K;
+    // staging: thread -> (row t/2, 32 consecutive k at (t&1)*32)
+    const int srow = tid >> 1, sk = (tid & 1) * 32;
+    const int arow = min(m0 + srow, M - 1);
+    const float amask = (m0 + srow) < M ? 1.0f : 0.0f;
+    const float* Ap = A + (size_t)arow * lda + kb + sk;
+    const uint16_t* Wp = static_cast<const uint16_t*>(W) + (size_t)(n0 + srow) * K + kb + sk;
+    const int8_t* Wq = static_cast<const int8_t*>(W) + (size_t)(n0 + srow) * K + kb + sk;
+
+    G2Regs rg;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    g2_load<WQ8>(rg, Ap, Wp, Wq, 0);
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+    for (int st = 0; st < nst; st++) {
+        if (st) __syncthreads();  // the previous stage's fragments have been read
+#if VOX_G2_DIAG != 2
+        g2_store<WQ8>(rg, g2_lds, srow, sk, amask);
+        if (st + 1 < nst) g2_load<WQ8>(rg, Ap, Wp, Wq, (st + 1) * G2_K);  // in flight during this stage's MFMAs
+#endif
+        __syncthreads();
+#if VOX_G2_DIAG == 1
+        continue;
+#endif
+        const uint16_t* base = g2_lds;
+#pragma unroll
+        for (int kk = 0; kk < G2_K; kk += 32) {
+            bf16x8 bfrag[4];
+#pragma unroll
+            for (int ni = 0; ni < 4; ni++)
+                bfrag[ni] = *reinterpret_cast<const bf16x8*>(base + 3 * PLANE + (wc * 64 + ni * 16 + fr) * G2_LDS + kk + fk);
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+#pragma unroll
+                for (int mi = 0; mi < 4; mi++) {
+                    const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(base + p * PLANE + (wr * 64 + mi * 16 + fr) * G2_LDS + kk + fk);
+#pragma unroll
+                    for (int ni = 0; ni < 4; ni++)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag[ni], acc[mi][ni], 0, 0, 0);
+                }
+        }
+    }
+
+    // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r
+    const int cc = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+    for (int mi = 0; mi < 4; mi++) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int m = m0 + wr * 64 + mi * 16 + rq + r;
+            if (m >= M) continue;
+            if (EPI == EPI_PARTIAL) {
+#pragma unroll
+                for (int ni = 0; ni < 4; ni++)
+                    C[((size_t)blockIdx.z * M + m) * N + n0 + wc * 64 + ni * 16 + cc] = acc[mi][ni][r];
+            } else if (EPI == EPI_SWIGLU) {
+                // 16-row interleave: tiles (0,1) and (2,3) are (w1, w3) of one unit group
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int nb = n0 + wc * 64 + h * 32;
+                    float gt = acc[mi][2 * h][r], up = acc[mi][2 * h + 1][r];
+                    if (WQ8) {
+                        gt *= wscale[nb + cc];
+                        up *= wscale[nb + 16 + cc];
+                    }
+                    C[(size_t)m * ldc + (nb >> 5) * 16 + cc] = silu(gt) * up;
+                }
+            } else {
+#pragma unroll
+                for (int ni = 0; ni < 4; ni++) {
+                    const int n = n0 + wc * 64 + ni * 16 + cc;
+                    float v = acc[mi][ni][r];
+                    if (WQ8) v *= wscale[n];
+                    if (bias) v += bias[n];
+                    float* cp = C + (size_t)m * ldc + n;
+                    if (EPI == EPI_STORE) *cp = v;
+                    else if (EPI == EPI_RESID) *cp += v;
+                    else if (EPI == EPI_GELU) *cp = gelu_tanh(v);
+                    else if (EPI == EPI_GELU_ERF) *cp = gelu_erf(v);
+                }
+            }
+        }
+    }
+}
+constexpr size_t G2_LDS_BYTES = (size_t)4 * G2_M * G2_LDS * 2;  // 73,728 B: two blocks per CU
 
 // ============================================================================
 // Split-K finish: sum the S partial tiles in slice order (deterministic), then the GEMM
@@ -1257,10 +1454,58 @@ int gemm_ksplit(int M, int N, int K, size_t ws_elems) {
     return s;
 }
 
+// k_gemm2 split count: two 128x128 blocks per CU (LDS), so a launch of T tiles x S slices
+// runs ceil(T S / 512) rounds of K/(64 S) stages (~1.3 us each, two blocks sharing a CU);
+// a split adds the partial tiles' round trip (2 S M N 4 B at ~5 TB/s) and the reduce.
+static int gemm2_ksplit(int M, int N, int K, size_t ws_elems) {
+    const int tiles = (N / G2_N) * ((M + G2_M - 1) / G2_M);
+    int best = 1;
+    double best_t = 1e30;
+    for (int s = 1; s <= 32; s *= 2) {
+        if (K % (s * G2_K) || (s > 1 && ((size_t)s * M * N > ws_elems || K / s < 2 * G2_K))) break;
+        const double rounds = (double)((tiles * s + 511) / 512);
+        double t = rounds * (K / s / G2_K) * 1.3;
+        if (s > 1) t += 4.0 + 2.0 * s * (double)M * N * 4 / 5e6;
+        if (t < best_t) { best_t = t; best = s; }
+    }
+    return best;
+}
+
+template <int E, int Q>
+static hipError_t gemm2_launch(dim3 grid, hipStream_t st, const float* A, int lda, const void* W, int K,
+                               int M, int N, const float* wscale, const float* bias, float* C, int ldc) {
+    static bool attr = false;  // opt in to > 64 KB of dynamic LDS once per instance
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm2<E, Q>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)G2_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_gemm2<E, Q>), grid, dim3(256), G2_LDS_BYTES, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
+    return hipGetLastError();
+}
+
 template <int EPI, int NS>
 static hipError_t gemm_t(const float* A, int lda, const void* W, const float* wscale, int K, int M,
                          int N, const float* bias, float* C, int ldc, hipStream_t st, float* ws,
                          size_t ws_elems) {
+    if (NS == 3 && N % G2_N == 0 && K % G2_K == 0 && lda % 4 == 0) {
+        const int S = ws ? gemm2_ksplit(M, N, K, ws_elems) : 1;
+        if (S > 1) {
+            dim3 grid(N / G2_N, (M + G2_M - 1) / G2_M, S);
+            hipError_t e = wscale ? gemm2_launch<EPI_PARTIAL, 1>(grid, st, A, lda, W, K, M, N, wscale, nullptr, ws, N)
+                                  : gemm2_launch<EPI_PARTIAL, 0>(grid, st, A, lda, W, K, M, N, wscale, nullptr, ws, N);
+            if (e != hipSuccess) return e;
+            const size_t outs = (size_t)M * (EPI == EPI_SWIGLU ? N / 2 : N);
+            hipLaunchKernelGGL(k_splitk_reduce<EPI>, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, ws, S, M,
+                               N, wscale, bias, C, ldc);
+            LAUNCH_CHECK();
+            return hipSuccess;
+        }
+        dim3 grid(N / G2_N, (M + G2_M - 1) / G2_M, 1);
+        return wscale ? gemm2_launch<EPI, 1>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc)
+                      : gemm2_launch<EPI, 0>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
+    }
     const int S = ws ? gemm_ksplit(M, N, K, ws_elems) : 1;
     if (S > 1) {
         dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M, S);

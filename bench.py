@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=8, help="oracle decode steps in the CPU sample")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="config 4: streams per GPU decoded together (batched weight reads)")
     ap.add_argument("--q8", action="store_true",
                     help="config 5: Q8 weights (the quantize.py layout, quantised from the seeded bf16 set)")
     return ap.parse_args()
@@ -95,6 +97,25 @@ def transcribe(st, mel_dev, n_mel):
     t3 = time.perf_counter()
     return {"enc": t1 - t0, "prefill": t2 - t1, "steps": len(rest), "step_s": t3 - t2,
             "tokens": np.concatenate([first, rest])}
+
+
+def transcribe_batch(batch, streams, mel_dev, n_mel):
+    """config 4: S jfk-shaped transcriptions per GPU, encoders one after another, each
+    stream's prefill + first token alone, then every stream's greedy steps batched."""
+    t0 = time.perf_counter()
+    for i, st in enumerate(streams):
+        st.reset()
+        off = 0
+        for n in JFK_CHUNKS:
+            st.encode_mel_device(mel_dev[i].ptr + off * n_mel * 4, n)
+            off += n
+    t1 = time.perf_counter()
+    first = [st.decode(max_steps=1, stop_at_eos=False) for st in streams]
+    t2 = time.perf_counter()
+    rest = batch.decode(streams, max_steps=1 << 16, stop_at_eos=False)
+    t3 = time.perf_counter()
+    return {"enc": t1 - t0, "prefill": t2 - t1, "steps": sum(len(r) for r in rest), "step_s": t3 - t2,
+            "tokens": [np.concatenate([f, r]) for f, r in zip(first, rest)]}
 
 
 def cpu_baseline(cfg, weights, mel, n_steps, q8=False):
@@ -150,6 +171,8 @@ def main():
     rng = np.random.default_rng(1234 + d.rank)
     mel = rng.uniform(-0.6, 1.4, size=(sum(JFK_CHUNKS), cfg.mel_bins)).astype(np.float32)
     mel_dev = vox_hip.DeviceArray(mel)
+    if args.streams > 1:
+        return bench_streams(args, d, cfg, model, st, mel, mel_dev, rng)
 
     for _ in range(args.warmup):
         transcribe(st, mel_dev, cfg.mel_bins)
@@ -227,6 +250,54 @@ def main():
         print(json.dumps(out), flush=True)
     mel_dev.free()
     st.close()
+    model.close()
+
+
+def bench_streams(args, d, cfg, model, st0, mel0, mel_dev0, rng):
+    """config 4 (BASELINE.json configs[3]): S concurrent streams per GPU, batched decode."""
+    import vox_hip
+    S = args.streams
+    streams = [st0] + [vox_hip.Stream(model) for _ in range(S - 1)]
+    mels = [mel_dev0] + [vox_hip.DeviceArray(rng.uniform(-0.6, 1.4, size=mel0.shape).astype(np.float32))
+                         for _ in range(S - 1)]
+    batch = vox_hip.Batch(model, S)
+    for _ in range(args.warmup):
+        transcribe_batch(batch, streams, mels, cfg.mel_bins)
+    runs = []
+    d.barrier()
+    streams[0].sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runs.append(transcribe_batch(batch, streams, mels, cfg.mel_bins))
+    t1 = time.perf_counter()
+    d.barrier()
+    wall = d.max(t1 - t0)
+    dec_s = d.max(sum(r["step_s"] for r in runs))
+    steps_all = d.sum(sum(r["steps"] for r in runs))
+    tok_s = steps_all / dec_s
+    enc_s = d.max(sum(r["enc"] for r in runs))
+    out = {
+        "metric": "decoder tokens/sec + encoder RTF, Voxtral-4B " + ("q8" if args.q8 else "bf16")
+                  + f", {S} streams per MI355X (config 4), at 1/2/4/8 MI355X",
+        "value": round(tok_s, 2), "unit": "tokens/s", "n_gpus": d.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall * 1000.0 / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": round(tok_s / d.world / MPS_TOK_S, 2),
+        "dtype": "f32", "weights_dtype": "q8" if args.q8 else "bf16",
+        "data": "synthetic (seeded random weights of the exact architecture; synthetic log-mel per stream)",
+        "config": {"workload": f"{S} jfk.wav-shaped transcriptions per GPU; per-stream encoder and prefill, "
+                               "greedy steps batched across the streams (one weight read per step)",
+                   "model": "Voxtral-Mini-4B-Realtime", "global_batch": S * d.world, "seq_len": 149,
+                   "streams_per_gpu": S, "parallelism": f"replicas x{d.world}, {S} streams each"},
+        "encoder_rtf": round(enc_s / (AUDIO_SECONDS * S * args.steps), 5),
+        "decoder_ms_per_batched_step": round(dec_s * 1000.0 / max(1, steps_all / d.world / S), 4),
+    }
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    batch.close()
+    for m_ in mels:
+        m_.free()
+    for s_ in streams:
+        s_.close()
     model.close()
 
 

@@ -136,6 +136,20 @@ int vox_hip_stream_decode(vox_hip_stream_t *s, int max_steps, int stop_at_eos,
 #define VOX_HIP_MAX_ALT 4
 int vox_hip_stream_set_alt(vox_hip_stream_t *s, int n_alt, float cutoff);
 int vox_hip_stream_read_alts(vox_hip_stream_t *s, int first, int n, int *ids_out, float *probs_out);
+/* Cross-stream batched greedy decoding (C4; the reference decodes each
+ * vox_stream_t separately, voxtral.c:1105-1145).  A batch object holds scratch for up to
+ * max_streams (<= 16) streams of one model.  vox_hip_batch_decode advances every listed
+ * stream that has adapter rows left by one greedy token per step; the weights are streamed
+ * once per step for all of them, attention / KV / argmax use each stream's own state.
+ * Streams not started yet are prefilled first (their first token included).  Results and
+ * device state are exactly those of vox_hip_stream_decode on each stream (up to f32
+ * summation order of the shared GEMMs).  tokens_out: [n][max_steps]; counts_out[n].
+ * Returns the total number of tokens, < 0 on error. */
+typedef struct vox_hip_batch vox_hip_batch_t;
+vox_hip_batch_t *vox_hip_batch_create(vox_hip_model_t *m, int max_streams);
+void vox_hip_batch_free(vox_hip_batch_t *b);
+int vox_hip_batch_decode(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, int max_steps,
+                         int stop_at_eos, int *tokens_out, int *counts_out);
 /* Decoder state snapshot: [0]=kv logical length, [1]=next adapter row, [2]=prev token,
  * [3]=started, [4]=eos_seen, [5]=tokens generated. */
 int vox_hip_stream_state(vox_hip_stream_t *s, int *out6);

@@ -1,0 +1,81 @@
+"""Cross-stream batched decoding (C4) against per-stream decoding and the
+CPU oracle.  The batched step shares each weight GEMM across the streams (M = streams), so
+logits differ from the single-stream GEMV only in f32 summation order: greedy ids must be
+identical per stream, whatever mix of positions, lengths and start states the batch holds."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _mels(cfg, sizes, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.uniform(-0.6, 1.4, size=(n, cfg.mel_bins)).astype(np.float32) for n in sizes]
+
+
+def _reference_tokens(om, mel):
+    import vox_oracle
+    st = vox_oracle.OracleStream(om)
+    st.encode_mel(mel)
+    t = st.decode(stop_at_eos=False)
+    st.close()
+    return t.tolist()
+
+
+@pytest.fixture(scope="module")
+def models(tiny_cfg, tiny_weights):
+    import vox_hip
+    import vox_oracle
+    hm = vox_hip.Model(tiny_cfg, tiny_weights)
+    om = vox_oracle.OracleModel(tiny_cfg, tiny_weights)
+    yield hm, om
+    hm.close()
+    om.close()
+
+
+@pytest.mark.parametrize("nstreams", [1, 3, 8])
+def test_batch_matches_single_and_oracle(models, tiny_cfg, nstreams):
+    import vox_hip
+    hm, om = models
+    sizes = [400 + 37 * i for i in range(nstreams)]   # ragged lengths: streams drop out
+    mels = _mels(tiny_cfg, sizes, 100 + nstreams)
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 8)
+    got = b.decode(ss, max_steps=1000, stop_at_eos=False)
+    for i, mel in enumerate(mels):
+        ref = _reference_tokens(om, mel)
+        single = vox_hip.Stream(hm)
+        single.encode_mel(mel)
+        one = single.decode(stop_at_eos=False).tolist()
+        assert one == ref, i
+        assert got[i].tolist() == ref, (i, len(got[i]), len(ref))
+        single.close()
+    for s in ss:
+        s.close()
+    b.close()
+
+
+def test_batch_mixed_positions_and_continuation(models, tiny_cfg):
+    """streams at different decode positions (one advanced alone first), decoding resumed
+    in several batch calls and finished on the single-stream path."""
+    import vox_hip
+    hm, om = models
+    mels = _mels(tiny_cfg, [520, 600, 480, 700], 7)
+    refs = [_reference_tokens(om, m) for m in mels]
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    first = ss[1].decode(max_steps=5, stop_at_eos=False).tolist()   # ahead of the others
+    b = vox_hip.Batch(hm, 4)
+    out = [[] for _ in ss]
+    out[1] += first
+    for _ in range(2):
+        for i, t in enumerate(b.decode(ss, max_steps=9, stop_at_eos=False)):
+            out[i] += t.tolist()
+    for i, s in enumerate(ss):
+        out[i] += s.decode(stop_at_eos=False).tolist()
+        assert out[i] == refs[i], i
+        s.close()
+    b.close()

@@ -150,6 +150,7 @@ struct vox_hip_model {
     std::vector<std::vector<float>> ada_down, ada_up;
     float *rope_enc, *rope_dec;    // device tables [rope_positions][hd]
     int rope_positions;
+    int rope_gen;                  // bumped when the tables are reallocated (graphs hold the pointer)
 };
 
 static int upload(void* dst, const void* src, size_t bytes) {
@@ -271,6 +272,7 @@ static int model_rope_tables(vox_hip_model_t* m, int positions) {
     host_rope(t.data(), 0, positions, c.dec_head_dim, c.rope_theta);
     CK(hipMemcpy(m->rope_dec, t.data(), (size_t)positions * c.dec_head_dim * 4, hipMemcpyHostToDevice));
     m->rope_positions = positions;
+    m->rope_gen++;
     return 0;
 }
 
@@ -449,6 +451,7 @@ struct vox_hip_stream {
     int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
     float alt_cutoff;
     int graph_alt;           // alt mode the step graphs were captured with
+    int graph_rope_gen;      // model rope table generation the step graphs were captured with
     int *pidx, *state, *tokens;
     int dec_rows_cap, tokens_cap;
     hipGraphExec_t step_exec[STEP_GRAPHS];  // [g]: attention with 2^g key splits (g = 0: no combine)
@@ -868,6 +871,7 @@ static int build_step_graph(vox_hip_stream_t* s, int gi) {
     if (e != hipSuccess) return set_err("graph instantiate failed: %s", hipGetErrorString(e));
     s->graph_ready |= 1 << gi;
     s->graph_alt = s->n_alt > 1;
+    s->graph_rope_gen = s->m->rope_gen;
     return 0;
 }
 
@@ -915,7 +919,7 @@ static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
             if (enqueue_graph_step(s, splits)) return -1;
         return 0;
     }
-    if (s->graph_ready && s->graph_alt != (s->n_alt > 1)) s->graph_ready = 0;
+    if (s->graph_ready && (s->graph_alt != (s->n_alt > 1) || s->graph_rope_gen != s->m->rope_gen)) s->graph_ready = 0;
     if (!(s->graph_ready & (1 << gi)) && build_step_graph(s, gi)) return -1;
     for (int i = 0; i < n; i++) CK(hipGraphLaunch(s->step_exec[gi], s->st));
     return 0;
@@ -1283,4 +1287,193 @@ extern "C" void* vox_hip_device_upload(const void* host, size_t bytes) {
 extern "C" int vox_hip_device_free(void* dev) {
     CK(hipFree(dev));
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Cross-stream batched greedy decoding (C4).  Row i of every batch
+// activation buffer belongs to stream i; the weight GEMMs run once per step for all rows
+// (M = streams), attention / RoPE / KV append / argmax use each stream's own state, rings
+// and adapter rows.  Each stream's device state and token log advance exactly as in
+// vox_hip_stream_decode, so streams can switch between the two paths.
+// ---------------------------------------------------------------------------
+struct vox_hip_batch {
+    vox_hip_model_t* m;
+    int cap;
+    hipStream_t st;
+    float *x, *xn, *qkv, *q, *att, *gated, *logits, *pval;
+    int* pidx;
+    float* gws;
+    size_t gws_n;
+};
+
+extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
+    if (!b) return;
+    if (b->st) hipStreamSynchronize(b->st);
+    dfree(b->x); dfree(b->xn); dfree(b->qkv); dfree(b->q); dfree(b->att); dfree(b->gated);
+    dfree(b->logits); dfree(b->pval); dfree(b->pidx); dfree(b->gws);
+    if (b->st) hipStreamDestroy(b->st);
+    delete b;
+}
+
+extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_streams) {
+    if (!m || max_streams < 1 || max_streams > VOX_MAX_BATCH) {
+        set_err("batch size must be 1..%d", VOX_MAX_BATCH);
+        return nullptr;
+    }
+    const vox_hip_config_t& c = m->c;
+    vox_hip_batch_t* b = new vox_hip_batch_t();
+    memset((void*)b, 0, sizeof *b);
+    b->m = m;
+    b->cap = max_streams;
+    const size_t B = max_streams, D = c.dec_dim, QKV = c.dec_heads * c.dec_head_dim + 2 * c.dec_kv_heads * c.dec_head_dim;
+    auto fail = [&]() -> vox_hip_batch_t* { vox_hip_batch_free(b); return nullptr; };
+#define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
+    TRYH(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
+    TRYH(dalloc(&b->x, B * D));
+    TRYH(dalloc(&b->xn, B * D));
+    TRYH(dalloc(&b->qkv, B * QKV));
+    TRYH(dalloc(&b->q, B * c.dec_heads * c.dec_head_dim));
+    TRYH(dalloc(&b->att, B * c.dec_heads * c.dec_head_dim));
+    TRYH(dalloc(&b->gated, B * c.dec_hidden));
+    TRYH(dalloc(&b->logits, B * c.vocab));
+    TRYH(dalloc(&b->pval, B * ARGB));
+    TRYH(dalloc(&b->pidx, B * ARGB));
+    b->gws_n = GEMM_WS_ELEMS;
+    TRYH(dalloc(&b->gws, b->gws_n));
+#undef TRYH
+    return b;
+}
+
+// one batched step over the nb streams in ss (their input rows already in b->x)
+static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, int splits) {
+    vox_hip_model_t* m = b->m;
+    const vox_hip_config_t& c = m->c;
+    const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
+    const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = b->st;
+    StepPtrs sp;
+    memset(&sp, 0, sizeof sp);
+    AttnPtrs ap;
+    memset(&ap, 0, sizeof ap);
+    for (int i = 0; i < nb; i++) {
+        sp.state[i] = ss[i]->state;
+        sp.tokens[i] = ss[i]->tokens;
+        sp.adapter[i] = ss[i]->adapter;
+        sp.adapter_rows[i] = ss[i]->adapter_cap;
+        ap.q[i] = b->q + (size_t)i * DQ;
+        ap.state[i] = ss[i]->state;
+        ap.part[i] = ss[i]->part;
+        ap.out[i] = b->att + (size_t)i * DQ;
+    }
+    const int cap = ss[0]->dcap;
+    for (int l = 0; l < c.dec_layers; l++) {
+        const DecLayerD& L = m->dec[l];
+        for (int i = 0; i < nb; i++) {
+            sp.Kc[i] = ss[i]->dk + (size_t)l * cap * DKV;
+            sp.Vc[i] = ss[i]->dv + (size_t)l * cap * DKV;
+            ap.Kc[i] = sp.Kc[i];
+            ap.Vc[i] = sp.Vc[i];
+        }
+        CK(launch_rmsnorm_rows(b->x, DD, b->xn, DD, L.attn_norm, nullptr, nb, DD, c.dec_eps, st));
+        CK(launch_gemm(EPI_STORE, 3, b->xn, DD, L.wqkv, L.sqkv, DD, nb, DQ + 2 * DKV, nullptr, b->qkv, DQ + 2 * DKV,
+                       st, b->gws, b->gws_n));
+        CK(launch_rope_kv_batch(b->qkv, nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
+        CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st));
+        CK(launch_gemm(EPI_RESID, 3, b->att, DQ, L.wo, L.so, DQ, nb, DD, nullptr, b->x, DD, st, b->gws, b->gws_n));
+        CK(launch_rmsnorm_rows(b->x, DD, b->xn, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, nb, DD, c.dec_eps, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, b->xn, DD, L.w13, L.s13, DD, nb, 2 * DH, nullptr, b->gated, DH, st, b->gws,
+                       b->gws_n));
+        CK(launch_gemm(EPI_RESID, 3, b->gated, DH, L.w2, L.s2, DH, nb, DD, nullptr, b->x, DD, st, b->gws, b->gws_n));
+    }
+    // final norm + LM head (tied embeddings) + per-stream argmax, next inputs (decoder.c:762-779)
+    CK(launch_rmsnorm_rows(b->x, DD, b->xn, DD, m->dec_norm, nullptr, nb, DD, c.dec_eps, st));
+    CK(launch_gemm(EPI_STORE, 3, b->xn, DD, m->tok_emb, m->tok_emb_s, DD, nb, c.vocab, nullptr, b->logits, c.vocab, st,
+                   b->gws, b->gws_n));
+    CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, sp, ss[0]->tokens_cap, m->tok_emb, m->tok_emb_s,
+                           DD, b->x, st));
+    return 0;
+}
+
+// host mirror after `produced` device steps of stream s (as vox_hip_stream_decode)
+static void stream_steps_done(vox_hip_stream_t* s, int produced, int last_token) {
+    s->n_generated += produced;
+    s->h_state[0] += produced;
+    s->h_state[1] += produced;
+    if (produced) s->h_state[2] = last_token;
+    s->h_state[3] = s->n_generated;
+}
+
+extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, int max_steps,
+                                    int stop_at_eos, int* tokens_out, int* counts_out) {
+    if (!b || n < 1 || n > b->cap || max_steps < 0) return set_err("bad batch arguments");
+    vox_hip_model_t* m = b->m;
+    const vox_hip_config_t& c = m->c;
+    const int D = c.dec_dim;
+    for (int i = 0; i < n; i++) {
+        if (!streams[i] || streams[i]->m != m) return set_err("batch streams must share the batch's model");
+        for (int j = 0; j < i; j++)
+            if (streams[j] == streams[i]) return set_err("stream listed twice in a batch");
+        counts_out[i] = 0;
+    }
+    int total = 0;
+    // streams not started yet: prefill + first token on their own stream (voxtral.c:1036-1061)
+    for (int i = 0; i < n; i++) {
+        vox_hip_stream_t* s = streams[i];
+        if (!s->started && max_steps > 0 && !s->eos_seen) {
+            const int r = vox_hip_stream_decode(s, 1, stop_at_eos, tokens_out + (size_t)i * max_steps, nullptr);
+            if (r < 0) return -1;
+            counts_out[i] = r;
+            total += r;
+        }
+        CK(hipStreamSynchronize(s->st));  // the batch stream reads the stream's buffers
+    }
+    std::vector<vox_hip_stream_t*> act;
+    std::vector<int> idx;
+    std::vector<int> tok;
+    for (;;) {
+        // active set: started, no EOS, steps left, an adapter row for the next step
+        act.clear();
+        idx.clear();
+        int steps = max_steps;
+        for (int i = 0; i < n; i++) {
+            vox_hip_stream_t* s = streams[i];
+            const int avail = s->total_adapter - s->h_state[1];
+            const int left = std::min(max_steps - counts_out[i], s->tokens_cap - s->n_generated);
+            if (!s->started || s->eos_seen || avail <= 0 || left <= 0) continue;
+            act.push_back(s);
+            idx.push_back(i);
+            steps = std::min(steps, std::min(avail, left));
+        }
+        if (act.empty()) break;
+        const int nb = (int)act.size();
+        steps = std::min(steps, STEP_BATCH);
+        int longest = 0;
+        for (vox_hip_stream_t* s : act) {
+            longest = std::max(longest, s->h_state[0] + steps);
+            if (ensure_rope(s, (long long)s->h_state[0] + steps + 1)) return -1;
+        }
+        const int splits = graph_splits(act[0], graph_index(act[0], std::min(longest, c.dec_window)));
+        for (int i = 0; i < nb; i++)
+            CK(launch_embed_step(act[i]->adapter, m->tok_emb, m->tok_emb_s, act[i]->state, D, b->x + (size_t)i * D,
+                                 b->st));
+        for (int k = 0; k < steps; k++)
+            if (batch_step(b, act.data(), nb, splits)) return -1;
+        CK(hipStreamSynchronize(b->st));
+        for (int i = 0; i < nb; i++) {
+            vox_hip_stream_t* s = act[i];
+            tok.resize(steps);
+            CK(hipMemcpy(tok.data(), s->tokens + s->n_generated, (size_t)steps * 4, hipMemcpyDeviceToHost));
+            int produced = steps;
+            if (stop_at_eos)
+                for (int k = 0; k < steps; k++)
+                    if (tok[k] == TOKEN_EOS) { produced = k + 1; s->eos_seen = 1; break; }
+            int* out = tokens_out + (size_t)idx[i] * max_steps + counts_out[idx[i]];
+            memcpy(out, tok.data(), (size_t)produced * 4);
+            counts_out[idx[i]] += produced;
+            total += produced;
+            stream_steps_done(s, produced, tok[produced - 1]);
+        }
+    }
+    return total;
 }

@@ -41,6 +41,28 @@ struct GemvArgs {
     float* part_alt;       // EPI_LOGITS_ALT: [blocks][ALT_PART]
 };
 
+constexpr int VOX_MAX_BATCH = 16;    // streams per batched decode step
+// per-stream operands of one decode-attention launch (blockIdx.z = stream of a batch)
+struct AttnPtrs {
+    const float* q[VOX_MAX_BATCH];
+    const float* Kc[VOX_MAX_BATCH];
+    const float* Vc[VOX_MAX_BATCH];
+    const int* state[VOX_MAX_BATCH];
+    float* part[VOX_MAX_BATCH];
+    float* out[VOX_MAX_BATCH];
+};
+
+// per-stream state of a batched decode step (row i of the batch = stream i)
+struct StepPtrs {
+    int* state[VOX_MAX_BATCH];          // {kv logical pos, next adapter row, prev token, step}
+    float* Kc[VOX_MAX_BATCH];           // layer base of the stream's decoder K ring
+    float* Vc[VOX_MAX_BATCH];
+    int* tokens[VOX_MAX_BATCH];         // the stream's token log (tokens_cap entries)
+    const float* adapter[VOX_MAX_BATCH];
+    int adapter_rows[VOX_MAX_BATCH];
+};
+constexpr int ARGB = 64;                // argmax partial blocks per row
+
 int gemv_grid(int rows);
 int attn_maxch(int window);
 hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,
@@ -63,7 +85,11 @@ int gemv_occupancy(const void* fn);
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
                               int KVH, float* part, float* out, int splits, hipStream_t st);
+// the same over nb streams at once (device state positions; pointers per stream)
+hipError_t launch_attn_decode_batch(int hd, const AttnPtrs& p, int nb, int cap, int window, float scale,
+                                    int H, int KVH, int splits, hipStream_t st);
 constexpr int ATT_BLOCK_KEYS = 256;  // keys one decode-attention block covers
+
 constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st);
@@ -75,6 +101,11 @@ hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state
                                int cap, const float* adapter, int adapter_rows,
                                const void* emb, const float* esc, int D, float* x,
                                const float* part_alt, float* alts, hipStream_t st);
+hipError_t launch_rope_kv_batch(const float* qkv, int nb, int qd, int kvd, int hd, const float* rope,
+                                const StepPtrs& sp, int cap, float* q, hipStream_t st);
+hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, const StepPtrs& sp,
+                               int tokens_cap, const void* emb, const float* esc, int D, float* x,
+                               hipStream_t st);
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
+#include <string.h>
 
 namespace vox {
 
@@ -999,13 +1000,16 @@ constexpr int ATT_WAVES = 16;   // waves per block (1024 threads)
 constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per block
 
 template <int HD, int HPB, int DBG = 0>
-__global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ q,
-                                                      const float* __restrict__ Kc,
-                                                      const float* __restrict__ Vc, int cap,
-                                                      const int* __restrict__ state, int pos_host,
+__global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap, int pos_host,
                                                       int window, float scale, int H, int KVH,
-                                                      int maxs, float* __restrict__ part,
-                                                      float* __restrict__ out) {
+                                                      int maxs) {
+    const int zb = blockIdx.z;  // stream of a batched step (0 for a single stream)
+    const float* __restrict__ q = P.q[zb];
+    const float* __restrict__ Kc = P.Kc[zb];
+    const float* __restrict__ Vc = P.Vc[zb];
+    const int* __restrict__ state = P.state[zb];
+    float* __restrict__ part = P.part[zb];
+    float* __restrict__ out = P.out[zb];
     constexpr int DQ = HD / 4;   // dims per lane for Q.K
     constexpr int DPL = HD / 64; // dims per lane for P.V
     __shared__ __attribute__((aligned(16))) float sQ[HPB][HD];
@@ -1182,9 +1186,10 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const float* __restrict__ 
 }
 
 template <int HD>
-__global__ __launch_bounds__(256) void k_attn_combine(const float* __restrict__ part, int maxs,
-                                                      const int* __restrict__ state, int pos_host,
-                                                      int window, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int maxs, int pos_host, int window) {
+    const float* __restrict__ part = ptrs.part[blockIdx.y];
+    const int* __restrict__ state = ptrs.state[blockIdx.y];
+    float* __restrict__ out = ptrs.out[blockIdx.y];
     __shared__ float sf[64];
     __shared__ float sden;
     const int h = blockIdx.x, tid = threadIdx.x;
@@ -1396,6 +1401,109 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
         for (int i = threadIdx.x; i < D; i += 256) x[i] = a[i] + emb_at(emb, esc, stok, D, i);
     }
     if (alts && sstep < tokens_cap) alt_merge(part_alt, n, stok, sv[0], sstep, alts);
+}
+
+// ============================================================================
+// Batched decode step (C4): row i of the batch belongs to stream i.
+// ============================================================================
+// RoPE + KV append per row at that stream's own logical position (decoder.c:709-722)
+__global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__ qkv, int qd, int kvd, int hd,
+                                                       const float* __restrict__ rope, const StepPtrs sp, int cap,
+                                                       float* __restrict__ q) {
+    const int i = blockIdx.x;
+    const int ld = qd + 2 * kvd;
+    const float* row = qkv + (size_t)i * ld;
+    const int pos = sp.state[i][0];
+    const float* rp = rope + (size_t)pos * hd;
+    const int slot = pos % cap;
+    float* kr = sp.Kc[i] + (size_t)slot * kvd;
+    float* vr = sp.Vc[i] + (size_t)slot * kvd;
+    for (int p = threadIdx.x; p < qd / 2; p += 256) {
+        const int d = (2 * p) % hd / 2;
+        const float c = rp[2 * d], sn = rp[2 * d + 1];
+        const float x0 = row[2 * p], x1 = row[2 * p + 1];
+        q[(size_t)i * qd + 2 * p] = x0 * c - x1 * sn;
+        q[(size_t)i * qd + 2 * p + 1] = x0 * sn + x1 * c;
+    }
+    for (int p = threadIdx.x; p < kvd / 2; p += 256) {
+        const int d = (2 * p) % hd / 2;
+        const float c = rp[2 * d], sn = rp[2 * d + 1];
+        const float x0 = row[qd + 2 * p], x1 = row[qd + 2 * p + 1];
+        kr[2 * p] = x0 * c - x1 * sn;
+        kr[2 * p + 1] = x0 * sn + x1 * c;
+    }
+    for (int p = threadIdx.x; p < kvd; p += 256) vr[p] = row[qd + kvd + p];
+}
+
+// argmax over row i's logits, first max wins (voxtral_decoder.c:771-779): ARGB slices
+__global__ __launch_bounds__(256) void k_argmax_rows(const float* __restrict__ logits, int V, float* __restrict__ pval,
+                                                     int* __restrict__ pidx) {
+    __shared__ float sv[256];
+    __shared__ int si[256];
+    const int i = blockIdx.y, b = blockIdx.x;
+    const int per = (V + ARGB - 1) / ARGB;
+    const int lo = b * per, hi = min(V, lo + per);
+    const float* lg = logits + (size_t)i * V;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = lo + threadIdx.x; j < hi; j += 256) {
+        const float v = lg[j];
+        if (v > bv) { bv = v; bi = j; }  // j ascends per thread
+    }
+    sv[threadIdx.x] = bv;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) {
+            const float v = sv[threadIdx.x + h];
+            const int id = si[threadIdx.x + h];
+            if (v > sv[threadIdx.x] || (v == sv[threadIdx.x] && id < si[threadIdx.x])) {
+                sv[threadIdx.x] = v;
+                si[threadIdx.x] = id;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        pval[i * ARGB + b] = sv[0];
+        pidx[i * ARGB + b] = si[0];
+    }
+}
+
+// per row: final argmax, the stream's state / token log, next step's input row
+// x_i = adapter_i[row] + tok_emb[token] (voxtral.c:1106-1113)
+__global__ __launch_bounds__(256) void k_argmax_batch_final(const float* __restrict__ pval, const int* __restrict__ pidx,
+                                                            const StepPtrs sp, int tokens_cap,
+                                                            const void* __restrict__ emb, const float* __restrict__ esc,
+                                                            int D, float* __restrict__ x) {
+    __shared__ int stok, srow;
+    const int i = blockIdx.x;
+    if (threadIdx.x < 64) {
+        float bv = pval[i * ARGB + threadIdx.x];
+        int bi = pidx[i * ARGB + threadIdx.x];
+        for (int off = 32; off > 0; off >>= 1) {
+            const float v = __shfl_xor(bv, off, 64);
+            const int id = __shfl_xor(bi, off, 64);
+            if (v > bv || (v == bv && id < bi)) { bv = v; bi = id; }
+        }
+        if (threadIdx.x == 0) {
+            int tok = bi == 0x7fffffff ? 0 : bi;
+            int* st = sp.state[i];
+            const int step = st[3];
+            if (step < tokens_cap) sp.tokens[i][step] = tok;
+            st[0] += 1;
+            st[1] += 1;
+            st[2] = tok;
+            st[3] = step + 1;
+            stok = tok;
+            srow = st[1];
+        }
+    }
+    __syncthreads();
+    if (srow < sp.adapter_rows[i]) {
+        const float* a = sp.adapter[i] + (size_t)srow * D;
+        for (int j = threadIdx.x; j < D; j += 256) x[(size_t)i * D + j] = a[j] + emb_at(emb, esc, stok, D, j);
+    }
 }
 
 // im2col for the causal conv stem (voxtral_kernels.c:430-447):
@@ -1659,21 +1767,20 @@ int attn_maxch(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 
 // splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
 // step the launch serves); 1 -> one block per query head, no combine kernel.
-hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
-                              const int* state, int pos_host, int window, float scale, int H,
-                              int KVH, float* part, float* out, int splits, hipStream_t st) {
+static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int pos_host, int window, float scale,
+                              int H, int KVH, int splits, hipStream_t st) {
     const int maxs = attn_maxch(window);
-    if (H % KVH || H / KVH > 4 || maxs > 64 || splits < 1 || splits > maxs) return hipErrorInvalidValue;
-#define VOX_ATT(HD)                                                                                  \
-    if (splits == 1) {                                                                               \
-        hipLaunchKernelGGL((k_attn_decode<HD, 1>), dim3(1, H), dim3(1024), 0, st, q, Kc, Vc, cap,   \
-                           state, pos_host, window, scale, H, KVH, maxs, part, out);                 \
-    } else {                                                                                         \
-        hipLaunchKernelGGL((k_attn_decode<HD, 4>), dim3(splits, KVH), dim3(1024), 0, st, q, Kc, Vc, \
-                           cap, state, pos_host, window, scale, H, KVH, maxs, part, out);            \
-        LAUNCH_CHECK();                                                                              \
-        hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H), dim3(256), 0, st, part, maxs, state,        \
-                           pos_host, window, out);                                                   \
+    if (H % KVH || H / KVH > 4 || maxs > 64 || splits < 1 || splits > maxs || nb < 1 || nb > VOX_MAX_BATCH)
+        return hipErrorInvalidValue;
+#define VOX_ATT(HD)                                                                                        \
+    if (splits == 1) {                                                                                     \
+        hipLaunchKernelGGL((k_attn_decode<HD, 1>), dim3(1, H, nb), dim3(1024), 0, st, p, cap, pos_host,    \
+                           window, scale, H, KVH, maxs);                                                   \
+    } else {                                                                                               \
+        hipLaunchKernelGGL((k_attn_decode<HD, 4>), dim3(splits, KVH, nb), dim3(1024), 0, st, p, cap,       \
+                           pos_host, window, scale, H, KVH, maxs);                                         \
+        LAUNCH_CHECK();                                                                                    \
+        hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H, nb), dim3(256), 0, st, p, maxs, pos_host, window); \
     }
     if (hd == 128) {
         VOX_ATT(128)
@@ -1686,16 +1793,32 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
     LAUNCH_CHECK();
     return hipSuccess;
 }
-#ifdef VOX_GEMV_STAMPS
-hipError_t gemv_set_stamps(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_gemv_stamps), &p, sizeof p); }
-#endif
+
+// splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
+// step the launch serves); 1 -> one block per query head, no combine kernel.
+hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
+                              const int* state, int pos_host, int window, float scale, int H,
+                              int KVH, float* part, float* out, int splits, hipStream_t st) {
+    AttnPtrs p;
+    memset(&p, 0, sizeof p);
+    p.q[0] = q; p.Kc[0] = Kc; p.Vc[0] = Vc; p.state[0] = state; p.part[0] = part; p.out[0] = out;
+    return attn_launch(hd, p, 1, cap, pos_host, window, scale, H, KVH, splits, st);
+}
+
+hipError_t launch_attn_decode_batch(int hd, const AttnPtrs& p, int nb, int cap, int window, float scale,
+                                    int H, int KVH, int splits, hipStream_t st) {
+    return attn_launch(hd, p, nb, cap, 0, window, scale, H, KVH, splits, st);
+}
 // diagnostic variants for tools/kbench (not used by the engine)
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st) {
     dim3 grid(1, 32);
-    if (dbg == 1) hipLaunchKernelGGL((k_attn_decode<128, 1, 1>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
-    if (dbg == 3) hipLaunchKernelGGL((k_attn_decode<128, 1, 3>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
-    if (dbg == 4) hipLaunchKernelGGL((k_attn_decode<128, 1, 4>), grid, dim3(1024), 0, st, q, Kc, Vc, cap, state, 0, 8192, 0.088f, 32, 8, 32, part, out);
+    AttnPtrs p;
+    memset(&p, 0, sizeof p);
+    p.q[0] = q; p.Kc[0] = Kc; p.Vc[0] = Vc; p.state[0] = state; p.part[0] = part; p.out[0] = out;
+    if (dbg == 1) hipLaunchKernelGGL((k_attn_decode<128, 1, 1>), grid, dim3(1024), 0, st, p, cap, 0, 8192, 0.088f, 32, 8, 32);
+    if (dbg == 3) hipLaunchKernelGGL((k_attn_decode<128, 1, 3>), grid, dim3(1024), 0, st, p, cap, 0, 8192, 0.088f, 32, 8, 32);
+    if (dbg == 4) hipLaunchKernelGGL((k_attn_decode<128, 1, 4>), grid, dim3(1024), 0, st, p, cap, 0, 8192, 0.088f, 32, 8, 32);
     return hipGetLastError();
 }
 
@@ -1720,6 +1843,25 @@ hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state
                                const float* part_alt, float* alts, hipStream_t st) {
     hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, pv, pi, n, state, tokens, cap,
                        adapter, adapter_rows, emb, esc, D, x, part_alt, alts);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_rope_kv_batch(const float* qkv, int nb, int qd, int kvd, int hd, const float* rope,
+                                const StepPtrs& sp, int cap, float* q, hipStream_t st) {
+    if (nb < 1 || nb > VOX_MAX_BATCH) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_rope_kv_batch, dim3(nb), dim3(256), 0, st, qkv, qd, kvd, hd, rope, sp, cap, q);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, const StepPtrs& sp,
+                               int tokens_cap, const void* emb, const float* esc, int D, float* x,
+                               hipStream_t st) {
+    if (nb < 1 || nb > VOX_MAX_BATCH) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_argmax_rows, dim3(ARGB, nb), dim3(256), 0, st, logits, V, pval, pidx);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_argmax_batch_final, dim3(nb), dim3(256), 0, st, pval, pidx, sp, tokens_cap, emb, esc, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
 }

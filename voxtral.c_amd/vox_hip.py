@@ -38,6 +38,7 @@ EXPORTS = [
     "vox_hip_model_ada_scale", "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
+    "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode",
     "vox_hip_stream_state", "vox_hip_stream_set_alt", "vox_hip_stream_read_alts", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
@@ -72,6 +73,8 @@ def lib():
         "vox_hip_stream_read_adapter": (I, [P, I, I, fp]),
         "vox_hip_stream_decode": (I, [P, I, I, ip, fp]),
         "vox_hip_stream_state": (I, [P, ip]),
+        "vox_hip_batch_create": (P, [P, I]), "vox_hip_batch_free": (None, [P]),
+        "vox_hip_batch_decode": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, I, I, ip, ip]),
         "vox_hip_stream_set_alt": (I, [P, I, F]),
         "vox_hip_stream_read_alts": (I, [P, I, I, ip, fp]),
         "vox_hip_sgemm_bf16": (None, [I, I, I, fp, P, fp]),
@@ -308,6 +311,33 @@ class DeviceArray:
 # ---------------------------------------------------------------------------
 # reference-boundary twins (voxtral_metal.h), host arrays in / out
 # ---------------------------------------------------------------------------
+class Batch:
+    """Cross-stream batched greedy decoding (C4): one weight read per step for all streams."""
+
+    def __init__(self, model: "Model", max_streams: int):
+        self.h = lib().vox_hip_batch_create(model.h, max_streams)
+        if not self.h:
+            _err("vox_hip_batch_create")
+
+    def decode(self, streams, max_steps: int, stop_at_eos: bool = True):
+        """Returns one int32 token array per stream."""
+        n = len(streams)
+        arr = (ctypes.c_void_p * n)(*[s.h for s in streams])
+        toks = np.zeros((n, max(1, max_steps)), np.int32)
+        cnt = np.zeros(n, np.int32)
+        r = lib().vox_hip_batch_decode(self.h, arr, n, max_steps, int(stop_at_eos),
+                                       toks.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                       cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        if r < 0:
+            _err("vox_hip_batch_decode")
+        return [toks[i, :cnt[i]].copy() for i in range(n)]
+
+    def close(self):
+        if self.h:
+            lib().vox_hip_batch_free(self.h)
+            self.h = None
+
+
 def sgemm_bf16(A: np.ndarray, B_bf16: np.ndarray) -> np.ndarray:
     A = np.ascontiguousarray(A, np.float32)
     M, K = A.shape

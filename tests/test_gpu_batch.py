@@ -79,3 +79,35 @@ def test_batch_mixed_positions_and_continuation(models, tiny_cfg):
         assert out[i] == refs[i], i
         s.close()
     b.close()
+
+
+@pytest.mark.slow
+def test_batch_full_size_matches_single():
+    """Full Voxtral-4B shapes: 3 jfk-shaped streams decoded as one batch give the tokens of
+    decoding each stream alone (and stream 0 those of the CPU oracle)."""
+    import os
+    import vox_hip
+    import vox_oracle
+    from vox_weights import VOXTRAL_4B, synth_weights
+    w = synth_weights(VOXTRAL_4B, seed=0)
+    hm = vox_hip.Model(VOXTRAL_4B, w)
+    mels = _mels(VOXTRAL_4B, [1496, 1496, 1200], 42)
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 4)
+    got = b.decode(ss, max_steps=1000, stop_at_eos=False)
+    for i, mel in enumerate(mels):
+        one = vox_hip.Stream(hm)
+        one.encode_mel(mel)
+        ref = one.decode(stop_at_eos=False).tolist()
+        assert got[i].tolist() == ref, i
+        one.close()
+    om = vox_oracle.OracleModel(VOXTRAL_4B, w)
+    vox_oracle.set_threads(min(16, os.cpu_count() or 1))
+    assert got[0].tolist() == _reference_tokens(om, mels[0])
+    om.close()
+    for s in ss:
+        s.close()
+    b.close()
+    hm.close()

@@ -11,6 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
+namespace vox { extern int g_sk_rt, g_sk_u, g_sk_nw; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -121,9 +122,14 @@ int main(int argc, char** argv) {
         // M>1 GEMMs of the encoder / prefill (useful TFLOP/s = 2 M N K / t)
         float* ws = (float*)dmalloc((size_t)8 << 22, 0);
         float* Am = (float*)dmalloc((size_t)1024 * 9216 * 4, 1);
-        float* Cm = (float*)dmalloc((size_t)1024 * 18432 * 4, 0);
+        float* Cm = (float*)dmalloc((size_t)1024 * 131072 * 4, 0);
         struct G { const char* n; int epi, M, N, K; const uint16_t* W; };
-        for (G g : {G{"enc qkv  677x6144x1280", EPI_STORE, 677, 6144, 1280, wqkv[1]},
+        for (G g : {G{"b8  qkv  8x6144x3072", EPI_STORE, 8, 6144, 3072, wqkv[3]},
+                    G{"b8  wo   8x3072x4096", EPI_RESID, 8, 3072, 4096, wo[3]},
+                    G{"b8  w13  8x18432x3072", EPI_SWIGLU, 8, 18432, 3072, w13[3]},
+                    G{"b8  w2   8x3072x9216", EPI_RESID, 8, 3072, 9216, w2[3]},
+                    G{"b8  lm   8x131072x3072", EPI_STORE, 8, 131072, 3072, emb},
+                    G{"enc qkv  677x6144x1280", EPI_STORE, 677, 6144, 1280, wqkv[1]},
                     G{"enc w13  677x10240x1280", EPI_SWIGLU, 677, 10240, 1280, w13[1]},
                     G{"enc wo   677x1280x2048", EPI_RESID, 677, 1280, 2048, wo[1]},
                     G{"enc w2   677x1280x5120", EPI_RESID, 677, 1280, 5120, w2[1]},
@@ -135,6 +141,26 @@ int main(int argc, char** argv) {
             snprintf(nm, sizeof nm, "gemm %s", g.n);
             printf("%-34s %9.2f us  %8.1f TFLOP/s (useful)\n", nm, us, 2.0 * g.M * g.N * g.K / us / 1e6);
         }
+    }
+    {
+        // skinny MFMA GEMM (batched decode rows): 8 streams
+        uint16_t* xp = (uint16_t*)dmalloc((size_t)3 * 16 * 9216 * 2, 1);
+        uint16_t* op = (uint16_t*)dmalloc((size_t)3 * 16 * 9216 * 2, 0);
+        float* Cs = (float*)dmalloc((size_t)16 * 131072 * 4, 0);
+        for (int cfg = 0; cfg < 7; cfg++) {
+        const int RTs[7] = {2, 2, 4, 4, 8, 4, 4}, Us[7] = {4, 8, 2, 4, 2, 4, 4}, NWs[7] = {0, 0, 0, 0, 0, 4, 8};
+        g_sk_rt = RTs[cfg]; g_sk_u = Us[cfg]; g_sk_nw = NWs[cfg];
+        printf("-- skinny RT %d U %d NW %d\n", g_sk_rt, g_sk_u, g_sk_nw);
+        struct S { const char* n; int epi, N, K; uint16_t* const* W; double bytes; };
+        for (S g : {S{"sk qkv  6144x3072 nb8", EPI_STORE, DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
+                    S{"sk wo   3072x4096 nb8", EPI_RESID, D, DQ, wo.data(), (double)D * DQ * 2},
+                    S{"sk w13  18432x3072 nb8", EPI_SWIGLU, 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
+                    S{"sk w2   3072x9216 nb8", EPI_RESID, D, DH, w2.data(), (double)D * DH * 2}}) {
+            add(g.n, timeit([&] { CK(launch_gemm_sk(g.epi, xp, g.K, g.W[layer++ % NL], nullptr, g.N, 8, nullptr, Cs, g.N, op, st)); }, iters, st), g.bytes);
+        }
+        add("sk lm   131072x3072 nb8", timeit([&] { CK(launch_gemm_sk(EPI_STORE, xp, D, emb, nullptr, V, 8, nullptr, Cs, V, op, st)); }, iters / 10 + 1, st), (double)V * D * 2);
+        }
+        g_sk_rt = 0; g_sk_u = 0; g_sk_nw = 0;
     }
     for (int L : {64, 187, 256, 1000, 4096, 8192}) {
         int st4[4] = {L - 1, 0, 0, 0};

@@ -1304,6 +1304,7 @@ struct vox_hip_batch {
     int* pidx;
     float* gws;
     size_t gws_n;
+    uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows
 };
 
 extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
@@ -1311,6 +1312,7 @@ extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     if (b->st) hipStreamSynchronize(b->st);
     dfree(b->x); dfree(b->xn); dfree(b->qkv); dfree(b->q); dfree(b->att); dfree(b->gated);
     dfree(b->logits); dfree(b->pval); dfree(b->pidx); dfree(b->gws);
+    dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h);
     if (b->st) hipStreamDestroy(b->st);
     delete b;
 }
@@ -1340,6 +1342,9 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     TRYH(dalloc(&b->pidx, B * ARGB));
     b->gws_n = GEMM_WS_ELEMS;
     TRYH(dalloc(&b->gws, b->gws_n));
+    TRYH(dalloc(&b->xp_d, (size_t)3 * SK_ROWS * D));
+    TRYH(dalloc(&b->xp_q, (size_t)3 * SK_ROWS * c.dec_heads * c.dec_head_dim));
+    TRYH(dalloc(&b->xp_h, (size_t)3 * SK_ROWS * c.dec_hidden));
 #undef TRYH
     return b;
 }
@@ -1375,21 +1380,22 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
             ap.Kc[i] = sp.Kc[i];
             ap.Vc[i] = sp.Vc[i];
         }
-        CK(launch_rmsnorm_rows(b->x, DD, b->xn, DD, L.attn_norm, nullptr, nb, DD, c.dec_eps, st));
-        CK(launch_gemm(EPI_STORE, 3, b->xn, DD, L.wqkv, L.sqkv, DD, nb, DQ + 2 * DKV, nullptr, b->qkv, DQ + 2 * DKV,
-                       st, b->gws, b->gws_n));
+        // skinny MFMA GEMMs: the streams are the 16-column B operand, weights read once
+        CK(launch_rmsnorm_planes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, st));
+        CK(launch_gemm_sk(EPI_STORE, b->xp_d, DD, L.wqkv, L.sqkv, DQ + 2 * DKV, nb, nullptr, b->qkv, DQ + 2 * DKV,
+                          nullptr, st));
         CK(launch_rope_kv_batch(b->qkv, nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
         CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st));
+        // the two N = 3072 residual projections measure faster on the tiled GEMM path at 8 rows
         CK(launch_gemm(EPI_RESID, 3, b->att, DQ, L.wo, L.so, DQ, nb, DD, nullptr, b->x, DD, st, b->gws, b->gws_n));
-        CK(launch_rmsnorm_rows(b->x, DD, b->xn, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, nb, DD, c.dec_eps, st));
-        CK(launch_gemm(EPI_SWIGLU, 3, b->xn, DD, L.w13, L.s13, DD, nb, 2 * DH, nullptr, b->gated, DH, st, b->gws,
-                       b->gws_n));
+        CK(launch_rmsnorm_planes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d, st));
+        CK(launch_gemm_sk(EPI_SWIGLU, b->xp_d, DD, L.w13, L.s13, 2 * DH, nb, nullptr, b->gated, DH, b->xp_h, st));
         CK(launch_gemm(EPI_RESID, 3, b->gated, DH, L.w2, L.s2, DH, nb, DD, nullptr, b->x, DD, st, b->gws, b->gws_n));
     }
     // final norm + LM head (tied embeddings) + per-stream argmax, next inputs (decoder.c:762-779)
-    CK(launch_rmsnorm_rows(b->x, DD, b->xn, DD, m->dec_norm, nullptr, nb, DD, c.dec_eps, st));
-    CK(launch_gemm(EPI_STORE, 3, b->xn, DD, m->tok_emb, m->tok_emb_s, DD, nb, c.vocab, nullptr, b->logits, c.vocab, st,
-                   b->gws, b->gws_n));
+    CK(launch_rmsnorm_planes(b->x, nb, DD, m->dec_norm, nullptr, c.dec_eps, b->xp_d, st));
+    CK(launch_gemm_sk(EPI_STORE, b->xp_d, DD, m->tok_emb, m->tok_emb_s, c.vocab, nb, nullptr, b->logits, c.vocab,
+                      nullptr, st));
     CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, sp, ss[0]->tokens_cap, m->tok_emb, m->tok_emb_s,
                            DD, b->x, st));
     return 0;

@@ -106,6 +106,14 @@ hipError_t launch_rope_kv_batch(const float* qkv, int nb, int qd, int kvd, int h
 hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, const StepPtrs& sp,
                                int tokens_cap, const void* emb, const float* esc, int D, float* x,
                                hipStream_t st);
+// skinny GEMM for M <= 16 rows held as three bf16 planes xs[3][16][K] (hi/mid/lo = the
+// exact f32 rows): C[j][n] (op)= sum_k x_j[k] W[n][k], j < nb
+constexpr int SK_ROWS = 16;
+hipError_t launch_rmsnorm_planes(const float* x, int nb, int D, const float* w, const float* ada, float eps,
+                                 uint16_t* xs, hipStream_t st);
+hipError_t launch_split_planes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st);
+hipError_t launch_gemm_sk(int epi, const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                          const float* bias, float* C, int ldc, uint16_t* out_planes, hipStream_t st);
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

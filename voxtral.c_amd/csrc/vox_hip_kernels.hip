@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
+#include <algorithm>
 #include <string.h>
 
 namespace vox {
@@ -1506,6 +1507,183 @@ __global__ __launch_bounds__(256) void k_argmax_batch_final(const float* __restr
     }
 }
 
+// ============================================================================
+// Skinny MFMA GEMM (M <= 16 rows: the streams of a batched decode step).
+// The weight rows are the MFMA A operand (16 rows x 32 k per fragment, 16 B per lane read
+// straight from HBM, non-temporal), the rows of x the B operand (32 k x 16 columns) read
+// from three bf16 planes hi/mid/lo (hi + mid + lo = the f32 row exactly), so every
+// product is exact.  A block takes groups of 32 weight rows (2 MFMA tiles; for SwiGLU the
+// W1 and W3 tiles of 16 hidden units) and splits K across its NW waves; the wave partials
+// meet in LDS and the block's threads finish the 32 x 16 outputs.
+// ============================================================================
+__device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const uint32_t b0 = f2bf(v);
+    const float r1 = v - __uint_as_float(b0 << 16);
+    const uint32_t b1 = f2bf(r1);
+    const float r2 = r1 - __uint_as_float(b1 << 16);
+    h = (uint16_t)b0;
+    m = (uint16_t)b1;
+    l = (uint16_t)f2bf(r2);
+}
+
+// RMSNorm (+ ada) of nb rows (voxtral_kernels.c:475-492, decoder.c:742-745) into planes
+__global__ __launch_bounds__(256) void k_rmsnorm_planes(const float* __restrict__ x, int D,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ ada, float eps,
+                                                        uint16_t* __restrict__ xs) {
+    __shared__ float red[4];
+    const int j = blockIdx.x;
+    const float* xr = x + (size_t)j * D;
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < D; i += 256) ss = fmaf(xr[i], xr[i], ss);
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const float inv = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)D + eps);
+    const size_t P = (size_t)SK_ROWS * D;
+    for (int i = threadIdx.x; i < D; i += 256) {
+        float v = xr[i] * inv * w[i];
+        if (ada) v *= (1.0f + ada[i]);
+        uint16_t h, m, l;
+        split3(v, h, m, l);
+        xs[(size_t)j * D + i] = h;
+        xs[P + (size_t)j * D + i] = m;
+        xs[2 * P + (size_t)j * D + i] = l;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_split_planes(const float* __restrict__ x, int K, uint16_t* __restrict__ xs) {
+    const int j = blockIdx.y;
+    const size_t P = (size_t)SK_ROWS * K;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < K; i += gridDim.x * 256) {
+        uint16_t h, m, l;
+        split3(x[(size_t)j * K + i], h, m, l);
+        xs[(size_t)j * K + i] = h;
+        xs[P + (size_t)j * K + i] = m;
+        xs[2 * P + (size_t)j * K + i] = l;
+    }
+}
+
+// W fragment of row r, k32 step at k (16 B of bf16, or 8 int8 converted exactly).  In the
+// MFMA layout one wave-instruction reads half of each of 16 rows' 128-B lines; plain loads
+// keep the line in L2 for the other half (non-temporal ones fetched it twice: 1.6-1.9x the
+// weight bytes from HBM by FETCH_SIZE).
+template <int WQ8>
+__device__ __forceinline__ bf16x8 sk_wfrag(const void* __restrict__ W, size_t r, int K, int k) {
+    if (WQ8) {
+        const uint2 q = *reinterpret_cast<const uint2*>(static_cast<const int8_t*>(W) + r * K + k);
+        uint32_t h[8];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            h[b] = __float_as_uint(i8f(q.x, b)) >> 16;
+            h[4 + b] = __float_as_uint(i8f(q.y, b)) >> 16;
+        }
+        return __builtin_bit_cast(bf16x8, make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16)));
+    }
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(W) + r * K + k));
+}
+
+// RT row tiles of 16 per group (RT even: SwiGLU pairs tiles 2i (W1) and 2i+1 (W3)),
+// U k32 steps per load round, NW waves splitting K
+template <int EPI, int WQ8, int NW, int RT, int U>
+__global__ __launch_bounds__(NW * 64) void k_gemm_sk(const uint16_t* __restrict__ xs, int K,
+                                                     const void* __restrict__ W, const float* __restrict__ wscale,
+                                                     int N, int nb, const float* __restrict__ bias,
+                                                     float* __restrict__ C, int ldc, uint16_t* __restrict__ op) {
+    __shared__ float red[NW][RT][4][64];  // [wave][tile][r][lane]: the lane's D registers
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ks = K / 32;
+    const int s0 = (int)((long long)ks * wave / NW), s1 = (int)((long long)ks * (wave + 1) / NW);
+    const int fr = lane & 15, fk = (lane >> 4) * 8;
+    const size_t P = (size_t)SK_ROWS * K;
+    const uint16_t* xp = xs + (size_t)fr * K + fk;
+    constexpr int GR = 16 * RT;  // rows per group
+    const int ngroups = N / GR;
+    for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+        f32x4 acc[RT];
+#pragma unroll
+        for (int t = 0; t < RT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const size_t rbase = (size_t)g * GR + fr;
+        int s = s0;
+        for (; s + U <= s1; s += U) {
+            bf16x8 wf[U][RT], xf[U][3];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int k = (s + u) * 32 + fk;
+#pragma unroll
+                for (int t = 0; t < RT; t++) wf[u][t] = sk_wfrag<WQ8>(W, rbase + 16 * t, K, k);
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    xf[u][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xp + p * P + (s + u) * 32));
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+#pragma unroll
+                    for (int t = 0; t < RT; t++)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[u][t], xf[u][p], acc[t], 0, 0, 0);
+        }
+        for (; s < s1; s++) {  // steps left over when K / 32 is not a multiple of U NW
+            const int k = s * 32 + fk;
+#pragma unroll
+            for (int p = 0; p < 3; p++) {
+                const bf16x8 bx = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xp + p * P + s * 32));
+#pragma unroll
+                for (int t = 0; t < RT; t++)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sk_wfrag<WQ8>(W, rbase + 16 * t, K, k), bx, acc[t], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < RT; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) red[wave][t][r][lane] = acc[t][r];
+        __syncthreads();
+        // outputs: row rr of the group, column j (stream); D layout inside a 16-row tile:
+        // col = lane&15, row = (lane>>4)*4 + r
+        for (int o = tid; o < GR * 16; o += NW * 64) {
+            const int rr = o >> 4, j = o & 15;
+            if (j >= nb) continue;
+            const int t = rr >> 4, rt = rr & 15;
+            const int ln = ((rt >> 2) << 4) + j, r = rt & 3;
+            const int row = g * GR + rr;
+            if (EPI == EPI_SWIGLU) {
+                if (t & 1) continue;  // W3 tiles are read by their W1 partner
+                float v = 0.f, u = 0.f;
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    v += red[w][t][r][ln];
+                    u += red[w][t + 1][r][ln];
+                }
+                if (WQ8) {
+                    v *= wscale[row];
+                    u *= wscale[row + 16];
+                }
+                const float gv = silu(v) * u;
+                const int unit = (row >> 5) * 16 + rt;  // 16-row interleave: rows 32q..32q+15 = W1
+                const int H = N / 2;
+                uint16_t h, m, l;
+                split3(gv, h, m, l);
+                const size_t PH = (size_t)SK_ROWS * H;
+                op[(size_t)j * H + unit] = h;
+                op[PH + (size_t)j * H + unit] = m;
+                op[2 * PH + (size_t)j * H + unit] = l;
+                if (C) C[(size_t)j * ldc + unit] = gv;
+            } else {
+                float v = 0.f;
+#pragma unroll
+                for (int w = 0; w < NW; w++) v += red[w][t][r][ln];
+                if (WQ8) v *= wscale[row];
+                if (bias) v += bias[row];
+                float* cp = C + (size_t)j * ldc + row;
+                if (EPI == EPI_RESID) *cp += v;
+                else *cp = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // im2col for the causal conv stem (voxtral_kernels.c:430-447):
 // A[t][ic*3 + k] = src[(stride*t + off + k) * C + ic]
 __global__ __launch_bounds__(256) void k_im2col3(const float* __restrict__ src, int C, int T,
@@ -1864,6 +2042,74 @@ hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, 
     hipLaunchKernelGGL(k_argmax_batch_final, dim3(nb), dim3(256), 0, st, pval, pidx, sp, tokens_cap, emb, esc, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
+}
+
+hipError_t launch_rmsnorm_planes(const float* x, int nb, int D, const float* w, const float* ada, float eps,
+                                 uint16_t* xs, hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_rmsnorm_planes, dim3(nb), dim3(256), 0, st, x, D, w, ada, eps, xs);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_split_planes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_split_planes, dim3((K + 1023) / 1024, nb), dim3(256), 0, st, x, K, xs);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// tuning knobs (kbench; 0 = automatic): row tiles per group, k32 steps per load round,
+// waves per block
+int g_sk_rt = 0, g_sk_u = 0, g_sk_nw = 0;
+
+template <int E, int Q, int NW, int RT, int U>
+static hipError_t sk_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                            const float* bias, float* C, int ldc, uint16_t* op, hipStream_t st) {
+    const int groups = N / (16 * RT);
+    const int grid = std::min(groups, 2048);
+    hipLaunchKernelGGL((k_gemm_sk<E, Q, NW, RT, U>), dim3(grid), dim3(NW * 64), 0, st, xs, K, W, wscale, N, nb, bias, C,
+                       ldc, op);
+    return hipGetLastError();
+}
+
+template <int E, int Q, int RT, int U>
+static hipError_t sk_nw(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                        const float* bias, float* C, int ldc, uint16_t* op, hipStream_t st) {
+    const int groups = N / (16 * RT);
+    // waves per block: enough waves on the chip when the row groups are few (N = 3072)
+    const int nw = g_sk_nw ? g_sk_nw : (groups >= 512 ? 4 : groups >= 192 ? 8 : 16);
+    if (nw == 4) return sk_launch<E, Q, 4, RT, U>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
+    if (nw == 8) return sk_launch<E, Q, 8, RT, U>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
+    return sk_launch<E, Q, 16, RT, U>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
+}
+
+template <int E, int Q>
+static hipError_t sk_ru(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                        const float* bias, float* C, int ldc, uint16_t* op, hipStream_t st) {
+    // measured at 8 rows (tools/kbench): 8 tiles per group for the wide weights (W1|W3,
+    // LM head: the x fragments are reused 8 times), 2 for the rest
+    int rt = g_sk_rt ? g_sk_rt : (N >= 16384 ? 8 : 2);
+    if (N % (16 * rt)) rt = 2;
+    const int u = g_sk_u ? g_sk_u : (rt == 8 ? 2 : 4);
+#define SK_RU(R, UU) \
+    if (rt == R && u == UU) return sk_nw<E, Q, R, UU>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
+    SK_RU(2, 4) SK_RU(2, 8) SK_RU(4, 2) SK_RU(4, 4) SK_RU(8, 2)
+#undef SK_RU
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_gemm_sk(int epi, const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                          const float* bias, float* C, int ldc, uint16_t* out_planes, hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS || N % 32 || K % 32) return hipErrorInvalidValue;
+    if (epi == EPI_SWIGLU && !out_planes) return hipErrorInvalidValue;
+#define SK_CASE(E)                                                                                     \
+    if (epi == E)                                                                                      \
+        return wscale ? sk_ru<E, 1>(xs, K, W, wscale, N, nb, bias, C, ldc, out_planes, st)             \
+                      : sk_ru<E, 0>(xs, K, W, wscale, N, nb, bias, C, ldc, out_planes, st);
+    SK_CASE(EPI_STORE) SK_CASE(EPI_RESID) SK_CASE(EPI_SWIGLU)
+#undef SK_CASE
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,

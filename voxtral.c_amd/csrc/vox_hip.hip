@@ -57,9 +57,18 @@ static hipError_t dalloc(T** p, size_t n) {
     hipError_t e = hipMalloc((void**)p, n * sizeof(T));
     if (e == hipSuccess) {
         g_mem_used += n * sizeof(T);
-        e = hipMemset(*p, 0, n * sizeof(T));
+        // The streams are non-blocking, so nothing orders a null-stream memset before the
+        // kernels a stream enqueues next: wait for the zeroing before handing the buffer out.
+        e = hipMemsetAsync(*p, 0, n * sizeof(T), nullptr);
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     }
     return e;
+}
+// Host -> device copy that has landed when it returns (a pageable-source hipMemcpy may
+// return once the data is staged, before the DMA that the stream kernels depend on).
+static hipError_t h2d(void* dst, const void* src, size_t bytes) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, nullptr);
+    return e == hipSuccess ? hipStreamSynchronize(nullptr) : e;
 }
 template <class T>
 static void dfree(T*& p) {
@@ -155,7 +164,7 @@ struct vox_hip_model {
 
 static int upload(void* dst, const void* src, size_t bytes) {
     if (!src) return set_err("null weight pointer");
-    CK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    CK(h2d(dst, src, bytes));
     return 0;
 }
 
@@ -256,7 +265,7 @@ static int model_update_ada(vox_hip_model_t* m) {
             sc[i] = sum;
         }
     }
-    CK(hipMemcpy(m->ada_scale, m->ada_host.data(), m->ada_host.size() * 4, hipMemcpyHostToDevice));
+    CK(h2d(m->ada_scale, m->ada_host.data(), m->ada_host.size() * 4));
     return 0;
 }
 
@@ -267,10 +276,10 @@ static int model_rope_tables(vox_hip_model_t* m, int positions) {
     std::vector<float> t((size_t)positions * std::max(c.enc_head_dim, c.dec_head_dim));
     CK(dalloc(&m->rope_enc, (size_t)positions * c.enc_head_dim));
     host_rope(t.data(), 0, positions, c.enc_head_dim, c.rope_theta);
-    CK(hipMemcpy(m->rope_enc, t.data(), (size_t)positions * c.enc_head_dim * 4, hipMemcpyHostToDevice));
+    CK(h2d(m->rope_enc, t.data(), (size_t)positions * c.enc_head_dim * 4));
     CK(dalloc(&m->rope_dec, (size_t)positions * c.dec_head_dim));
     host_rope(t.data(), 0, positions, c.dec_head_dim, c.rope_theta);
-    CK(hipMemcpy(m->rope_dec, t.data(), (size_t)positions * c.dec_head_dim * 4, hipMemcpyHostToDevice));
+    CK(h2d(m->rope_dec, t.data(), (size_t)positions * c.dec_head_dim * 4));
     m->rope_positions = positions;
     m->rope_gen++;
     return 0;
@@ -741,7 +750,8 @@ extern "C" int vox_hip_stream_adapter_tokens(vox_hip_stream_t* s) { return s->to
 extern "C" int vox_hip_stream_read_adapter(vox_hip_stream_t* s, int first, int n, float* out) {
     const int D = s->m->c.dec_dim;
     if (first < 0 || first + n > s->total_adapter) return set_err("adapter rows out of range");
-    CK(hipMemcpy(out, s->adapter + (size_t)first * D, (size_t)n * D * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpyAsync(out, s->adapter + (size_t)first * D, (size_t)n * D * 4, hipMemcpyDeviceToHost, s->st));
+    CK(hipStreamSynchronize(s->st));
     return 0;
 }
 
@@ -1100,7 +1110,7 @@ static uint8_t* twin_weight(const void* host, size_t bytes) {
     if (it != g_wcache.end()) return it->second;
     uint8_t* d = nullptr;
     if (dalloc(&d, bytes) != hipSuccess) { set_err("weight alloc failed"); return nullptr; }
-    if (hipMemcpy(d, host, bytes, hipMemcpyHostToDevice) != hipSuccess) { set_err("weight upload failed"); return nullptr; }
+    if (h2d(d, host, bytes) != hipSuccess) { set_err("weight upload failed"); return nullptr; }
     g_wcache[host] = d;
     return d;
 }
@@ -1280,7 +1290,7 @@ extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_
 extern "C" void* vox_hip_device_upload(const void* host, size_t bytes) {
     void* d = nullptr;
     if (hipMalloc(&d, bytes) != hipSuccess) { set_err("device_upload: hipMalloc(%zu) failed", bytes); return nullptr; }
-    if (hipMemcpy(d, host, bytes, hipMemcpyHostToDevice) != hipSuccess) { hipFree(d); set_err("device_upload: copy failed"); return nullptr; }
+    if (h2d(d, host, bytes) != hipSuccess) { hipFree(d); set_err("device_upload: copy failed"); return nullptr; }
     return d;
 }
 

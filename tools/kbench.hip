@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_sk_rt, g_sk_u, g_sk_nw; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -143,24 +143,39 @@ int main(int argc, char** argv) {
         }
     }
     {
-        // skinny MFMA GEMM (batched decode rows): 8 streams
+        // batched decode GEMMs (16 streams, fragment-major weights and planes); weights are
+        // constant-filled, so the packed layout does not matter for timing
         uint16_t* xp = (uint16_t*)dmalloc((size_t)3 * 16 * 9216 * 2, 1);
-        uint16_t* op = (uint16_t*)dmalloc((size_t)3 * 16 * 9216 * 2, 0);
         float* Cs = (float*)dmalloc((size_t)16 * 131072 * 4, 0);
-        for (int cfg = 0; cfg < 7; cfg++) {
-        const int RTs[7] = {2, 2, 4, 4, 8, 4, 4}, Us[7] = {4, 8, 2, 4, 2, 4, 4}, NWs[7] = {0, 0, 0, 0, 0, 4, 8};
-        g_sk_rt = RTs[cfg]; g_sk_u = Us[cfg]; g_sk_nw = NWs[cfg];
-        printf("-- skinny RT %d U %d NW %d\n", g_sk_rt, g_sk_u, g_sk_nw);
-        struct S { const char* n; int epi, N, K; uint16_t* const* W; double bytes; };
-        for (S g : {S{"sk qkv  6144x3072 nb8", EPI_STORE, DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
-                    S{"sk wo   3072x4096 nb8", EPI_RESID, D, DQ, wo.data(), (double)D * DQ * 2},
-                    S{"sk w13  18432x3072 nb8", EPI_SWIGLU, 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
-                    S{"sk w2   3072x9216 nb8", EPI_RESID, D, DH, w2.data(), (double)D * DH * 2}}) {
-            add(g.n, timeit([&] { CK(launch_gemm_sk(g.epi, xp, g.K, g.W[layer++ % NL], nullptr, g.N, 8, nullptr, Cs, g.N, op, st)); }, iters, st), g.bytes);
+        float* part = (float*)dmalloc((size_t)16 * 18 * 18432 * 4, 0);
+        for (int nw : {0, 4, 8}) {
+            g_skl_nw = nw;
+            printf("-- skl NW %d (0 = auto)\n", nw);
+            struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
+            for (S g : {S{"skl qkv  6144x3072 nb16", DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
+                        S{"skl wo   3072x4096 nb16", D, DQ, wo.data(), (double)D * DQ * 2},
+                        S{"skl w13  18432x3072 nb16", 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
+                        S{"skl w2   3072x9216 nb16", D, DH, w2.data(), (double)D * DH * 2}})
+                add(g.n, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
         }
-        add("sk lm   131072x3072 nb8", timeit([&] { CK(launch_gemm_sk(EPI_STORE, xp, D, emb, nullptr, V, 8, nullptr, Cs, V, op, st)); }, iters / 10 + 1, st), (double)V * D * 2);
+        g_skl_nw = 0;
+        const int Rs[] = {0, 2, 2, 4, 4}, NWs[] = {0, 4, 4, 4, 8}, Ds[] = {0, 2, 3, 2, 2};
+        for (int cfg = 0; cfg < (int)(sizeof Rs / sizeof Rs[0]); cfg++) {
+            g_skf_r = Rs[cfg];
+            g_skf_nw = NWs[cfg];
+            g_skf_d = Ds[cfg];
+            char nm[80];
+            snprintf(nm, sizeof nm, "skf lm R%d NW%d D%d nb16", Rs[cfg], NWs[cfg], Ds[cfg]);
+            add(nm, timeit([&] { CK(launch_gemm_skf(xp, D, emb, nullptr, V, 16, Cs, V, st)); }, iters / 10 + 1, st), (double)V * D * 2);
         }
-        g_sk_rt = 0; g_sk_u = 0; g_sk_nw = 0;
+        g_skf_r = 0;
+        g_skf_nw = 0;
+        g_skf_d = 0;
+        float* xr = (float*)dmalloc((size_t)16 * 9216 * 4, 1);
+        add("rmsnorm fplanes 16x3072", timeit([&] { CK(launch_rmsnorm_fplanes(xr, 16, D, xr, xr, 1e-5f, xp, nullptr, 0, st)); }, iters, st), 16.0 * D * 10);
+        add("resid(18)+rmsnorm fplanes 16x3072", timeit([&] { CK(launch_rmsnorm_fplanes(xr, 16, D, xr, xr, 1e-5f, xp, part, 18, st)); }, iters, st), 16.0 * D * (10 + 4 * 18));
+        add("split fplanes 16x4096", timeit([&] { CK(launch_split_fplanes(xr, 16, DQ, xp, st)); }, iters, st), 16.0 * DQ * 10);
+        add("swiglu(6) fplanes 16x9216", timeit([&] { CK(launch_swiglu_fplanes(part, 6, DH, 16, xp, st)); }, iters, st), 16.0 * DH * (6 * 8 + 6));
     }
     for (int L : {64, 187, 256, 1000, 4096, 8192}) {
         int st4[4] = {L - 1, 0, 0, 0};

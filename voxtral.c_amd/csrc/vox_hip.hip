@@ -144,6 +144,10 @@ struct DecLayerD {
     float *sqkv, *so, *s13, *s2;
     float *attn_norm, *ffn_norm;
 };
+// the same matrices in MFMA fragment order for the batched step (k_skf; built on first use)
+struct DecFragD {
+    uint8_t *wqkv, *wo, *w13, *w2;
+};
 
 struct vox_hip_model {
     vox_hip_config_t c;
@@ -160,6 +164,8 @@ struct vox_hip_model {
     float *rope_enc, *rope_dec;    // device tables [rope_positions][hd]
     int rope_positions;
     int rope_gen;                  // bumped when the tables are reallocated (graphs hold the pointer)
+    std::vector<DecFragD> dfrag;   // fragment-major decoder matrices (empty until a batch exists)
+    uint8_t* lm_frag;              // fragment-major LM head (tied embeddings)
 };
 
 static int upload(void* dst, const void* src, size_t bytes) {
@@ -407,6 +413,10 @@ extern "C" void vox_hip_model_free(vox_hip_model_t* m) {
         dfree(L.sqkv); dfree(L.so); dfree(L.s13); dfree(L.s2);
         dfree(L.attn_norm); dfree(L.ffn_norm);
     }
+    for (auto& F : m->dfrag) {
+        dfree(F.wqkv); dfree(F.wo); dfree(F.w13); dfree(F.w2);
+    }
+    dfree(m->lm_frag);
     dfree(m->enc_norm); dfree(m->ad0); dfree(m->ad1); dfree(m->tok_emb); dfree(m->dec_norm);
     dfree(m->ad0_s); dfree(m->ad1_s); dfree(m->tok_emb_s);
     dfree(m->ada_scale); dfree(m->rope_enc); dfree(m->rope_dec);
@@ -1310,18 +1320,47 @@ struct vox_hip_batch {
     vox_hip_model_t* m;
     int cap;
     hipStream_t st;
-    float *x, *xn, *qkv, *q, *att, *gated, *logits, *pval;
+    float *x, *q, *att, *logits, *pval;
+    float* part;     // split-K slabs of the current projection (k_skl), consumed by the next kernel
     int* pidx;
-    float* gws;
-    size_t gws_n;
-    uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows
+    uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows (fragment order)
 };
+
+// pack one [N, K] matrix (bf16, or int8 when q8) into fragment order (k_frag_pack)
+static int frag_copy(uint8_t** dst, const uint8_t* src, int N, int K, int q8) {
+    CK(dalloc(dst, (size_t)N * K * (q8 ? 1 : 2)));
+    CK(launch_frag_pack(src, N, K, q8, *dst, nullptr));
+    CK(hipStreamSynchronize(nullptr));
+    return 0;
+}
+
+// fragment-major copies of the decoder matrices and the LM head, made once per model
+// (6.86 GB bf16 / 3.83 GB Q8 beside the row-major weights the single-stream GEMVs read)
+static int model_frag(vox_hip_model_t* m) {
+    if (m->lm_frag) return 0;
+    const vox_hip_config_t& c = m->c;
+    const int DD = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
+    const int DH = c.dec_hidden;
+    m->dfrag.assign(c.dec_layers, DecFragD{});
+    for (int l = 0; l < c.dec_layers; l++) {
+        const DecLayerD& L = m->dec[l];
+        DecFragD& F = m->dfrag[l];
+        if (frag_copy(&F.wqkv, L.wqkv, DQ + 2 * DKV, DD, L.sqkv != nullptr)) return -1;
+        if (frag_copy(&F.wo, L.wo, DD, DQ, L.so != nullptr)) return -1;
+        if (frag_copy(&F.w13, L.w13, 2 * DH, DD, L.s13 != nullptr)) return -1;
+        if (frag_copy(&F.w2, L.w2, DD, DH, L.s2 != nullptr)) return -1;
+    }
+    uint8_t* lm = nullptr;
+    if (frag_copy(&lm, m->tok_emb, c.vocab, DD, m->tok_emb_s != nullptr)) { dfree(lm); return -1; }
+    m->lm_frag = lm;
+    return 0;
+}
 
 extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     if (!b) return;
     if (b->st) hipStreamSynchronize(b->st);
-    dfree(b->x); dfree(b->xn); dfree(b->qkv); dfree(b->q); dfree(b->att); dfree(b->gated);
-    dfree(b->logits); dfree(b->pval); dfree(b->pidx); dfree(b->gws);
+    dfree(b->x); dfree(b->part); dfree(b->q); dfree(b->att);
+    dfree(b->logits); dfree(b->pval); dfree(b->pidx);
     dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h);
     if (b->st) hipStreamDestroy(b->st);
     delete b;
@@ -1342,16 +1381,22 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
     TRYH(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
     TRYH(dalloc(&b->x, B * D));
-    TRYH(dalloc(&b->xn, B * D));
-    TRYH(dalloc(&b->qkv, B * QKV));
+    {
+        const size_t DQ = (size_t)c.dec_heads * c.dec_head_dim, DH = c.dec_hidden;
+        const size_t n = std::max(std::max(skl_splits(D) * QKV, skl_splits(DQ) * D),
+                                  std::max(skl_splits(D) * 2 * DH, skl_splits(DH) * D));
+        if (!skl_splits(D) || !skl_splits(DQ) || !skl_splits(DH)) {
+            set_err("batched decode needs dec_dim, heads*head_dim and dec_hidden divisible by 256");
+            return fail();
+        }
+        TRYH(dalloc(&b->part, (size_t)SK_ROWS * n));
+    }
     TRYH(dalloc(&b->q, B * c.dec_heads * c.dec_head_dim));
     TRYH(dalloc(&b->att, B * c.dec_heads * c.dec_head_dim));
-    TRYH(dalloc(&b->gated, B * c.dec_hidden));
     TRYH(dalloc(&b->logits, B * c.vocab));
     TRYH(dalloc(&b->pval, B * ARGB));
     TRYH(dalloc(&b->pidx, B * ARGB));
-    b->gws_n = GEMM_WS_ELEMS;
-    TRYH(dalloc(&b->gws, b->gws_n));
+    if (model_frag(m)) return fail();
     TRYH(dalloc(&b->xp_d, (size_t)3 * SK_ROWS * D));
     TRYH(dalloc(&b->xp_q, (size_t)3 * SK_ROWS * c.dec_heads * c.dec_head_dim));
     TRYH(dalloc(&b->xp_h, (size_t)3 * SK_ROWS * c.dec_hidden));
@@ -1382,6 +1427,7 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         ap.out[i] = b->att + (size_t)i * DQ;
     }
     const int cap = ss[0]->dcap;
+    const int Sres = skl_splits(DH);  // slabs the previous layer's w2 left for the residual
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         for (int i = 0; i < nb; i++) {
@@ -1390,22 +1436,26 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
             ap.Kc[i] = sp.Kc[i];
             ap.Vc[i] = sp.Vc[i];
         }
-        // skinny MFMA GEMMs: the streams are the 16-column B operand, weights read once
-        CK(launch_rmsnorm_planes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, st));
-        CK(launch_gemm_sk(EPI_STORE, b->xp_d, DD, L.wqkv, L.sqkv, DQ + 2 * DKV, nb, nullptr, b->qkv, DQ + 2 * DKV,
-                          nullptr, st));
-        CK(launch_rope_kv_batch(b->qkv, nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
+        const DecFragD& F = m->dfrag[l];
+        // skinny MFMA GEMMs over fragment-major weights: the streams are the 16-column B
+        // operand, every weight byte read once per step; each projection leaves split-K slabs
+        // in b->part that the next kernel sums (with the residual for wo / w2)
+        CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, b->part, l ? Sres : 0, st));
+        CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
+        CK(launch_rope_kv_batch(b->part, skl_splits(DD), nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
         CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st));
-        // the two N = 3072 residual projections measure faster on the tiled GEMM path at 8 rows
-        CK(launch_gemm(EPI_RESID, 3, b->att, DQ, L.wo, L.so, DQ, nb, DD, nullptr, b->x, DD, st, b->gws, b->gws_n));
-        CK(launch_rmsnorm_planes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d, st));
-        CK(launch_gemm_sk(EPI_SWIGLU, b->xp_d, DD, L.w13, L.s13, 2 * DH, nb, nullptr, b->gated, DH, b->xp_h, st));
-        CK(launch_gemm(EPI_RESID, 3, b->gated, DH, L.w2, L.s2, DH, nb, DD, nullptr, b->x, DD, st, b->gws, b->gws_n));
+        CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
+        CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
+        CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d, b->part,
+                                  skl_splits(DQ), st));
+        CK(launch_gemm_skl(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st));
+        CK(launch_swiglu_fplanes(b->part, skl_splits(DD), DH, nb, b->xp_h, st));
+        CK(launch_gemm_skl(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
     }
-    // final norm + LM head (tied embeddings) + per-stream argmax, next inputs (decoder.c:762-779)
-    CK(launch_rmsnorm_planes(b->x, nb, DD, m->dec_norm, nullptr, c.dec_eps, b->xp_d, st));
-    CK(launch_gemm_sk(EPI_STORE, b->xp_d, DD, m->tok_emb, m->tok_emb_s, c.vocab, nb, nullptr, b->logits, c.vocab,
-                      nullptr, st));
+    // final norm (after the last w2 residual) + LM head (tied embeddings) + per-stream argmax,
+    // next inputs (decoder.c:762-779)
+    CK(launch_rmsnorm_fplanes(b->x, nb, DD, m->dec_norm, nullptr, c.dec_eps, b->xp_d, b->part, Sres, st));
+    CK(launch_gemm_skf(b->xp_d, DD, m->lm_frag, m->tok_emb_s, c.vocab, nb, b->logits, c.vocab, st));
     CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, sp, ss[0]->tokens_cap, m->tok_emb, m->tok_emb_s,
                            DD, b->x, st));
     return 0;

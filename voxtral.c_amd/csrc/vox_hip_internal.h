@@ -101,19 +101,29 @@ hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state
                                int cap, const float* adapter, int adapter_rows,
                                const void* emb, const float* esc, int D, float* x,
                                const float* part_alt, float* alts, hipStream_t st);
-hipError_t launch_rope_kv_batch(const float* qkv, int nb, int qd, int kvd, int hd, const float* rope,
+// rows (i, n) = sum of the S split slabs part[s][16][qd + 2 kvd] (S = 1: a plain row block)
+hipError_t launch_rope_kv_batch(const float* part, int S, int nb, int qd, int kvd, int hd, const float* rope,
                                 const StepPtrs& sp, int cap, float* q, hipStream_t st);
 hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, const StepPtrs& sp,
                                int tokens_cap, const void* emb, const float* esc, int D, float* x,
                                hipStream_t st);
-// skinny GEMM for M <= 16 rows held as three bf16 planes xs[3][16][K] (hi/mid/lo = the
-// exact f32 rows): C[j][n] (op)= sum_k x_j[k] W[n][k], j < nb
+// Batched decode GEMMs for M <= 16 rows held as three bf16 planes xs[3][16][K] (hi/mid/lo =
+// the exact f32 rows) in MFMA fragment order; weights packed by launch_frag_pack.
 constexpr int SK_ROWS = 16;
-hipError_t launch_rmsnorm_planes(const float* x, int nb, int D, const float* w, const float* ada, float eps,
-                                 uint16_t* xs, hipStream_t st);
-hipError_t launch_split_planes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st);
-hipError_t launch_gemm_sk(int epi, const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
-                          const float* bias, float* C, int ldc, uint16_t* out_planes, hipStream_t st);
+hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hipStream_t st);
+// RMSNorm (+ ada) of nb rows into planes; S > 0: x += the S split slabs of part first
+hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
+                                  uint16_t* xs, const float* part, int S, hipStream_t st);
+hipError_t launch_split_fplanes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st);
+// silu(W1 x) * (W3 x) from the split W1|W3 slabs (N = 2H rows) into planes
+hipError_t launch_swiglu_fplanes(const float* part, int S, int H, int nb, uint16_t* xs, hipStream_t st);
+// C[j][n] = sum_k x_j[k] W[n][k] (LM head: k_skf)
+hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* C,
+                           int ldc, hipStream_t st);
+// split-K slabs part[s][16][N], s < skl_splits(K) (projections: k_skl)
+int skl_splits(int K);
+hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
+                           float* part, hipStream_t st);
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

@@ -1408,32 +1408,41 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
 // Batched decode step (C4): row i of the batch belongs to stream i.
 // ============================================================================
 // RoPE + KV append per row at that stream's own logical position (decoder.c:709-722)
-__global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__ qkv, int qd, int kvd, int hd,
-                                                       const float* __restrict__ rope, const StepPtrs sp, int cap,
-                                                       float* __restrict__ q) {
+// element (stream j, column n) of a split-K result: the S partial slabs summed in order
+__device__ __forceinline__ float psum(const float* __restrict__ part, int S, int N, int j, int n) {
+    float v = part[(size_t)j * N + n];
+    for (int s = 1; s < S; s++) v += part[((size_t)s * SK_ROWS + j) * N + n];
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__ part, int S, int qd, int kvd,
+                                                       int hd, const float* __restrict__ rope, const StepPtrs sp,
+                                                       int cap, float* __restrict__ q) {
+    // stream i = blockIdx.x; the row's value (i, n) is the sum of the S split slabs of the
+    // QKV projection (k_skl; S = 1: a plain [16][ld] row block)
     const int i = blockIdx.x;
     const int ld = qd + 2 * kvd;
-    const float* row = qkv + (size_t)i * ld;
     const int pos = sp.state[i][0];
     const float* rp = rope + (size_t)pos * hd;
     const int slot = pos % cap;
     float* kr = sp.Kc[i] + (size_t)slot * kvd;
     float* vr = sp.Vc[i] + (size_t)slot * kvd;
-    for (int p = threadIdx.x; p < qd / 2; p += 256) {
+    const int t0 = blockIdx.y * 256 + threadIdx.x, tn = gridDim.y * 256;
+    for (int p = t0; p < qd / 2; p += tn) {
         const int d = (2 * p) % hd / 2;
         const float c = rp[2 * d], sn = rp[2 * d + 1];
-        const float x0 = row[2 * p], x1 = row[2 * p + 1];
+        const float x0 = psum(part, S, ld, i, 2 * p), x1 = psum(part, S, ld, i, 2 * p + 1);
         q[(size_t)i * qd + 2 * p] = x0 * c - x1 * sn;
         q[(size_t)i * qd + 2 * p + 1] = x0 * sn + x1 * c;
     }
-    for (int p = threadIdx.x; p < kvd / 2; p += 256) {
+    for (int p = t0; p < kvd / 2; p += tn) {
         const int d = (2 * p) % hd / 2;
         const float c = rp[2 * d], sn = rp[2 * d + 1];
-        const float x0 = row[qd + 2 * p], x1 = row[qd + 2 * p + 1];
+        const float x0 = psum(part, S, ld, i, qd + 2 * p), x1 = psum(part, S, ld, i, qd + 2 * p + 1);
         kr[2 * p] = x0 * c - x1 * sn;
         kr[2 * p + 1] = x0 * sn + x1 * c;
     }
-    for (int p = threadIdx.x; p < kvd; p += 256) vr[p] = row[qd + kvd + p];
+    for (int p = t0; p < kvd; p += tn) vr[p] = psum(part, S, ld, i, qd + kvd + p);
 }
 
 // argmax over row i's logits, first max wins (voxtral_decoder.c:771-779): ARGB slices
@@ -1508,13 +1517,9 @@ __global__ __launch_bounds__(256) void k_argmax_batch_final(const float* __restr
 }
 
 // ============================================================================
-// Skinny MFMA GEMM (M <= 16 rows: the streams of a batched decode step).
-// The weight rows are the MFMA A operand (16 rows x 32 k per fragment, 16 B per lane read
-// straight from HBM, non-temporal), the rows of x the B operand (32 k x 16 columns) read
-// from three bf16 planes hi/mid/lo (hi + mid + lo = the f32 row exactly), so every
-// product is exact.  A block takes groups of 32 weight rows (2 MFMA tiles; for SwiGLU the
-// W1 and W3 tiles of 16 hidden units) and splits K across its NW waves; the wave partials
-// meet in LDS and the block's threads finish the 32 x 16 outputs.
+// Batched decode (M <= 16 rows: the streams of a batched step).  Each f32 row is held as
+// three bf16 planes hi/mid/lo (hi + mid + lo = the row exactly) so that MFMA products with
+// bf16 / int8 weights are exact.
 // ============================================================================
 __device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
     const uint32_t b0 = f2bf(v);
@@ -1526,162 +1531,328 @@ __device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16
     l = (uint16_t)f2bf(r2);
 }
 
-// RMSNorm (+ ada) of nb rows (voxtral_kernels.c:475-492, decoder.c:742-745) into planes
-__global__ __launch_bounds__(256) void k_rmsnorm_planes(const float* __restrict__ x, int D,
+// ============================================================================
+// Fragment-major skinny GEMM (batched decode, M <= 16 rows).  The batched path keeps its own
+// copy of every decoder matrix and the LM head in MFMA fragment order, so that each 1 KiB a
+// wave loads is one A operand: for 16-row group g and 64-k block b,
+//   bf16: two 1-KiB halves t = 0, 1; lane l's 16 B = W[16g + (l&15)][64b + 16(l>>4) + 8t .. +7]
+//   int8: one 1-KiB block;           lane l's 16 B = W[16g + (l&15)][64b + 16(l>>4) .. +15]
+//         (its first 8 bytes feed half 0, the last 8 half 1, converted to bf16 exactly).
+// The k order inside a block is permuted the same way for the x planes (B operand), so the
+// sum over k is unchanged:
+//   plane p, chunk (b, t) of 1 KiB: lane l's 16 B = x_p[row l&15][64b + 16(l>>4) + 8t .. +7].
+// Weight and plane loads are then contiguous 1 KiB per wave-instruction (the row-major
+// fragment loads touched 16 rows x 64 B each and cost twice the address-unit time).
+// ============================================================================
+__device__ __forceinline__ size_t frag_off(int j, int k) {  // element (row j, col k) in a plane
+    const int b = k >> 6, r = k & 63;
+    return ((size_t)(b * 2 + ((r >> 3) & 1)) * 64 + (r >> 4) * 16 + j) * 8 + (r & 7);
+}
+
+// one thread per 16 B of the packed copy
+template <int WQ8>
+__global__ __launch_bounds__(256) void k_frag_pack(const uint8_t* __restrict__ src, int K, size_t n16,
+                                                   uint8_t* __restrict__ dst) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n16) return;
+    const int lane = (int)(i & 63);
+    const size_t chunk = i >> 6;
+    const int KB = K >> 6;
+    const int t = WQ8 ? 0 : (int)(chunk & 1);
+    const size_t gb = WQ8 ? chunk : chunk >> 1;
+    const size_t g = gb / KB;
+    const int b = (int)(gb % KB);
+    const size_t row = g * 16 + (lane & 15);
+    const int col = b * 64 + (lane >> 4) * 16 + t * 8;
+    const size_t esz = WQ8 ? 1 : 2;
+    *reinterpret_cast<uint4*>(dst + i * 16) = *reinterpret_cast<const uint4*>(src + (row * K + col) * esz);
+}
+
+// residual of a split projection: x[j][n] += sum of its S slabs (k_skl), one element per thread
+__global__ __launch_bounds__(256) void k_resid_slabs(float* __restrict__ x, int D, const float* __restrict__ part,
+                                                     int S) {
+    const int j = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+    if (n < D) x[(size_t)j * D + n] += psum(part, S, D, j, n);
+}
+
+// RMSNorm (+ ada) of row blockIdx.y into fragment-major planes, columns chunk blockIdx.x of
+// 512 (every block sums the squares of the whole row: 12 KB from L2); a thread owns 8
+// consecutive columns: one 16-B piece of each plane
+__global__ __launch_bounds__(64) void k_rmsnorm_fplanes(const float* __restrict__ x, int D,
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ ada, float eps,
                                                         uint16_t* __restrict__ xs) {
-    __shared__ float red[4];
-    const int j = blockIdx.x;
+    const int j = blockIdx.y, tid = threadIdx.x;
     const float* xr = x + (size_t)j * D;
     float ss = 0.f;
-    for (int i = threadIdx.x; i < D; i += 256) ss = fmaf(xr[i], xr[i], ss);
+    for (int i = tid * 4; i < D; i += 64 * 4) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + i);
+        ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, ss))));
+    }
     ss = wave_sum(ss);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-    __syncthreads();
-    const float inv = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)D + eps);
+    const float inv = 1.0f / sqrtf(ss / (float)D + eps);
     const size_t P = (size_t)SK_ROWS * D;
-    for (int i = threadIdx.x; i < D; i += 256) {
-        float v = xr[i] * inv * w[i];
-        if (ada) v *= (1.0f + ada[i]);
-        uint16_t h, m, l;
-        split3(v, h, m, l);
-        xs[(size_t)j * D + i] = h;
-        xs[P + (size_t)j * D + i] = m;
-        xs[2 * P + (size_t)j * D + i] = l;
+    const int c = blockIdx.x * 64 + tid;
+    if (c >= D / 8) return;
+    const int k = c * 8;
+    uint32_t hp[4], mp[4], lp[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+        uint16_t h0, m0, l0, h1, m1, l1;
+        float v0 = xr[k + e] * inv * w[k + e], v1 = xr[k + e + 1] * inv * w[k + e + 1];
+        if (ada) {
+            v0 *= (1.0f + ada[k + e]);
+            v1 *= (1.0f + ada[k + e + 1]);
+        }
+        split3(v0, h0, m0, l0);
+        split3(v1, h1, m1, l1);
+        hp[e / 2] = h0 | ((uint32_t)h1 << 16);
+        mp[e / 2] = m0 | ((uint32_t)m1 << 16);
+        lp[e / 2] = l0 | ((uint32_t)l1 << 16);
     }
+    const size_t o = frag_off(j, k);
+    *reinterpret_cast<uint4*>(xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+    *reinterpret_cast<uint4*>(xs + P + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+    *reinterpret_cast<uint4*>(xs + 2 * P + o) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
 }
 
-__global__ __launch_bounds__(256) void k_split_planes(const float* __restrict__ x, int K, uint16_t* __restrict__ xs) {
+// rows of x (f32) into fragment-major planes
+__global__ __launch_bounds__(256) void k_split_fplanes(const float* __restrict__ x, int K, uint16_t* __restrict__ xs) {
     const int j = blockIdx.y;
-    const size_t P = (size_t)SK_ROWS * K;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < K; i += gridDim.x * 256) {
-        uint16_t h, m, l;
-        split3(x[(size_t)j * K + i], h, m, l);
-        xs[(size_t)j * K + i] = h;
-        xs[P + (size_t)j * K + i] = m;
-        xs[2 * P + (size_t)j * K + i] = l;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= K / 8) return;
+    const int k = c * 8;
+    const float* xr = x + (size_t)j * K + k;
+    const float4 a = *reinterpret_cast<const float4*>(xr), b = *reinterpret_cast<const float4*>(xr + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t hp[4], mp[4], lp[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+        uint16_t h0, m0, l0, h1, m1, l1;
+        split3(v[e], h0, m0, l0);
+        split3(v[e + 1], h1, m1, l1);
+        hp[e / 2] = h0 | ((uint32_t)h1 << 16);
+        mp[e / 2] = m0 | ((uint32_t)m1 << 16);
+        lp[e / 2] = l0 | ((uint32_t)l1 << 16);
     }
+    const size_t P = (size_t)SK_ROWS * K, o = frag_off(j, k);
+    *reinterpret_cast<uint4*>(xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+    *reinterpret_cast<uint4*>(xs + P + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+    *reinterpret_cast<uint4*>(xs + 2 * P + o) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
 }
 
-// W fragment of row r, k32 step at k (16 B of bf16, or 8 int8 converted exactly).  In the
-// MFMA layout one wave-instruction reads half of each of 16 rows' 128-B lines; plain loads
-// keep the line in L2 for the other half (non-temporal ones fetched it twice: 1.6-1.9x the
-// weight bytes from HBM by FETCH_SIZE).
-template <int WQ8>
-__device__ __forceinline__ bf16x8 sk_wfrag(const void* __restrict__ W, size_t r, int K, int k) {
-    if (WQ8) {
-        const uint2 q = *reinterpret_cast<const uint2*>(static_cast<const int8_t*>(W) + r * K + k);
-        uint32_t h[8];
+__device__ __forceinline__ bf16x8 i8x8_bf16(uint32_t lo, uint32_t hi) {
+    uint32_t h[8];
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            h[b] = __float_as_uint(i8f(q.x, b)) >> 16;
-            h[4 + b] = __float_as_uint(i8f(q.y, b)) >> 16;
-        }
-        return __builtin_bit_cast(bf16x8, make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16)));
+    for (int b = 0; b < 4; b++) {
+        h[b] = __float_as_uint(i8f(lo, b)) >> 16;
+        h[4 + b] = __float_as_uint(i8f(hi, b)) >> 16;
     }
-    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(W) + r * K + k));
+    return __builtin_bit_cast(bf16x8, make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16)));
 }
 
-// RT row tiles of 16 per group (RT even: SwiGLU pairs tiles 2i (W1) and 2i+1 (W3)),
-// U k32 steps per load round, NW waves splitting K
-template <int EPI, int WQ8, int NW, int RT, int U>
-__global__ __launch_bounds__(NW * 64) void k_gemm_sk(const uint16_t* __restrict__ xs, int K,
-                                                     const void* __restrict__ W, const float* __restrict__ wscale,
-                                                     int N, int nb, const float* __restrict__ bias,
-                                                     float* __restrict__ C, int ldc, uint16_t* __restrict__ op) {
-    __shared__ float red[NW][RT][4][64];  // [wave][tile][r][lane]: the lane's D registers
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ks = K / 32;
-    const int s0 = (int)((long long)ks * wave / NW), s1 = (int)((long long)ks * (wave + 1) / NW);
-    const int fr = lane & 15, fk = (lane >> 4) * 8;
-    const size_t P = (size_t)SK_ROWS * K;
-    const uint16_t* xp = xs + (size_t)fr * K + fk;
-    constexpr int GR = 16 * RT;  // rows per group
-    const int ngroups = N / GR;
-    for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
-        f32x4 acc[RT];
+// one 64-k block of R row groups (A halves) and of the three planes (B halves)
+template <int WQ8, int R>
+struct SkfRegs {
+    u32x4 a[R][WQ8 ? 1 : 2];
+    uint4 x[3][2];
+};
+
+// block b of the wave's range; past the range the loads go through zero-length descriptors
+// (they return 0 and move no bytes, so the ring below needs no branches)
+template <int WQ8, int R>
+__device__ __forceinline__ void skf_load(SkfRegs<WQ8, R>& s, __amdgpu_buffer_rsrc_t W, __amdgpu_buffer_rsrc_t X,
+                                         int kbytes, int b, int pbytes) {
+    constexpr int FB = WQ8 ? 1024 : 2048;
+    const int lo = (threadIdx.x & 63) * 16;
 #pragma unroll
-        for (int t = 0; t < RT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const size_t rbase = (size_t)g * GR + fr;
-        int s = s0;
-        for (; s + U <= s1; s += U) {
-            bf16x8 wf[U][RT], xf[U][3];
+    for (int p = 0; p < 3; p++)
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int k = (s + u) * 32 + fk;
-#pragma unroll
-                for (int t = 0; t < RT; t++) wf[u][t] = sk_wfrag<WQ8>(W, rbase + 16 * t, K, k);
-#pragma unroll
-                for (int p = 0; p < 3; p++)
-                    xf[u][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xp + p * P + (s + u) * 32));
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++)
-#pragma unroll
-                for (int p = 0; p < 3; p++)
-#pragma unroll
-                    for (int t = 0; t < RT; t++)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[u][t], xf[u][p], acc[t], 0, 0, 0);
-        }
-        for (; s < s1; s++) {  // steps left over when K / 32 is not a multiple of U NW
-            const int k = s * 32 + fk;
-#pragma unroll
-            for (int p = 0; p < 3; p++) {
-                const bf16x8 bx = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xp + p * P + s * 32));
-#pragma unroll
-                for (int t = 0; t < RT; t++)
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sk_wfrag<WQ8>(W, rbase + 16 * t, K, k), bx, acc[t], 0, 0, 0);
-            }
+        for (int t = 0; t < 2; t++) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(X, lo + t * 1024, p * pbytes + b * 2048, 0);
+            s.x[p][t] = make_uint4(v.x, v.y, v.z, v.w);
         }
 #pragma unroll
-        for (int t = 0; t < RT; t++)
+    for (int r = 0; r < R; r++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) red[wave][t][r][lane] = acc[t][r];
-        __syncthreads();
-        // outputs: row rr of the group, column j (stream); D layout inside a 16-row tile:
-        // col = lane&15, row = (lane>>4)*4 + r
-        for (int o = tid; o < GR * 16; o += NW * 64) {
-            const int rr = o >> 4, j = o & 15;
-            if (j >= nb) continue;
-            const int t = rr >> 4, rt = rr & 15;
-            const int ln = ((rt >> 2) << 4) + j, r = rt & 3;
-            const int row = g * GR + rr;
-            if (EPI == EPI_SWIGLU) {
-                if (t & 1) continue;  // W3 tiles are read by their W1 partner
-                float v = 0.f, u = 0.f;
+        for (int t = 0; t < (WQ8 ? 1 : 2); t++)
+            s.a[r][t] = __builtin_amdgcn_raw_buffer_load_b128(W, lo + t * 1024, r * kbytes + b * FB, 2);
+}
+
+template <int WQ8, int R>
+__device__ __forceinline__ void skf_mma(const SkfRegs<WQ8, R>& s, f32x4 (&acc)[R]) {
 #pragma unroll
-                for (int w = 0; w < NW; w++) {
-                    v += red[w][t][r][ln];
-                    u += red[w][t + 1][r][ln];
-                }
-                if (WQ8) {
-                    v *= wscale[row];
-                    u *= wscale[row + 16];
-                }
-                const float gv = silu(v) * u;
-                const int unit = (row >> 5) * 16 + rt;  // 16-row interleave: rows 32q..32q+15 = W1
-                const int H = N / 2;
-                uint16_t h, m, l;
-                split3(gv, h, m, l);
-                const size_t PH = (size_t)SK_ROWS * H;
-                op[(size_t)j * H + unit] = h;
-                op[PH + (size_t)j * H + unit] = m;
-                op[2 * PH + (size_t)j * H + unit] = l;
-                if (C) C[(size_t)j * ldc + unit] = gv;
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            bf16x8 af;
+            if (WQ8) {
+                const u32x4 q = s.a[r][0];
+                af = t ? i8x8_bf16(q.z, q.w) : i8x8_bf16(q.x, q.y);
             } else {
-                float v = 0.f;
-#pragma unroll
-                for (int w = 0; w < NW; w++) v += red[w][t][r][ln];
-                if (WQ8) v *= wscale[row];
-                if (bias) v += bias[row];
-                float* cp = C + (size_t)j * ldc + row;
-                if (EPI == EPI_RESID) *cp += v;
-                else *cp = v;
+                const u32x4 q = s.a[r][t];
+                af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
             }
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, s.x[p][t]), acc[r], 0, 0, 0);
         }
-        __syncthreads();
+}
+
+// Block = R row groups (16R rows) x all of K, K split over NW waves in 64-k blocks; the
+// wave partials meet in LDS and the block stores its 16R x 16 outputs C[j][row] (the LM head:
+// its planes fit no LDS, and at 8192 row groups the per-block plane re-reads are amortised
+// over R = 4 groups).
+template <int WQ8, int R, int NW, int D>
+__global__ __launch_bounds__(NW * 64) void k_skf(const uint16_t* __restrict__ xs, int K,
+                                                 const uint8_t* __restrict__ W, const float* __restrict__ wscale,
+                                                 int N, int nb, float* __restrict__ C, int ldc) {
+    __shared__ float red[NW][R][4][64];
+    constexpr int FB = WQ8 ? 1024 : 2048;
+    // wave index through readfirstlane: a provably uniform block range keeps the buffer
+    // loads' soffset in an SGPR (else every load becomes a waterfall loop)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int KB = K >> 6;
+    const int b0 = KB * wave / NW, b1 = KB * (wave + 1) / NW;
+    const int g0 = blockIdx.x * R;
+    const int kbytes = KB * FB;  // bytes of one row group
+    const __amdgpu_buffer_rsrc_t Wd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g0 * kbytes, 0, R * kbytes, 0x00020000);
+    const int pbytes = SK_ROWS * K * 2;  // one plane
+    const __amdgpu_buffer_rsrc_t Xd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xs), 0, 3 * pbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t Wz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W), 0, 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t Xz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xs), 0, 0, 0x00020000);
+    f32x4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // register ring of D blocks: block b + D - 1 is requested before block b's MFMAs, so a
+    // wave keeps D - 1 blocks of weights and planes in flight
+    SkfRegs<WQ8, R> s[D];
+#define SKF_LOAD(slot, blk)                                                                  \
+    do {                                                                                     \
+        const int bb__ = (blk);                                                              \
+        const bool in__ = bb__ < b1;                                                         \
+        skf_load<WQ8, R>(s[slot], in__ ? Wd : Wz, in__ ? Xd : Xz, kbytes, in__ ? bb__ : 0, pbytes); \
+    } while (0)
+#pragma unroll
+    for (int i = 0; i < D - 1; i++) SKF_LOAD(i, b0 + i);
+    for (int b = b0; b < b1; b += D) {
+#pragma unroll
+        for (int i = 0; i < D; i++) {
+            SKF_LOAD((i + D - 1) % D, b + i + D - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            skf_mma<WQ8, R>(s[i], acc);  // zeros past the range: acc + 0
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
+#undef SKF_LOAD
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) red[wave][r][i][lane] = acc[r][i];
+    __syncthreads();
+    // output o: group r = o >> 8, row rr = (o >> 4) & 15, stream j = o & 15; D layout:
+    // col = lane&15, row = (lane>>4)*4 + i
+    for (int o = tid; o < R * 256; o += NW * 64) {
+        const int r = o >> 8, rr = (o >> 4) & 15, j = o & 15;
+        if (j >= nb) continue;
+        const int ln = ((rr >> 2) << 4) + j, i = rr & 3;
+        const int row = (g0 + r) * 16 + rr;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; w++) v += red[w][r][i][ln];
+        C[(size_t)j * ldc + row] = WQ8 ? v * wscale[row] : v;
+    }
+}
+
+// ============================================================================
+// LDS-planes skinny GEMM (batched decode projections): block (chunk c, k-split s) stages the
+// planes of its KS 64-k blocks in LDS once (KS x 6 KiB, shared by its waves), each wave
+// streams one 16-row group's KS weight blocks -- all issued before the first wait -- and
+// writes its 16 x 16 partial sums to part[s][16][N] (scaled for Q8).  The consumer sums the
+// splits in order (k_rope_kv_batch, k_rmsnorm_fplanes, k_swiglu_fplanes), so no reduction
+// kernel runs and the result does not depend on timing.  Re-reading the planes from L2 per
+// 16-row group (k_skf at R = 1) moved 3x the weight bytes through the load path.
+// ============================================================================
+template <int WQ8, int NW, int KS>
+__global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs, int K,
+                                                 const uint8_t* __restrict__ W, const float* __restrict__ wscale,
+                                                 int N, int nb, float* __restrict__ part) {
+    __shared__ uint4 xb[KS * 6 * 64];  // [block][plane][half][lane]
+    constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
+    constexpr int NF = KS * 6 / NW;  // 16-B plane pieces per thread
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int KB = K >> 6, s = blockIdx.y, kb0 = s * KS;
+    const int g = blockIdx.x * NW + wave;
+    const size_t P = (size_t)SK_ROWS * K;
+    // planes first: vmcnt retires in issue order, so the weights issued after them stay in
+    // flight while the plane pieces are written to LDS
+    uint4 f[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        const int idx = tid + i * NW * 64;
+        const int blk = idx / 384, rem = idx % 384;
+        const int p = rem >> 7, t = (rem >> 6) & 1, l = rem & 63;
+        f[i] = *reinterpret_cast<const uint4*>(xs + p * P + (size_t)((kb0 + blk) * 2 + t) * 512 + l * 8);
+    }
+    const __amdgpu_buffer_rsrc_t Wd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g * KB * FB, 0, KB * FB, 0x00020000);
+    u32x4 a[KS][NH];
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < NH; t++) a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(Wd, lane * 16 + t * 1024, (kb0 + kb) * FB, 2);
+#pragma unroll
+    for (int i = 0; i < NF; i++) xb[tid + i * NW * 64] = f[i];
+    __syncthreads();
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            bf16x8 af;
+            if (WQ8) {
+                const u32x4 q = a[kb][0];
+                af = t ? i8x8_bf16(q.z, q.w) : i8x8_bf16(q.x, q.y);
+            } else {
+                const u32x4 q = a[kb][t];
+                af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
+            }
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, xb[((kb * 3 + p) * 2 + t) * 64 + lane]),
+                                                             acc, 0, 0, 0);
+        }
+    const int j = lane & 15;
+    if (j < nb) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = g * 16 + (lane >> 4) * 4 + i;
+            part[((size_t)s * SK_ROWS + j) * N + row] = WQ8 ? acc[i] * wscale[row] : acc[i];
+        }
+    }
+}
+
+// silu(W1 x) * (W3 x) of the split W1|W3 result (16-row interleave, upload_w13) into the
+// fragment-major planes of the w2 input; a thread owns 2 consecutive hidden units
+__global__ __launch_bounds__(256) void k_swiglu_fplanes(const float* __restrict__ part, int S, int H,
+                                                        uint16_t* __restrict__ xs) {
+    const int j = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= H / 2) return;
+    const int h0 = c * 2, N = 2 * H;
+    const int rg = (h0 >> 4) * 32 + (h0 & 15);  // W1 row of unit h0; its W3 row is rg + 16
+    uint16_t hh[2], mm[2], ll[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const float gv = psum(part, S, N, j, rg + q), uv = psum(part, S, N, j, rg + 16 + q);
+        split3(silu(gv) * uv, hh[q], mm[q], ll[q]);
+    }
+    const size_t P = (size_t)SK_ROWS * H, o = frag_off(j, h0);  // h0 even: one 4-B piece
+    *reinterpret_cast<uint32_t*>(xs + o) = hh[0] | ((uint32_t)hh[1] << 16);
+    *reinterpret_cast<uint32_t*>(xs + P + o) = mm[0] | ((uint32_t)mm[1] << 16);
+    *reinterpret_cast<uint32_t*>(xs + 2 * P + o) = ll[0] | ((uint32_t)ll[1] << 16);
 }
 
 // im2col for the causal conv stem (voxtral_kernels.c:430-447):
@@ -2025,10 +2196,10 @@ hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state
     return hipSuccess;
 }
 
-hipError_t launch_rope_kv_batch(const float* qkv, int nb, int qd, int kvd, int hd, const float* rope,
+hipError_t launch_rope_kv_batch(const float* part, int S, int nb, int qd, int kvd, int hd, const float* rope,
                                 const StepPtrs& sp, int cap, float* q, hipStream_t st) {
-    if (nb < 1 || nb > VOX_MAX_BATCH) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_rope_kv_batch, dim3(nb), dim3(256), 0, st, qkv, qd, kvd, hd, rope, sp, cap, q);
+    if (nb < 1 || nb > VOX_MAX_BATCH || S < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_rope_kv_batch, dim3(nb, 8), dim3(256), 0, st, part, S, qd, kvd, hd, rope, sp, cap, q);
     LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2044,71 +2215,109 @@ hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, 
     return hipSuccess;
 }
 
-hipError_t launch_rmsnorm_planes(const float* x, int nb, int D, const float* w, const float* ada, float eps,
-                                 uint16_t* xs, hipStream_t st) {
-    if (nb < 1 || nb > SK_ROWS) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_rmsnorm_planes, dim3(nb), dim3(256), 0, st, x, D, w, ada, eps, xs);
+hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hipStream_t st) {
+    if (N % 16 || K % 64) return hipErrorInvalidValue;
+    const size_t n16 = (size_t)N * K * (q8 ? 1 : 2) / 16;
+    const dim3 grid((unsigned)((n16 + 255) / 256));
+    if (q8)
+        hipLaunchKernelGGL(k_frag_pack<1>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(src), K, n16,
+                           static_cast<uint8_t*>(dst));
+    else
+        hipLaunchKernelGGL(k_frag_pack<0>, grid, dim3(256), 0, st, static_cast<const uint8_t*>(src), K, n16,
+                           static_cast<uint8_t*>(dst));
     LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t launch_split_planes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st) {
-    if (nb < 1 || nb > SK_ROWS) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_split_planes, dim3((K + 1023) / 1024, nb), dim3(256), 0, st, x, K, xs);
+hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
+                                  uint16_t* xs, const float* part, int S, hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS || D % 64) return hipErrorInvalidValue;
+    if (S > 0) {
+        hipLaunchKernelGGL(k_resid_slabs, dim3((D + 255) / 256, nb), dim3(256), 0, st, x, D, part, S);
+        LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_rmsnorm_fplanes, dim3((D / 8 + 63) / 64, nb), dim3(64), 0, st, x, D, w, ada, eps, xs);
     LAUNCH_CHECK();
     return hipSuccess;
 }
 
-// tuning knobs (kbench; 0 = automatic): row tiles per group, k32 steps per load round,
-// waves per block
-int g_sk_rt = 0, g_sk_u = 0, g_sk_nw = 0;
+hipError_t launch_split_fplanes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS || K % 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_split_fplanes, dim3((K / 8 + 255) / 256, nb), dim3(256), 0, st, x, K, xs);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
 
-template <int E, int Q, int NW, int RT, int U>
-static hipError_t sk_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
-                            const float* bias, float* C, int ldc, uint16_t* op, hipStream_t st) {
-    const int groups = N / (16 * RT);
-    const int grid = std::min(groups, 2048);
-    hipLaunchKernelGGL((k_gemm_sk<E, Q, NW, RT, U>), dim3(grid), dim3(NW * 64), 0, st, xs, K, W, wscale, N, nb, bias, C,
-                       ldc, op);
+hipError_t launch_swiglu_fplanes(const float* part, int S, int H, int nb, uint16_t* xs, hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS || H % 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_swiglu_fplanes, dim3((H / 2 + 255) / 256, nb), dim3(256), 0, st, part, S, H, xs);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// tuning knobs (tools/kbench; 0 = automatic): k_skf row groups per block, waves per block,
+// ring depth; k_skl waves per block
+int g_skf_r = 0, g_skf_nw = 0, g_skf_d = 0, g_skl_nw = 0;
+
+template <int Q, int R, int NW, int D>
+static hipError_t skf_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                             float* C, int ldc, hipStream_t st) {
+    hipLaunchKernelGGL((k_skf<Q, R, NW, D>), dim3(N / (16 * R)), dim3(NW * 64), 0, st, xs, K,
+                       static_cast<const uint8_t*>(W), wscale, N, nb, C, ldc);
     return hipGetLastError();
 }
 
-template <int E, int Q, int RT, int U>
-static hipError_t sk_nw(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
-                        const float* bias, float* C, int ldc, uint16_t* op, hipStream_t st) {
-    const int groups = N / (16 * RT);
-    // waves per block: enough waves on the chip when the row groups are few (N = 3072)
-    const int nw = g_sk_nw ? g_sk_nw : (groups >= 512 ? 4 : groups >= 192 ? 8 : 16);
-    if (nw == 4) return sk_launch<E, Q, 4, RT, U>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
-    if (nw == 8) return sk_launch<E, Q, 8, RT, U>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
-    return sk_launch<E, Q, 16, RT, U>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
-}
+// the configurations built (1024-thread blocks cap a wave at 128 VGPRs: shallower rings)
+#define SKF_CONFIGS(X) \
+    X(1, 4, 2) X(1, 8, 2) X(2, 4, 2) X(2, 4, 3) X(2, 8, 2) X(4, 4, 2) X(4, 8, 2)
 
-template <int E, int Q>
-static hipError_t sk_ru(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
-                        const float* bias, float* C, int ldc, uint16_t* op, hipStream_t st) {
-    // measured at 8 rows (tools/kbench): 8 tiles per group for the wide weights (W1|W3,
-    // LM head: the x fragments are reused 8 times), 2 for the rest
-    int rt = g_sk_rt ? g_sk_rt : (N >= 16384 ? 8 : 2);
-    if (N % (16 * rt)) rt = 2;
-    const int u = g_sk_u ? g_sk_u : (rt == 8 ? 2 : 4);
-#define SK_RU(R, UU) \
-    if (rt == R && u == UU) return sk_nw<E, Q, R, UU>(xs, K, W, wscale, N, nb, bias, C, ldc, op, st);
-    SK_RU(2, 4) SK_RU(2, 8) SK_RU(4, 2) SK_RU(4, 4) SK_RU(8, 2)
-#undef SK_RU
+template <int Q>
+static hipError_t skf_cfg(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb, float* C,
+                          int ldc, hipStream_t st) {
+    const int groups = N / 16;
+    const int r = g_skf_r ? g_skf_r : (groups >= 2048 ? 4 : groups >= 512 ? 2 : 1);
+    if (groups % r) return hipErrorInvalidValue;
+    const int nw = g_skf_nw ? g_skf_nw : 4, d = g_skf_d ? g_skf_d : 2;
+#define SKF_X(RR, NWW, DD) \
+    if (r == RR && nw == NWW && d == DD) return skf_launch<Q, RR, NWW, DD>(xs, K, W, wscale, N, nb, C, ldc, st);
+    SKF_CONFIGS(SKF_X)
+#undef SKF_X
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_gemm_sk(int epi, const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
-                          const float* bias, float* C, int ldc, uint16_t* out_planes, hipStream_t st) {
-    if (nb < 1 || nb > SK_ROWS || N % 32 || K % 32) return hipErrorInvalidValue;
-    if (epi == EPI_SWIGLU && !out_planes) return hipErrorInvalidValue;
-#define SK_CASE(E)                                                                                     \
-    if (epi == E)                                                                                      \
-        return wscale ? sk_ru<E, 1>(xs, K, W, wscale, N, nb, bias, C, ldc, out_planes, st)             \
-                      : sk_ru<E, 0>(xs, K, W, wscale, N, nb, bias, C, ldc, out_planes, st);
-    SK_CASE(EPI_STORE) SK_CASE(EPI_RESID) SK_CASE(EPI_SWIGLU)
-#undef SK_CASE
+hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* C,
+                           int ldc, hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS || N % 64 || K % 64 || !C) return hipErrorInvalidValue;
+    return wscale ? skf_cfg<1>(xs, K, Wf, wscale, N, nb, C, ldc, st) : skf_cfg<0>(xs, K, Wf, wscale, N, nb, C, ldc, st);
+}
+
+template <int Q, int NW, int KS>
+static hipError_t skl_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                             float* part, hipStream_t st) {
+    hipLaunchKernelGGL((k_skl<Q, NW, KS>), dim3(N / (16 * NW), K / (64 * KS)), dim3(NW * 64), 0, st, xs, K,
+                       static_cast<const uint8_t*>(W), wscale, N, nb, part);
+    return hipGetLastError();
+}
+
+int skl_splits(int K) {
+    const int KB = K / 64;
+    return KB % 8 == 0 ? KB / 8 : KB % 4 == 0 ? KB / 4 : 0;
+}
+
+hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
+                           float* part, hipStream_t st) {
+    const int S = skl_splits(K);
+    if (nb < 1 || nb > SK_ROWS || K % 64 || !S) return hipErrorInvalidValue;
+    const int ks = K / 64 / S;
+    // waves (row groups) per block: 4, or 8 when that still gives >= 256 blocks
+    int nw = g_skl_nw ? g_skl_nw : ((N / 128) * S >= 256 && N % 128 == 0 ? 8 : 4);
+    if (N % (16 * nw)) nw = 4;
+    if (N % (16 * nw)) return hipErrorInvalidValue;
+#define SKL_X(Q, NWW, KSS) \
+    if ((wscale != nullptr) == Q && nw == NWW && ks == KSS) return skl_launch<Q, NWW, KSS>(xs, K, Wf, wscale, N, nb, part, st);
+    SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4)
+    SKL_X(1, 4, 8) SKL_X(1, 8, 8) SKL_X(1, 4, 4) SKL_X(1, 8, 4)
+#undef SKL_X
     return hipErrorInvalidValue;
 }
 

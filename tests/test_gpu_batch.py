@@ -111,3 +111,32 @@ def test_batch_full_size_matches_single():
         s.close()
     b.close()
     hm.close()
+
+
+def test_batch_long_context_multiblock(tiny_weights):
+    """TINY_LONG (8192-key window): 4 streams decoded past 256 positions, so the batched
+    attention runs on several 256-key blocks and the combine kernel writes the wo planes;
+    ids equal decoding each stream alone and the CPU oracle."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    mels = _mels(TINY_LONG, [2600, 2900, 2500, 2750], 11)
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 4)
+    got = b.decode(ss, max_steps=1000, stop_at_eos=False)
+    assert min(len(g) for g in got) > 256
+    for i, mel in enumerate(mels):
+        one = vox_hip.Stream(hm)
+        one.encode_mel(mel)
+        assert got[i].tolist() == one.decode(stop_at_eos=False).tolist(), i
+        one.close()
+    assert got[0].tolist() == _reference_tokens(om, mels[0])
+    for s in ss:
+        s.close()
+    b.close()
+    hm.close()
+    om.close()

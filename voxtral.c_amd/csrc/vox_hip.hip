@@ -1324,6 +1324,15 @@ struct vox_hip_batch {
     float* part;     // split-K slabs of the current projection (k_skl), consumed by the next kernel
     int* pidx;
     uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows (fragment order)
+    // one captured step for the current active set (kernel arguments hold per-stream
+    // pointers): replayed while the set, its adapter buffers, the split count and the rope
+    // table stay the same
+    hipGraphExec_t gexec;
+    int gnb, gsplits;
+    vox_hip_stream_t* gkey[VOX_MAX_BATCH];
+    const float* gadapter[VOX_MAX_BATCH];
+    int gadapter_cap[VOX_MAX_BATCH];
+    const float* grope;
 };
 
 // pack one [N, K] matrix (bf16, or int8 when q8) into fragment order (k_frag_pack)
@@ -1362,6 +1371,7 @@ extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     dfree(b->x); dfree(b->part); dfree(b->q); dfree(b->att);
     dfree(b->logits); dfree(b->pval); dfree(b->pidx);
     dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h);
+    if (b->gexec) hipGraphExecDestroy(b->gexec);
     if (b->st) hipStreamDestroy(b->st);
     delete b;
 }
@@ -1442,9 +1452,17 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         // in b->part that the next kernel sums (with the residual for wo / w2)
         CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, b->part, l ? Sres : 0, st));
         CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
-        CK(launch_rope_kv_batch(b->part, skl_splits(DD), nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
-        CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st));
-        CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
+        if (hd == 128) {
+            // RoPE + KV append + attention, output into the wo planes (one launch; + the
+            // combine kernel past 256 keys)
+            AttnFuse af;
+            af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
+            CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st));
+        } else {
+            CK(launch_rope_kv_batch(b->part, skl_splits(DD), nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
+            CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st));
+            CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
+        }
         CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
         CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d, b->part,
                                   skl_splits(DQ), st));
@@ -1458,6 +1476,46 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
     CK(launch_gemm_skf(b->xp_d, DD, m->lm_frag, m->tok_emb_s, c.vocab, nb, b->logits, c.vocab, st));
     CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, sp, ss[0]->tokens_cap, m->tok_emb, m->tok_emb_s,
                            DD, b->x, st));
+    return 0;
+}
+
+// `steps` batched steps: replays of one captured step graph (captured again when the
+// active set or anything its kernel arguments point at changed), or eager launches
+static int batch_run(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, int splits, int steps) {
+    if (!use_graphs()) {
+        for (int k = 0; k < steps; k++)
+            if (batch_step(b, ss, nb, splits)) return -1;
+        return 0;
+    }
+    bool same = b->gexec && b->gnb == nb && b->gsplits == splits && b->grope == b->m->rope_dec;
+    for (int i = 0; same && i < nb; i++)
+        same = b->gkey[i] == ss[i] && b->gadapter[i] == ss[i]->adapter && b->gadapter_cap[i] == ss[i]->adapter_cap;
+    if (!same) {
+        if (b->gexec) {
+            hipGraphExecDestroy(b->gexec);
+            b->gexec = nullptr;
+        }
+        hipGraph_t g = nullptr;
+        CK(hipStreamBeginCapture(b->st, hipStreamCaptureModeThreadLocal));
+        const int rc = batch_step(b, ss, nb, splits);
+        hipError_t e = hipStreamEndCapture(b->st, &g);
+        if (rc || e != hipSuccess) {
+            if (g) hipGraphDestroy(g);
+            return set_err("batch graph capture failed: %s", hipGetErrorString(e));
+        }
+        e = hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        if (e != hipSuccess) return set_err("batch graph instantiate failed: %s", hipGetErrorString(e));
+        b->gnb = nb;
+        b->gsplits = splits;
+        b->grope = b->m->rope_dec;
+        for (int i = 0; i < nb; i++) {
+            b->gkey[i] = ss[i];
+            b->gadapter[i] = ss[i]->adapter;
+            b->gadapter_cap[i] = ss[i]->adapter_cap;
+        }
+    }
+    for (int k = 0; k < steps; k++) CK(hipGraphLaunch(b->gexec, b->st));
     return 0;
 }
 
@@ -1523,8 +1581,7 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
         for (int i = 0; i < nb; i++)
             CK(launch_embed_step(act[i]->adapter, m->tok_emb, m->tok_emb_s, act[i]->state, D, b->x + (size_t)i * D,
                                  b->st));
-        for (int k = 0; k < steps; k++)
-            if (batch_step(b, act.data(), nb, splits)) return -1;
+        if (batch_run(b, act.data(), nb, splits, steps)) return -1;
         CK(hipStreamSynchronize(b->st));
         for (int i = 0; i < nb; i++) {
             vox_hip_stream_t* s = act[i];

@@ -52,6 +52,16 @@ struct AttnPtrs {
     float* out[VOX_MAX_BATCH];
 };
 
+// batched decode attention with the QKV epilogue folded in (k_attn_decode<.., FUSE = 1>):
+// RoPE of q / k and the KV append read the QKV projection's split-K slabs, and the output
+// goes straight into the wo input planes
+struct AttnFuse {
+    const float* qkv;      // [S][16][N] slabs, row z = stream z of the batch
+    int S, N;              // slab count, row length (H*hd + 2*KVH*hd)
+    const float* rope;     // [pos][hd] (cos, sin) table
+    uint16_t* xs;          // [3][16][H*hd] fragment-major planes of the attention output
+};
+
 // per-stream state of a batched decode step (row i of the batch = stream i)
 struct StepPtrs {
     int* state[VOX_MAX_BATCH];          // {kv logical pos, next adapter row, prev token, step}
@@ -89,6 +99,10 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
 hipError_t launch_attn_decode_batch(int hd, const AttnPtrs& p, int nb, int cap, int window, float scale,
                                     int H, int KVH, int splits, hipStream_t st);
 constexpr int ATT_BLOCK_KEYS = 256;  // keys one decode-attention block covers
+// the batched step's attention: RoPE + KV append from the QKV slabs, output as planes
+// (one block per stream x kv head x 256-key split; splits > 1 adds the combine kernel)
+hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window,
+                                   float scale, int H, int KVH, int splits, hipStream_t st);
 
 constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,

@@ -21,6 +21,7 @@
 #include <stdint.h>
 #include <algorithm>
 #include <string.h>
+#include <stdlib.h>
 
 namespace vox {
 
@@ -86,6 +87,30 @@ __device__ __forceinline__ float gelu_tanh(float v) {  // voxtral_kernels.c:505-
 }
 __device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
 __device__ __forceinline__ float silu(float v) { return v / (1.0f + expf(-v)); }  // :498-503
+
+// f32 -> three bf16 terms hi + mid + lo (= the exact f32 value; see k_gemm)
+__device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const uint32_t b0 = f2bf(v);
+    const float r1 = v - __uint_as_float(b0 << 16);
+    const uint32_t b1 = f2bf(r1);
+    const float r2 = r1 - __uint_as_float(b1 << 16);
+    h = (uint16_t)b0;
+    m = (uint16_t)b1;
+    l = (uint16_t)f2bf(r2);
+}
+
+// element (row j, col k) of a fragment-major plane [16][K] (k_skl / k_skf B operand)
+__device__ __forceinline__ size_t frag_off(int j, int k) {  // element (row j, col k) in a plane
+    const int b = k >> 6, r = k & 63;
+    return ((size_t)(b * 2 + ((r >> 3) & 1)) * 64 + (r >> 4) * 16 + j) * 8 + (r & 7);
+}
+
+// element (stream j, column n) of a split-K result: the S partial slabs summed in order
+__device__ __forceinline__ float psum(const float* __restrict__ part, int S, int N, int j, int n) {
+    float v = part[(size_t)j * N + n];
+    for (int s = 1; s < S; s++) v += part[((size_t)s * SK_ROWS + j) * N + n];
+    return v;
+}
 
 // dot of 8 bf16 weights (one uint4) with 8 f32 activations
 __device__ __forceinline__ float dot8(uint4 w, float4 a, float4 b, float acc) {
@@ -1000,10 +1025,10 @@ constexpr int ATT_CH = 16;      // keys per wave
 constexpr int ATT_WAVES = 16;   // waves per block (1024 threads)
 constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per block
 
-template <int HD, int HPB, int DBG = 0>
+template <int HD, int HPB, int DBG = 0, int FUSE = 0>
 __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap, int pos_host,
                                                       int window, float scale, int H, int KVH,
-                                                      int maxs) {
+                                                      int maxs, const AttnFuse F = AttnFuse{}) {
     const int zb = blockIdx.z;  // stream of a batched step (0 for a single stream)
     const float* __restrict__ q = P.q[zb];
     const float* __restrict__ Kc = P.Kc[zb];
@@ -1017,6 +1042,7 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     __shared__ float sM[ATT_WAVES][4], sL[ATT_WAVES][4], sF[ATT_WAVES][4];
     __shared__ float sDen[4], sMax[4];
     __shared__ __attribute__((aligned(16))) float sO[ATT_WAVES][HPB][HD];
+    __shared__ __attribute__((aligned(16))) float sKn[FUSE ? HD : 1], sVn[FUSE ? HD : 1];  // the new key's K / V
     const int hpk = H / KVH;
     const int kvh = HPB == 1 ? (int)blockIdx.y % KVH : (int)blockIdx.y;
     const int h0 = HPB == 1 ? kvh * hpk + (int)blockIdx.y / KVH : kvh * hpk;  // first query head
@@ -1031,7 +1057,7 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     }
     // the query does not depend on the step state: its load goes out first
     float qreg = 0.f;
-    if (tid < nh * HD) qreg = q[(size_t)h0 * HD + tid];
+    if (!FUSE && tid < nh * HD) qreg = q[(size_t)h0 * HD + tid];
     const int lp = state ? state[0] : pos_host;
     const int L = min(lp + 1, window);
     const int first = lp - L + 1;
@@ -1067,12 +1093,62 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
         }
     }
     if (DBG == 4) ts[6] = __builtin_amdgcn_s_memtime();
-    if (tid < nh * HD) sQ[tid / HD][tid % HD] = qreg;
+    const bool holds_new = sb == S - 1;  // the split whose keys end at the new position lp
+    if (FUSE) {
+        // RoPE of this block's query heads and, in the split holding lp, of the new key plus
+        // the KV append (voxtral_decoder.c:709-722), from the QKV slabs of stream zb; the
+        // cache loads above went out first (the new key's K / V come from LDS below)
+        const int qd = H * HD;
+        const float* rp = F.rope + (size_t)lp * HD;
+        const size_t slot = (size_t)(lp % cap) * kvd + kvh * HD;
+        if (tid < nh * HD / 2) {
+            const int h = tid / (HD / 2), d = tid % (HD / 2);
+            const int col = (h0 + h) * HD + 2 * d;
+            const float x0 = psum(F.qkv, F.S, F.N, zb, col), x1 = psum(F.qkv, F.S, F.N, zb, col + 1);
+            const float c = rp[2 * d], sn = rp[2 * d + 1];
+            sQ[h][2 * d] = x0 * c - x1 * sn;
+            sQ[h][2 * d + 1] = x0 * sn + x1 * c;
+        } else if (tid >= 256 && tid < 256 + HD / 2) {
+            if (holds_new) {
+                const int d = tid - 256, col = qd + kvh * HD + 2 * d;
+                const float x0 = psum(F.qkv, F.S, F.N, zb, col), x1 = psum(F.qkv, F.S, F.N, zb, col + 1);
+                const float c = rp[2 * d], sn = rp[2 * d + 1];
+                const float k0v = x0 * c - x1 * sn, k1v = x0 * sn + x1 * c;
+                sKn[2 * d] = k0v;
+                sKn[2 * d + 1] = k1v;
+                float* kw = const_cast<float*>(Kc) + slot + 2 * d;
+                kw[0] = k0v;
+                kw[1] = k1v;
+            }
+        } else if (tid >= 512 && tid < 512 + HD) {
+            if (holds_new) {
+                const int e = tid - 512;
+                const float v = psum(F.qkv, F.S, F.N, zb, qd + kvd + kvh * HD + e);
+                sVn[e] = v;
+                const_cast<float*>(Vc)[slot + e] = v;
+            }
+        }
+    } else if (tid < nh * HD) {
+        sQ[tid / HD][tid % HD] = qreg;
+    }
     if (DBG == 4) {
         __builtin_amdgcn_s_waitcnt(0);
         ts[7] = __builtin_amdgcn_s_memtime();
     }
     __syncthreads();
+    if (FUSE && holds_new && lp >= k0 && lp < k0 + ATT_CH) {
+        // this wave holds the new key (wave-uniform test): its K / V from LDS
+        if (k0 + kk == lp) {
+#pragma unroll
+            for (int i = 0; i < DQ / 4; i++) kv[i] = *reinterpret_cast<const float4*>(&sKn[dq * DQ + 4 * i]);
+        }
+        const int kl = lp - k0;
+#pragma unroll
+        for (int k = 0; k < ATT_CH; k++)
+            if (k == kl)
+#pragma unroll
+                for (int e = 0; e < DPL; e++) vv[k][e] = sVn[lane * DPL + e];
+    }
     if (DBG == 4) ts[1] = __builtin_amdgcn_s_memtime();
     if (DBG == 3) {
         if (lane == 0) out[wave] = kv[0].x + vv[3][0];
@@ -1158,6 +1234,37 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     }
     __syncthreads();
     if (DBG == 4) ts[4] = __builtin_amdgcn_s_memtime();
+    if (FUSE && S == 1) {
+        // output row zb straight into the wo input planes: 8 consecutive dims per thread
+        const size_t Pn = (size_t)SK_ROWS * H * HD;
+        for (int e = tid; e < nh * HD / 8; e += 1024) {
+            const int h = e / (HD / 8), d0 = (e % (HD / 8)) * 8;
+            const float den = sDen[h];
+            uint32_t hp[4], mp[4], lq[4];
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                float v2[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    float num = 0.f;
+#pragma unroll
+                    for (int w = 0; w < ATT_WAVES; w++) num = fmaf(sF[w][h], sO[w][h][d0 + i + u], num);
+                    v2[u] = den > 0.f ? num * (1.0f / den) : 0.f;
+                }
+                uint16_t a0, b0, c0, a1, b1, c1;
+                split3(v2[0], a0, b0, c0);
+                split3(v2[1], a1, b1, c1);
+                hp[i / 2] = a0 | ((uint32_t)a1 << 16);
+                mp[i / 2] = b0 | ((uint32_t)b1 << 16);
+                lq[i / 2] = c0 | ((uint32_t)c1 << 16);
+            }
+            const size_t o = frag_off(zb, (h0 + h) * HD + d0);
+            *reinterpret_cast<uint4*>(F.xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+            *reinterpret_cast<uint4*>(F.xs + Pn + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+            *reinterpret_cast<uint4*>(F.xs + 2 * Pn + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+        }
+        return;
+    }
     for (int e = tid; e < nh * HD; e += 1024) {
         const int h = e / HD, d = e % HD;
         float num = 0.f;
@@ -1187,7 +1294,8 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
 }
 
 template <int HD>
-__global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int maxs, int pos_host, int window) {
+__global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int maxs, int pos_host, int window,
+                                                      uint16_t* __restrict__ xs = nullptr, int H = 0) {
     const float* __restrict__ part = ptrs.part[blockIdx.y];
     const int* __restrict__ state = ptrs.state[blockIdx.y];
     float* __restrict__ out = ptrs.out[blockIdx.y];
@@ -1213,6 +1321,32 @@ __global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int m
         if (tid == 0) sden = den;
     }
     __syncthreads();
+    if (xs) {
+        // batched step: stream blockIdx.y's row of the wo input planes, 8 dims per thread
+        if (tid < HD / 8) {
+            const int d0 = tid * 8;
+            uint32_t hp[4], mp[4], lq[4];
+            for (int i = 0; i < 8; i += 2) {
+                float v2[2];
+                for (int u = 0; u < 2; u++) {
+                    float num = 0.f;
+                    for (int k = 0; k < P; k++) num = fmaf(sf[k], ph[(size_t)k * (HD + 2) + d0 + i + u], num);
+                    v2[u] = sden > 0.f ? num * (1.0f / sden) : 0.f;
+                }
+                uint16_t a0, b0, c0, a1, b1, c1;
+                split3(v2[0], a0, b0, c0);
+                split3(v2[1], a1, b1, c1);
+                hp[i / 2] = a0 | ((uint32_t)a1 << 16);
+                mp[i / 2] = b0 | ((uint32_t)b1 << 16);
+                lq[i / 2] = c0 | ((uint32_t)c1 << 16);
+            }
+            const size_t Pn = (size_t)SK_ROWS * H * HD, o = frag_off(blockIdx.y, h * HD + d0);
+            *reinterpret_cast<uint4*>(xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+            *reinterpret_cast<uint4*>(xs + Pn + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+            *reinterpret_cast<uint4*>(xs + 2 * Pn + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+        }
+        return;
+    }
     for (int d = tid; d < HD; d += 256) {
         float num = 0.f;
         for (int i = 0; i < P; i++) num = fmaf(sf[i], ph[(size_t)i * (HD + 2) + d], num);
@@ -1408,13 +1542,6 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
 // Batched decode step (C4): row i of the batch belongs to stream i.
 // ============================================================================
 // RoPE + KV append per row at that stream's own logical position (decoder.c:709-722)
-// element (stream j, column n) of a split-K result: the S partial slabs summed in order
-__device__ __forceinline__ float psum(const float* __restrict__ part, int S, int N, int j, int n) {
-    float v = part[(size_t)j * N + n];
-    for (int s = 1; s < S; s++) v += part[((size_t)s * SK_ROWS + j) * N + n];
-    return v;
-}
-
 __global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__ part, int S, int qd, int kvd,
                                                        int hd, const float* __restrict__ rope, const StepPtrs sp,
                                                        int cap, float* __restrict__ q) {
@@ -1521,15 +1648,6 @@ __global__ __launch_bounds__(256) void k_argmax_batch_final(const float* __restr
 // three bf16 planes hi/mid/lo (hi + mid + lo = the row exactly) so that MFMA products with
 // bf16 / int8 weights are exact.
 // ============================================================================
-__device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
-    const uint32_t b0 = f2bf(v);
-    const float r1 = v - __uint_as_float(b0 << 16);
-    const uint32_t b1 = f2bf(r1);
-    const float r2 = r1 - __uint_as_float(b1 << 16);
-    h = (uint16_t)b0;
-    m = (uint16_t)b1;
-    l = (uint16_t)f2bf(r2);
-}
 
 // ============================================================================
 // Fragment-major skinny GEMM (batched decode, M <= 16 rows).  The batched path keeps its own
@@ -1544,10 +1662,6 @@ __device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16
 // Weight and plane loads are then contiguous 1 KiB per wave-instruction (the row-major
 // fragment loads touched 16 rows x 64 B each and cost twice the address-unit time).
 // ============================================================================
-__device__ __forceinline__ size_t frag_off(int j, int k) {  // element (row j, col k) in a plane
-    const int b = k >> 6, r = k & 63;
-    return ((size_t)(b * 2 + ((r >> 3) & 1)) * 64 + (r >> 4) * 16 + j) * 8 + (r & 7);
-}
 
 // one thread per 16 B of the packed copy
 template <int WQ8>
@@ -2121,8 +2235,13 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
     const int maxs = attn_maxch(window);
     if (H % KVH || H / KVH > 4 || maxs > 64 || splits < 1 || splits > maxs || nb < 1 || nb > VOX_MAX_BATCH)
         return hipErrorInvalidValue;
+    // batches of >= 4 streams: one block per (stream, kv head), K/V read once for its query
+    // heads (16 streams: 15.8 -> ~10 us per layer); a single stream needs the 32 blocks
 #define VOX_ATT(HD)                                                                                        \
-    if (splits == 1) {                                                                                     \
+    if (splits == 1 && nb >= 4) {                                                                         \
+        hipLaunchKernelGGL((k_attn_decode<HD, 4>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, pos_host,  \
+                           window, scale, H, KVH, maxs);                                                   \
+    } else if (splits == 1) {                                                                              \
         hipLaunchKernelGGL((k_attn_decode<HD, 1>), dim3(1, H, nb), dim3(1024), 0, st, p, cap, pos_host,    \
                            window, scale, H, KVH, maxs);                                                   \
     } else {                                                                                               \
@@ -2157,6 +2276,22 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
 hipError_t launch_attn_decode_batch(int hd, const AttnPtrs& p, int nb, int cap, int window, float scale,
                                     int H, int KVH, int splits, hipStream_t st) {
     return attn_launch(hd, p, nb, cap, 0, window, scale, H, KVH, splits, st);
+}
+
+hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window,
+                                   float scale, int H, int KVH, int splits, hipStream_t st) {
+    const int maxs = attn_maxch(window);
+    if (hd != 128 || H % KVH || H / KVH > 4 || maxs > 64 || splits < 1 || splits > maxs || nb < 1 ||
+        nb > VOX_MAX_BATCH || !f.qkv || !f.rope || !f.xs || f.S < 1 || f.N != (H + 2 * KVH) * hd)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1>), dim3(splits, KVH, nb), dim3(1024), 0, st, p, cap, 0, window,
+                       scale, H, KVH, maxs, f);
+    LAUNCH_CHECK();
+    if (splits > 1) {
+        hipLaunchKernelGGL(k_attn_combine<128>, dim3(H, nb), dim3(256), 0, st, p, maxs, 0, window, f.xs, H);
+        LAUNCH_CHECK();
+    }
+    return hipSuccess;
 }
 // diagnostic variants for tools/kbench (not used by the engine)
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,

@@ -1730,6 +1730,71 @@ __global__ __launch_bounds__(64) void k_rmsnorm_fplanes(const float* __restrict_
     *reinterpret_cast<uint4*>(xs + 2 * P + o) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
 }
 
+// Residual + RMSNorm (+ ada) of row blockIdx.x in one pass: x += the S slabs of the previous
+// projection (k_skl, summed in split order as k_resid_slabs), the updated row written back,
+// its sum of squares reduced in the block, the normalised row stored as fragment-major
+// planes.  A thread owns 8 consecutive columns (D <= 8 * 512).
+__global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict__ x, int D,
+                                                               const float* __restrict__ part, int S,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ ada, float eps,
+                                                               uint16_t* __restrict__ xs) {
+    __shared__ float sred[8];
+    const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int k = tid * 8;
+    const bool own = k < D;
+    float v[8];
+    float ss = 0.f;
+    if (own) {
+        float* xr = x + (size_t)j * D + k;
+        const float4 a = *reinterpret_cast<const float4*>(xr), b = *reinterpret_cast<const float4*>(xr + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        if (S > 0) {
+            float r[8];
+            for (int s = 0; s < S; s++) {
+                const float* pp = part + ((size_t)s * SK_ROWS + j) * D + k;
+                const float4 c = *reinterpret_cast<const float4*>(pp), d = *reinterpret_cast<const float4*>(pp + 4);
+                const float t[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++) r[e] = s ? r[e] + t[e] : t[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] += r[e];
+            *reinterpret_cast<float4*>(xr) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(xr + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) ss = fmaf(v[e], v[e], ss);
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) sred[wave] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; i++) tot += sred[i];
+    if (!own) return;
+    const float inv = 1.0f / sqrtf(tot / (float)D + eps);
+    uint32_t hp[4], mp[4], lq[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+        float v0 = v[e] * inv * w[k + e], v1 = v[e + 1] * inv * w[k + e + 1];
+        if (ada) {
+            v0 *= (1.0f + ada[k + e]);
+            v1 *= (1.0f + ada[k + e + 1]);
+        }
+        uint16_t h0, m0, l0, h1, m1, l1;
+        split3(v0, h0, m0, l0);
+        split3(v1, h1, m1, l1);
+        hp[e / 2] = h0 | ((uint32_t)h1 << 16);
+        mp[e / 2] = m0 | ((uint32_t)m1 << 16);
+        lq[e / 2] = l0 | ((uint32_t)l1 << 16);
+    }
+    const size_t P = (size_t)SK_ROWS * D, o = frag_off(j, k);
+    *reinterpret_cast<uint4*>(xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+    *reinterpret_cast<uint4*>(xs + P + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+    *reinterpret_cast<uint4*>(xs + 2 * P + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+}
+
 // rows of x (f32) into fragment-major planes
 __global__ __launch_bounds__(256) void k_split_fplanes(const float* __restrict__ x, int K, uint16_t* __restrict__ xs) {
     const int j = blockIdx.y;
@@ -2367,6 +2432,11 @@ hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hi
 hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
                                   uint16_t* xs, const float* part, int S, hipStream_t st) {
     if (nb < 1 || nb > SK_ROWS || D % 64) return hipErrorInvalidValue;
+    if (D <= 8 * 512) {
+        hipLaunchKernelGGL(k_resid_rmsnorm_fplanes, dim3(nb), dim3(512), 0, st, x, D, part, S, w, ada, eps, xs);
+        LAUNCH_CHECK();
+        return hipSuccess;
+    }
     if (S > 0) {
         hipLaunchKernelGGL(k_resid_slabs, dim3((D + 255) / 256, nb), dim3(256), 0, st, x, D, part, S);
         LAUNCH_CHECK();

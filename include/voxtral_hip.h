@@ -117,6 +117,31 @@ int vox_hip_stream_reset_decoder(vox_hip_stream_t *s);
 int vox_hip_stream_encode_mel(vox_hip_stream_t *s, const float *mel, int n_frames,
                               int mel_on_device);
 int vox_hip_stream_adapter_tokens(vox_hip_stream_t *s);
+
+/* Incremental log-mel on the device: a vox_mel_ctx_t
+ * (voxtral_audio.c:405-671) whose padded sample buffer and frames live in HBM, computed on
+ * the stream's HIP queue ahead of the encoder (one block per frame: Hann window, direct
+ * 201 x 400 DFT, Slaney filters, log10 clamp).  Frame indices are global, as in the
+ * reference (vox_mel_frame_offset + position); a frame's device pointer feeds
+ * vox_hip_stream_encode_mel(..., mel_on_device = 1) directly. */
+typedef struct vox_hip_mel vox_hip_mel_t;
+/* vox_mel_ctx_init (voxtral_audio.c:515-558): 200 + left_pad_samples zeros of padding */
+vox_hip_mel_t *vox_hip_mel_create(vox_hip_stream_t *s, int left_pad_samples);
+/* vox_mel_feed (voxtral_audio.c:560-582): returns the frames added, <0 on error */
+int vox_hip_mel_feed(vox_hip_mel_t *m, const float *samples, int n_samples);
+/* vox_mel_finish (voxtral_audio.c:584-633): right_pad zeros, 200-sample reflect, last frame
+ * dropped; returns the live frame count */
+int vox_hip_mel_finish(vox_hip_mel_t *m, int right_pad_samples);
+/* vox_mel_data's count and vox_mel_frame_offset (voxtral_audio.c:635-643) */
+int vox_hip_mel_frames(const vox_hip_mel_t *m, int *frame_offset);
+/* device pointer of global frame f (frame_offset <= f <= frame_offset + frames) */
+const float *vox_hip_mel_frame_ptr(const vox_hip_mel_t *m, int global_frame);
+/* vox_mel_discard_before (voxtral_audio.c:645-662) */
+int vox_hip_mel_discard_before(vox_hip_mel_t *m, int keep_from_frame);
+/* copy live frames [first, first + n) to the host (tests) */
+int vox_hip_mel_read(vox_hip_mel_t *m, int global_first, int n, float *out);
+/* vox_mel_free (voxtral_audio.c:664-671) */
+void vox_hip_mel_free(vox_hip_mel_t *m);
 /* Copy adapter rows [first, first+n) to host (tests). */
 int vox_hip_stream_read_adapter(vox_hip_stream_t *s, int first, int n, float *out);
 

@@ -636,6 +636,226 @@ extern "C" int vox_hip_stream_sync(vox_hip_stream_t* s) {
 }
 
 // ---------------------------------------------------------------------------
+// Incremental log-mel on the device: the vox_mel_ctx_t of
+// voxtral_audio.c:405-671 with its padded sample buffer and its frames in HBM.  The
+// kernels run on the owning stream's queue, ahead of the encoder that reads the frames.
+// ---------------------------------------------------------------------------
+static const int MEL_FFT = 400, MEL_FREQ = 201, MEL_HOP = 160, MEL_BINS = 128, MEL_SR = 16000;
+static const float MEL_LOG_MAX = 1.5f;                // LOG_MEL_MAX (voxtral_audio.c:25)
+static const long long MEL_COMPACT_MIN = 16000;       // MEL_SAMPLE_COMPACT_MIN (:429)
+
+struct vox_hip_mel {
+    vox_hip_stream_t* s;
+    float *window, *dcosT, *dsinT, *filtT;  // device tables (built on the host as the reference does)
+    float* samples;                         // padded audio; samples[0] = global sample sample_offset
+    long long n_samples, samples_cap, sample_offset;
+    float* mel;                             // frames; mel[0] = global frame mel_phys0
+    int mel_cap, mel_phys0;
+    int frame_offset, n_frames;             // live frames: global [frame_offset, frame_offset + n_frames)
+    int finished;
+};
+
+// hertz_to_mel / mel_to_hertz / build_mel_filters (voxtral_audio.c:223-285), f32 as there
+static float mel_hz_to_mel(float f) {
+    const float logstep = 27.0f / logf(6.4f);
+    float m = 3.0f * f / 200.0f;
+    if (f >= 1000.0f) m = 15.0f + logf(f / 1000.0f) * logstep;
+    return m;
+}
+static float mel_mel_to_hz(float m) {
+    const float logstep = logf(6.4f) / 27.0f;
+    float f = 200.0f * m / 3.0f;
+    if (m >= 15.0f) f = 1000.0f * expf(logstep * (m - 15.0f));
+    return f;
+}
+
+extern "C" void vox_hip_mel_free(vox_hip_mel_t* m) {
+    if (!m) return;
+    if (m->s) hipStreamSynchronize(m->s->st);
+    dfree(m->window); dfree(m->dcosT); dfree(m->dsinT); dfree(m->filtT); dfree(m->samples); dfree(m->mel);
+    delete m;
+}
+
+extern "C" vox_hip_mel_t* vox_hip_mel_create(vox_hip_stream_t* s, int left_pad_samples) {
+    if (!s || left_pad_samples < 0) {
+        set_err("vox_hip_mel_create: bad arguments");
+        return nullptr;
+    }
+    vox_hip_mel_t* m = new vox_hip_mel_t();
+    memset((void*)m, 0, sizeof *m);
+    m->s = s;
+    auto fail = [&]() -> vox_hip_mel_t* { vox_hip_mel_free(m); return nullptr; };
+    std::vector<float> win(MEL_FFT), dc((size_t)MEL_FFT * MEL_FREQ), ds((size_t)MEL_FFT * MEL_FREQ),
+        ft((size_t)MEL_FREQ * MEL_BINS, 0.f);
+    // DFT tables and periodic Hann window (voxtral_audio.c:531-545)
+    for (int k = 0; k < MEL_FREQ; k++)
+        for (int n = 0; n < MEL_FFT; n++) {
+            const float ang = 2.0f * (float)M_PI * (float)k * (float)n / (float)MEL_FFT;
+            dc[(size_t)n * MEL_FREQ + k] = cosf(ang);
+            ds[(size_t)n * MEL_FREQ + k] = sinf(ang);
+        }
+    for (int i = 0; i < MEL_FFT; i++) win[i] = 0.5f * (1.0f - cosf(2.0f * (float)M_PI * (float)i / (float)MEL_FFT));
+    // Slaney filters (voxtral_audio.c:248-285), stored [freq][bin]
+    float fft_freqs[MEL_FREQ], ffq[MEL_BINS + 2], fdf[MEL_BINS + 1];
+    for (int i = 0; i < MEL_FREQ; i++) fft_freqs[i] = (float)i * ((float)MEL_SR / 2.0f) / (float)(MEL_FREQ - 1);
+    const float mmin = mel_hz_to_mel(0.0f), mmax = mel_hz_to_mel((float)MEL_SR / 2.0f);
+    for (int i = 0; i < MEL_BINS + 2; i++) ffq[i] = mel_mel_to_hz(mmin + (mmax - mmin) * (float)i / (float)(MEL_BINS + 1));
+    for (int i = 0; i < MEL_BINS + 1; i++) {
+        fdf[i] = ffq[i + 1] - ffq[i];
+        if (fdf[i] == 0.0f) fdf[i] = 1e-6f;
+    }
+    for (int b = 0; b < MEL_BINS; b++) {
+        const float enorm = 2.0f / (ffq[b + 2] - ffq[b]);
+        for (int f = 0; f < MEL_FREQ; f++) {
+            const float down = (fft_freqs[f] - ffq[b]) / fdf[b];
+            const float up = (ffq[b + 2] - fft_freqs[f]) / fdf[b + 1];
+            float v = fminf(down, up);
+            if (v < 0.0f) v = 0.0f;
+            ft[(size_t)f * MEL_BINS + b] = v * enorm;
+        }
+    }
+#define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
+    TRYH(dalloc(&m->window, win.size()));
+    TRYH(dalloc(&m->dcosT, dc.size()));
+    TRYH(dalloc(&m->dsinT, ds.size()));
+    TRYH(dalloc(&m->filtT, ft.size()));
+    TRYH(h2d(m->window, win.data(), win.size() * 4));
+    TRYH(h2d(m->dcosT, dc.data(), dc.size() * 4));
+    TRYH(h2d(m->dsinT, ds.data(), ds.size() * 4));
+    TRYH(h2d(m->filtT, ft.data(), ft.size() * 4));
+    // left padding: 200 (center reflect over silence) + left_pad_samples zeros (:547-557)
+    m->n_samples = 200 + (long long)left_pad_samples;
+    m->samples_cap = m->n_samples + 16000;
+    TRYH(dalloc(&m->samples, (size_t)m->samples_cap));   // zeroed
+    m->mel_cap = 1024;
+    TRYH(dalloc(&m->mel, (size_t)m->mel_cap * MEL_BINS));
+#undef TRYH
+    return m;
+}
+
+static int mel_reserve_samples(vox_hip_mel_t* m, long long need) {
+    if (need <= m->samples_cap) return 0;
+    long long nc = m->samples_cap;
+    while (nc < need) nc *= 2;
+    float* nb = nullptr;
+    CK(dalloc(&nb, (size_t)nc));
+    CK(hipMemcpyAsync(nb, m->samples, (size_t)m->n_samples * 4, hipMemcpyDeviceToDevice, m->s->st));
+    CK(hipStreamSynchronize(m->s->st));
+    dfree(m->samples);
+    m->samples = nb;
+    m->samples_cap = nc;
+    return 0;
+}
+
+// mel_compute_available (voxtral_audio.c:454-513): every frame whose window fits
+static int mel_compute(vox_hip_mel_t* m) {
+    const long long next = (long long)m->frame_offset + m->n_frames;  // global index of the next frame
+    long long nf = 0;
+    while ((next + nf) * MEL_HOP - m->sample_offset + MEL_FFT <= m->n_samples) nf++;
+    if (nf == 0) return 0;
+    const long long need = next + nf - m->mel_phys0;  // physical frames after this call
+    if (need > m->mel_cap) {
+        // grow, keeping only the live frames (discarded ones are dropped here)
+        int nc = m->mel_cap;
+        while (nc < need - (m->frame_offset - m->mel_phys0)) nc *= 2;
+        float* nb = nullptr;
+        CK(dalloc(&nb, (size_t)nc * MEL_BINS));
+        if (m->n_frames)
+            CK(hipMemcpyAsync(nb, m->mel + (size_t)(m->frame_offset - m->mel_phys0) * MEL_BINS,
+                              (size_t)m->n_frames * MEL_BINS * 4, hipMemcpyDeviceToDevice, m->s->st));
+        CK(hipStreamSynchronize(m->s->st));
+        dfree(m->mel);
+        m->mel = nb;
+        m->mel_cap = nc;
+        m->mel_phys0 = m->frame_offset;
+    }
+    CK(launch_mel_frames(m->samples, next * MEL_HOP - m->sample_offset, (int)nf, m->window, m->dcosT, m->dsinT,
+                         m->filtT, MEL_LOG_MAX - 8.0f, m->mel + (size_t)(next - m->mel_phys0) * MEL_BINS, m->s->st));
+    m->n_frames += (int)nf;
+    return (int)nf;
+}
+
+// mel_compact_samples (voxtral_audio.c:432-451): samples no future frame reads are dropped
+// once they reach 1 s (and never overlap the kept tail, so one device copy moves it)
+static int mel_compact(vox_hip_mel_t* m) {
+    const long long needed_from = ((long long)m->frame_offset + m->n_frames) * MEL_HOP;
+    long long discard = needed_from - m->sample_offset;
+    if (discard <= 0) return 0;
+    if (discard > m->n_samples) discard = m->n_samples;
+    const long long remain = m->n_samples - discard;
+    if (discard < MEL_COMPACT_MIN || remain > discard) return 0;
+    if (remain > 0)
+        CK(hipMemcpyAsync(m->samples, m->samples + discard, (size_t)remain * 4, hipMemcpyDeviceToDevice, m->s->st));
+    m->n_samples = remain;
+    m->sample_offset += discard;
+    return 0;
+}
+
+extern "C" int vox_hip_mel_feed(vox_hip_mel_t* m, const float* samples, int n) {
+    if (!m || m->finished) return set_err("vox_hip_mel_feed: no context or already finished");
+    if (n <= 0) return 0;
+    if (mel_reserve_samples(m, m->n_samples + n)) return -1;
+    CK(hipMemcpyAsync(m->samples + m->n_samples, samples, (size_t)n * 4, hipMemcpyHostToDevice, m->s->st));
+    m->n_samples += n;
+    const int nf = mel_compute(m);
+    if (nf < 0 || mel_compact(m)) return -1;
+    return nf;
+}
+
+extern "C" int vox_hip_mel_finish(vox_hip_mel_t* m, int right_pad) {
+    if (!m) return set_err("vox_hip_mel_finish: no context");
+    if (m->finished) return m->n_frames;
+    if (right_pad < 0) right_pad = 0;
+    if (mel_reserve_samples(m, m->n_samples + right_pad + 200)) return -1;
+    if (right_pad > 0)
+        CK(hipMemsetAsync(m->samples + m->n_samples, 0, (size_t)right_pad * 4, m->s->st));
+    m->n_samples += right_pad;
+    // right reflect over the last real samples (voxtral_audio.c:609-624)
+    CK(launch_mel_reflect(m->samples, m->n_samples, m->n_samples - right_pad, 200, m->s->st));
+    m->n_samples += 200;
+    if (mel_compute(m) < 0) return -1;
+    if (m->n_frames > 0) m->n_frames--;  // the last frame is dropped (:629-630)
+    m->finished = 1;
+    return m->n_frames;
+}
+
+extern "C" int vox_hip_mel_frames(const vox_hip_mel_t* m, int* frame_offset) {
+    if (!m) return -1;
+    if (frame_offset) *frame_offset = m->frame_offset;
+    return m->n_frames;
+}
+
+extern "C" const float* vox_hip_mel_frame_ptr(const vox_hip_mel_t* m, int global_frame) {
+    if (!m || global_frame < m->frame_offset || global_frame > m->frame_offset + m->n_frames) {
+        set_err("vox_hip_mel_frame_ptr: frame %d outside the live range", global_frame);
+        return nullptr;
+    }
+    return m->mel + (size_t)(global_frame - m->mel_phys0) * MEL_BINS;
+}
+
+// vox_mel_discard_before (voxtral_audio.c:645-662): frames before keep_from_frame leave the
+// live range (their memory is reclaimed at the next growth)
+extern "C" int vox_hip_mel_discard_before(vox_hip_mel_t* m, int keep_from_frame) {
+    if (!m) return -1;
+    if (keep_from_frame <= m->frame_offset) return 0;
+    int d = keep_from_frame - m->frame_offset;
+    if (d > m->n_frames) d = m->n_frames;
+    m->frame_offset += d;
+    m->n_frames -= d;
+    return mel_compact(m);
+}
+
+extern "C" int vox_hip_mel_read(vox_hip_mel_t* m, int global_first, int n, float* out) {
+    if (!m || n < 0 || global_first < m->frame_offset || global_first + n > m->frame_offset + m->n_frames)
+        return set_err("vox_hip_mel_read: range outside the live frames");
+    if (n == 0) return 0;
+    CK(hipMemcpyAsync(out, m->mel + (size_t)(global_first - m->mel_phys0) * MEL_BINS, (size_t)n * MEL_BINS * 4,
+                      hipMemcpyDeviceToHost, m->s->st));
+    CK(hipStreamSynchronize(m->s->st));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
 // Encoder: 32 layers on rows [0, n) of x (logical positions pos0..), in place.
 // voxtral_encoder.c:562-686.  rope: rows for these positions (table slice or per-call).
 // ---------------------------------------------------------------------------

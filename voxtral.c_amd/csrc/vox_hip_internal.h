@@ -141,5 +141,11 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);
+// device log-mel (vox_hip_mel_*): nframes frames from samples[start0 + 160 f ..]; tables
+// transposed: dcosT / dsinT [400][201], filtT [201][128]
+hipError_t launch_mel_frames(const float* samples, long long start0, int nframes, const float* window,
+                             const float* dcosT, const float* dsinT, const float* filtT, float log_min, float* mel,
+                             hipStream_t st);
+hipError_t launch_mel_reflect(float* buf, long long n, long long real_end, int len, hipStream_t st);
 
 }  // namespace vox

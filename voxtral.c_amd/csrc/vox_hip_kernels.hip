@@ -2065,6 +2065,60 @@ __global__ void k_mel_tail(const float* __restrict__ melp, int n_new, int MB, fl
 }
 
 // ============================================================================
+// Incremental log-mel on the device (voxtral_audio.c:454-513, one block per frame).
+// Frame f reads samples[start0 + 160 f .. + 400): Hann-windowed, direct 201 x 400 DFT with
+// the reference's float tables (cos/sin of 2 pi k n / 400 in float, transposed [n][k] so
+// the threads' k are consecutive), power re^2 + im^2, 128 Slaney filters ([k][b] order),
+// log10 clamped at LOG_MEL_MAX - 8, (v + 4) / 4.  Every product and sum is a separately
+// rounded f32 operation in the reference's order (n ascending, then k ascending): no FMA
+// contraction (#pragma below), so only log10f's last bit can differ from the CPU path.
+// ============================================================================
+constexpr int MELK_FFT = 400, MELK_FREQ = 201, MELK_HOP = 160, MELK_BINS = 128;
+
+__global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ samples, long long start0,
+                                                    const float* __restrict__ window,
+                                                    const float* __restrict__ dcosT,
+                                                    const float* __restrict__ dsinT,
+                                                    const float* __restrict__ filtT, float log_min,
+                                                    float* __restrict__ mel) {
+    // hipcc contracts a * b + c into an FMA by default; the reference rounds the product
+    // first, which moves low-power bins by up to 1e-4 relative
+#pragma clang fp contract(off)
+    __shared__ float win[MELK_FFT];
+    __shared__ float pw[MELK_FREQ];
+    const int tid = threadIdx.x;
+    const float* sp = samples + start0 + (long long)blockIdx.x * MELK_HOP;
+    for (int i = tid; i < MELK_FFT; i += 256) win[i] = sp[i] * window[i];
+    __syncthreads();
+    if (tid < MELK_FREQ) {
+        float re = 0.f, im = 0.f;
+        for (int n = 0; n < MELK_FFT; n++) {
+            const float w = win[n];
+            re = re + w * dcosT[n * MELK_FREQ + tid];
+            im = im + w * dsinT[n * MELK_FREQ + tid];
+        }
+        pw[tid] = re * re + im * im;
+    }
+    __syncthreads();
+    if (tid < MELK_BINS) {
+        float sum = 0.f;
+        for (int k = 0; k < MELK_FREQ; k++) sum = sum + filtT[k * MELK_BINS + tid] * pw[k];
+        if (sum < 1e-10f) sum = 1e-10f;
+        float v = log10f(sum);
+        if (v < log_min) v = log_min;
+        mel[(size_t)blockIdx.x * MELK_BINS + tid] = (v + 4.0f) / 4.0f;
+    }
+}
+
+// vox_mel_finish's right reflect (voxtral_audio.c:615-623): dst[i] = buf[real_end - 2 - i]
+__global__ void k_mel_reflect(float* __restrict__ buf, long long n, long long real_end, int len) {
+    for (int i = threadIdx.x; i < len; i += blockDim.x) {
+        const long long src = real_end - 2 - i;
+        buf[n + i] = src >= 0 ? buf[src] : 0.f;
+    }
+}
+
+// ============================================================================
 // Host-side launchers
 // ============================================================================
 #define LAUNCH_CHECK() \
@@ -2530,6 +2584,22 @@ hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, f
                           hipStream_t st) {
     if (T <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_im2col3, dim3(T), dim3(256), 0, st, src, C, T, stride, off, A);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_mel_frames(const float* samples, long long start0, int nframes, const float* window,
+                             const float* dcosT, const float* dsinT, const float* filtT, float log_min, float* mel,
+                             hipStream_t st) {
+    if (nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mel_frames, dim3(nframes), dim3(256), 0, st, samples, start0, window, dcosT, dsinT, filtT,
+                       log_min, mel);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_mel_reflect(float* buf, long long n, long long real_end, int len, hipStream_t st) {
+    hipLaunchKernelGGL(k_mel_reflect, dim3(1), dim3(256), 0, st, buf, n, real_end, len);
     LAUNCH_CHECK();
     return hipSuccess;
 }

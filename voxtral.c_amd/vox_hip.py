@@ -2,8 +2,9 @@
 
 Loads libvoxtral_hip.so (built in-tree by __graft_entry__.build()) and exposes the same
 objects the reference's C API has (voxtral.h:251-337): a model loaded once, streams fed
-incrementally, greedy token ids out.  The mel front-end stays on the host and is not
-part of this package (out of scope); streams are fed log-mel frames.
+incrementally, greedy token ids out.  Streams take log-mel frames (host or device
+arrays), or raw 16 kHz samples through AudioSession, whose incremental log-mel (Mel,
+vox_mel_ctx_t) runs on the device.
 
 There is no CPU fallback: if the HIP library or a GPU is missing every entry point
 raises.
@@ -44,6 +45,8 @@ EXPORTS = [
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
     "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
     "vox_hip_stream_sync", "vox_hip_device_upload", "vox_hip_device_free",
+    "vox_hip_mel_create", "vox_hip_mel_feed", "vox_hip_mel_finish", "vox_hip_mel_frames",
+    "vox_hip_mel_frame_ptr", "vox_hip_mel_discard_before", "vox_hip_mel_read", "vox_hip_mel_free",
 ]
 
 _lib = None
@@ -91,6 +94,10 @@ def lib():
         "vox_hip_stream_sync": (I, [P]),
         "vox_hip_device_upload": (P, [P, ctypes.c_size_t]),
         "vox_hip_device_free": (I, [P]),
+        "vox_hip_mel_create": (P, [P, I]), "vox_hip_mel_feed": (I, [P, fp, I]),
+        "vox_hip_mel_finish": (I, [P, I]), "vox_hip_mel_frames": (I, [P, ip]),
+        "vox_hip_mel_frame_ptr": (P, [P, I]), "vox_hip_mel_discard_before": (I, [P, I]),
+        "vox_hip_mel_read": (I, [P, I, I, fp]), "vox_hip_mel_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -253,8 +260,13 @@ class Session:
         self.tokens: list[int] = []
         self.chunks: list[int] = []
 
-    def _run_encoder(self, mel_all: np.ndarray, min_new: int):
-        total = mel_all.shape[0]
+    def _run_encoder(self, mel_all, min_new: int):
+        """stream_run_encoder's chunk decision (voxtral.c:827-851); mel_all is the host
+        frame array so far, or a device Mel (frames stay in HBM, discarded once encoded)."""
+        dev = isinstance(mel_all, Mel)
+        total = mel_all.total if dev else mel_all.shape[0]
+        if dev:
+            self.mel_cursor = max(self.mel_cursor, mel_all.offset)
         new = total - self.mel_cursor
         need = STREAM_FIRST_CHUNK_MIN_MEL if not self.conv_started else min_new
         if new < need and not self.finished:
@@ -262,9 +274,14 @@ class Session:
         if new <= 0:
             return
         self.chunks.append(new)
-        self.s.encode_mel(mel_all[self.mel_cursor:total])
+        if dev:
+            self.s.encode_mel_device(mel_all.ptr(self.mel_cursor), new)
+        else:
+            self.s.encode_mel(mel_all[self.mel_cursor:total])
         self.conv_started = True
         self.mel_cursor = total
+        if dev:
+            mel_all.discard_before(self.mel_cursor)
 
     def _run_decoder(self, stop_at_eos=True):
         self.tokens += self.s.decode(stop_at_eos=stop_at_eos).tolist()
@@ -284,6 +301,91 @@ class Session:
         self.finished = True
         self._run_encoder(mel_all, self.min_new_mel)
         self._run_decoder(stop_at_eos)
+
+
+class Mel:
+    """Incremental log-mel on the device (vox_mel_ctx_t twin, voxtral_audio.c:405-671):
+    samples in, frames kept in HBM for encode_mel_device.  Frame indices are global."""
+
+    def __init__(self, stream: Stream, left_pad_samples: int = 32 * 1280):
+        self.h = lib().vox_hip_mel_create(stream.h, left_pad_samples)
+        if not self.h:
+            _err("vox_hip_mel_create")
+
+    def feed(self, samples: np.ndarray) -> int:
+        samples = np.ascontiguousarray(samples, dtype=np.float32)
+        n = lib().vox_hip_mel_feed(self.h, fptr(samples), samples.shape[0])
+        if n < 0:
+            _err("mel_feed")
+        return n
+
+    def finish(self, right_pad: int = 0) -> int:
+        n = lib().vox_hip_mel_finish(self.h, right_pad)
+        if n < 0:
+            _err("mel_finish")
+        return n
+
+    @property
+    def offset(self) -> int:
+        off = ctypes.c_int(0)
+        lib().vox_hip_mel_frames(self.h, ctypes.byref(off))
+        return off.value
+
+    @property
+    def total(self) -> int:
+        off = ctypes.c_int(0)
+        n = lib().vox_hip_mel_frames(self.h, ctypes.byref(off))
+        return off.value + n
+
+    def ptr(self, frame: int) -> int:
+        p = lib().vox_hip_mel_frame_ptr(self.h, frame)
+        if not p:
+            _err("mel_frame_ptr")
+        return p
+
+    def discard_before(self, frame: int):
+        if lib().vox_hip_mel_discard_before(self.h, frame) != 0:
+            _err("mel_discard_before")
+
+    def read(self, first: int, n: int) -> np.ndarray:
+        out = np.empty((n, 128), np.float32)
+        if n and lib().vox_hip_mel_read(self.h, first, n, fptr(out)) != 0:
+            _err("mel_read")
+        return out
+
+    def close(self):
+        if self.h:
+            lib().vox_hip_mel_free(self.h)
+            self.h = None
+
+
+class AudioSession(Session):
+    """vox_stream_feed / vox_stream_flush / vox_stream_finish (voxtral.c:1288-1316,
+    1640-1667) over raw 16 kHz samples: the log-mel is computed on the device (Mel) and
+    encoded from HBM, so only the samples cross PCIe."""
+
+    def __init__(self, stream: Stream, interval_s: float = STREAM_DEFAULT_INTERVAL):
+        super().__init__(stream, interval_s)
+        self.mel = Mel(stream, 32 * RAW_AUDIO_LENGTH_PER_TOK)
+        self.real_samples = 0
+
+    def feed_samples(self, samples: np.ndarray, stop_at_eos=True):
+        self.mel.feed(samples)
+        self.real_samples += int(samples.shape[0])
+        self.feed(self.mel, stop_at_eos)
+
+    def flush_samples(self, stop_at_eos=True):
+        pad = right_pad_samples(self.real_samples, self.s.model.delay_tokens)
+        self.mel.feed(np.zeros(pad, np.float32))
+        self.flush(self.mel, stop_at_eos)
+
+    def finish_samples(self, stop_at_eos=True):
+        self.flush_samples(stop_at_eos)
+        self.mel.finish(0)
+        self.finish(self.mel, stop_at_eos)
+
+    def close(self):
+        self.mel.close()
 
 
 def right_pad_samples(n_real_samples: int, delay_tokens: int) -> int:

@@ -48,6 +48,10 @@ def parse():
                     help="config 4: streams per GPU decoded together (batched weight reads)")
     ap.add_argument("--q8", action="store_true",
                     help="config 5: Q8 weights (the quantize.py layout, quantised from the seeded bf16 set)")
+    ap.add_argument("--streaming", action="store_true",
+                    help="config 3: raw audio fed in -I-sized pieces through the device mel + chunked encoder")
+    ap.add_argument("--audio-seconds", type=float, default=180.0, help="config 3 audio length")
+    ap.add_argument("--interval", type=float, default=0.5, help="config 3 -I interval (s)")
     return ap.parse_args()
 
 
@@ -173,6 +177,8 @@ def main():
     mel_dev = vox_hip.DeviceArray(mel)
     if args.streams > 1:
         return bench_streams(args, d, cfg, model, st, mel, mel_dev, rng)
+    if args.streaming:
+        return bench_streaming(args, d, cfg, model, st)
 
     for _ in range(args.warmup):
         transcribe(st, mel_dev, cfg.mel_bins)
@@ -249,6 +255,113 @@ def main():
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     mel_dev.free()
+    st.close()
+    model.close()
+
+
+def synth_audio(seconds, seed):
+    """Speech-band synthetic audio: noise bursts under a slow envelope plus drifting tones
+    (no recording is available offline; the path's work depends only on the length)."""
+    rng = np.random.default_rng(seed)
+    n = int(seconds * 16000)
+    t = np.arange(n) / 16000.0
+    env = 0.5 + 0.5 * np.sin(2 * np.pi * 0.7 * t) * np.sin(2 * np.pi * 0.13 * t)
+    x = 0.05 * rng.standard_normal(n) * env + 0.1 * env * np.sin(2 * np.pi * (180 + 60 * np.sin(0.5 * t)) * t)
+    return x.astype(np.float32)
+
+
+def bench_streaming(args, d, cfg, model, st):
+    """config 3 (BASELINE.json configs[2]): main.c's file mode with -I <interval>
+    (main.c:110-118, 200-204): the audio goes in interval-sized pieces through
+    vox_stream_feed (device log-mel, incremental conv stem, chunked encoder with the
+    rolling 750-row KV, adapter) with the decoder drained after every piece, then
+    vox_stream_finish.  Decoding ignores EOS so the work is fixed."""
+    import vox_hip
+    audio = synth_audio(args.audio_seconds, 99 + d.rank)
+    piece = max(160, min(int(args.interval * 16000), 16000 * 60))
+    secs = len(audio) / 16000.0
+
+    class Timed:
+        """the stream with its encoder / decoder calls timed (synchronised)"""
+        def __init__(self, s):
+            self.s, self.model, self.cfg = s, s.model, s.cfg
+            self.t_enc = self.t_dec = 0.0
+            self.steps = 0
+
+        def encode_mel_device(self, ptr, n):
+            t0 = time.perf_counter()
+            r = self.s.encode_mel_device(ptr, n)
+            self.s.sync()
+            self.t_enc += time.perf_counter() - t0
+            return r
+
+        def decode(self, **kw):
+            t0 = time.perf_counter()
+            r = self.s.decode(**kw)
+            self.t_dec += time.perf_counter() - t0
+            self.steps += len(r)
+            return r
+
+    def run():
+        st.reset()
+        ts = Timed(st)
+        sess = vox_hip.AudioSession(st, interval_s=args.interval)
+        sess.s = ts
+        t_mel = 0.0
+        t0 = time.perf_counter()
+        for i in range(0, len(audio), piece):
+            a = time.perf_counter()
+            sess.mel.feed(audio[i:i + piece])
+            st.sync()
+            t_mel += time.perf_counter() - a
+            sess.real_samples += min(piece, len(audio) - i)
+            sess.feed(sess.mel, stop_at_eos=False)
+        sess.finish_samples(stop_at_eos=False)
+        st.sync()
+        wall = time.perf_counter() - t0
+        sess.close()
+        return {"wall": wall, "enc": ts.t_enc + t_mel, "dec": ts.t_dec, "steps": ts.steps,
+                "chunks": len(sess.chunks), "tokens": len(sess.tokens)}
+
+    for _ in range(args.warmup):
+        run()
+    d.barrier()
+    runs = [run() for _ in range(args.steps)]
+    d.barrier()
+    dec_s = d.max(sum(r["dec"] for r in runs))
+    steps_all = d.sum(sum(r["steps"] for r in runs))
+    enc_s = d.max(sum(r["enc"] for r in runs))
+    wall = d.max(sum(r["wall"] for r in runs))
+    tok_s = steps_all / dec_s
+    # encoder chunk roofline: a 0.5 s chunk is ~25 encoder rows, far below the MFMA ridge
+    # (SURVEY.md 8d): every chunk streams the encoder + adapter weights once (bf16 / int8)
+    wb = 1 if args.q8 else 2
+    eq, ekv = cfg.enc_heads * cfg.enc_head_dim, cfg.enc_kv_heads * cfg.enc_head_dim
+    enc_w = cfg.enc_layers * (eq + 2 * ekv + eq + 2 * cfg.enc_hidden + cfg.enc_hidden) * cfg.enc_dim * wb
+    enc_w += (4 * cfg.enc_dim + cfg.dec_dim) * cfg.dec_dim * wb
+    ms_chunk = enc_s * 1000.0 / max(1, sum(r["chunks"] for r in runs))
+    out = {
+        "metric": "decoder tokens/sec + encoder RTF, Voxtral-4B " + ("q8" if args.q8 else "bf16")
+                  + f", streaming -I {args.interval} (config 3), at 1/2/4/8 MI355X",
+        "value": round(tok_s, 2), "unit": "tokens/s", "n_gpus": d.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall * 1000.0 / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": round(tok_s / d.world / MPS_TOK_S, 2),
+        "dtype": "f32", "weights_dtype": "q8" if args.q8 else "bf16",
+        "data": "synthetic (seeded random weights of the exact architecture; synthetic speech-band audio)",
+        "config": {"workload": f"{args.audio_seconds:.0f} s of 16 kHz audio fed in {piece}-sample pieces "
+                               f"(main.c file mode, -I {args.interval}): device log-mel, {runs[0]['chunks']} encoder "
+                               f"chunks, {runs[0]['steps']} greedy steps (KV to ~{runs[0]['steps'] + 40} positions)",
+                   "model": "Voxtral-Mini-4B-Realtime", "global_batch": d.world, "seq_len": runs[0]["steps"],
+                   "streams_per_gpu": 1, "parallelism": f"replicas x{d.world} (no collective)"},
+        "encoder_rtf": round(enc_s / (secs * args.steps), 5),
+        "overall_rtf": round(wall / (secs * args.steps), 5),
+        "encoder_ms_per_chunk": round(ms_chunk, 3),
+        "encoder_weight_bytes_per_chunk": enc_w,
+        "encoder_chunk_weight_gbs": round(enc_w / (ms_chunk * 1e-3) / 1e9, 1),
+        "decoder_ms_per_token": round(dec_s * 1000.0 / max(1, steps_all / d.world), 4),
+    }
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
     st.close()
     model.close()
 

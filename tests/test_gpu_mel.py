@@ -113,3 +113,33 @@ def test_audio_session_matches_oracle_tokens(tiny_cfg, tiny_weights, jfk_samples
     assert sess.chunks == osess.chunks
     sess.close()
     hs.close(); hm.close(); os_.close(); om.close()
+
+
+def test_audio_session_long_window_streaming(tiny_weights):
+    """TINY_LONG (real 750-row encoder window): 30 s of audio in 0.5 s pieces at -I 0.5, so
+    every encoder chunk (~25 rows) attends over up to ~775 cached keys through the
+    key-split tiled attention; adapter rows and tokens match the oracle."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    rng = np.random.default_rng(5)
+    t = np.arange(16000 * 30) / 16000.0
+    x = (0.05 * rng.standard_normal(t.size) + 0.1 * np.sin(2 * np.pi * 220 * t)).astype(np.float32)
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    hs = vox_hip.Stream(hm)
+    sess = vox_hip.AudioSession(hs, interval_s=0.5)
+    for i in range(0, len(x), 8000):
+        sess.feed_samples(x[i:i + 8000], stop_at_eos=False)
+    sess.finish_samples(stop_at_eos=False)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    os_ = vox_oracle.OracleStream(om)
+    osess = vox_oracle.OracleSession(os_, interval_s=0.5)
+    for kind, mel in vox_oracle.transcribe_mel_schedule(x, feed_size=8000):
+        getattr(osess, kind)(mel, stop_at_eos=False)
+    assert sess.chunks == osess.chunks and len(sess.chunks) > 50
+    ha, oa = hs.read_adapter(), os_.read_adapter()
+    assert ha.shape == oa.shape
+    assert np.max(np.abs(ha - oa)) < 1e-3 * float(np.max(np.abs(oa)))
+    assert sess.tokens == osess.tokens
+    sess.close()
+    hs.close(); hm.close(); os_.close(); om.close()

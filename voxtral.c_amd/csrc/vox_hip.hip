@@ -874,7 +874,8 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.attn_norm, nullptr, n, ED, c.enc_eps, st));
         CK(launch_gemm(EPI_STORE, 3, s->xn, ED, L.wqkv, L.sqkv, ED, n, EQ + 2 * EKV, L.bqkv, s->qkv, EQ + 2 * EKV, st, s->gws, s->gws_n));
         CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
-        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st));
+        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
+                             s->gws, s->gws_n));
         CK(launch_gemm(EPI_RESID, 3, s->att, EQ, L.wo, L.so, EQ, n, ED, L.bo, x, ED, st, s->gws, s->gws_n));
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.ffn_norm, nullptr, n, ED, c.enc_eps, st));
         CK(launch_gemm(EPI_SWIGLU, 3, s->xn, ED, L.w13, L.s13, ED, n, 2 * EH, nullptr, s->gate, EH, st, s->gws, s->gws_n));
@@ -1005,7 +1006,8 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.attn_norm, nullptr, n, DD, c.dec_eps, st));
         CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, L.sqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st, s->gws, s->gws_n));
         CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st));
-        CK(launch_attn_tiled(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st));
+        CK(launch_attn_tiled(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st,
+                             s->gws, s->gws_n));
         CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, L.so, DQ, n, DD, nullptr, x, DD, st, s->gws, s->gws_n));
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, n, DD, c.dec_eps, st));
         CK(launch_gemm(EPI_SWIGLU, 3, s->xnd, DD, L.w13, L.s13, DD, n, 2 * DH, nullptr, s->gated, DH, st, s->gws, s->gws_n));

@@ -592,7 +592,10 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
                                                     const float* __restrict__ Vc, int cap,
                                                     float* __restrict__ O, int ldo, int M, int H,
                                                     int KVH, int q_pos0, int k_first, int window,
-                                                    float scale) {
+                                                    float scale, int ns, float* __restrict__ part) {
+    // ns > 1 (few query rows, long key range: streaming encoder chunks): blockIdx.z takes
+    // the z-th of ns key ranges and writes an unnormalised (o, m, l) partial per query row
+    // to part[(h * M + q) * ns + z][HD + 2]; k_attn_tiled_combine merges them in z order.
     constexpr int QT = 16, KT = 64, DPT = HD / 16;
     __shared__ __attribute__((aligned(16))) float sQ[QT][HD];
     __shared__ __attribute__((aligned(16))) float sK[KT][HD + 4];
@@ -612,7 +615,13 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
     const int qfirst = q_pos0 + q0, qlast = q_pos0 + q0 + nq - 1;
     int kstart = qfirst - window + 1;
     if (kstart < k_first) kstart = k_first;
-    const int kend = qlast;
+    int kend = qlast;
+    if (ns > 1) {
+        const int span = ((kend - kstart + 1 + ns - 1) / ns + KT - 1) / KT * KT;
+        const int z = blockIdx.z;
+        kstart += z * span;
+        kend = min(kend, kstart + span - 1);
+    }
 
     float m = -1e30f, l = 0.f;
     float o[DPT];
@@ -686,12 +695,38 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
             }
         }
     }
-    if (qvalid) {
+    if (qvalid && ns > 1) {
+        float* pp = part + ((size_t)(h * M + q0 + qi) * ns + blockIdx.z) * (HD + 2);
+#pragma unroll
+        for (int e = 0; e < DPT; e++) pp[j * DPT + e] = o[e];
+        if (j == 0) {
+            pp[HD] = m;
+            pp[HD + 1] = l;
+        }
+    } else if (qvalid) {
         float inv = l > 0.f ? 1.0f / l : 0.f;
         float* op = O + (size_t)(q0 + qi) * ldo + h * HD + j * DPT;
 #pragma unroll
         for (int e = 0; e < DPT; e++) op[e] = o[e] * inv;
     }
+}
+
+// merge of k_attn_tiled's ns key-range partials: one block per (head, query row)
+template <int HD>
+__global__ __launch_bounds__(HD) void k_attn_tiled_combine(const float* __restrict__ part, int ns, int M,
+                                                           float* __restrict__ O, int ldo) {
+    const int h = blockIdx.x, q = blockIdx.y, d = threadIdx.x;
+    const float* pp = part + (size_t)(h * M + q) * ns * (HD + 2);
+    float mx = -1e30f;
+    for (int z = 0; z < ns; z++) mx = fmaxf(mx, pp[(size_t)z * (HD + 2) + HD]);
+    float num = 0.f, den = 0.f;
+    for (int z = 0; z < ns; z++) {
+        const float* pz = pp + (size_t)z * (HD + 2);
+        const float f = expf(pz[HD] - mx);
+        den = fmaf(f, pz[HD + 1], den);
+        num = fmaf(f, pz[d], num);
+    }
+    O[(size_t)q * ldo + h * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
 }
 
 // ============================================================================
@@ -2245,16 +2280,35 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
 
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
-                             int k_first, int window, float scale, hipStream_t st) {
+                             int k_first, int window, float scale, hipStream_t st, float* ws, size_t ws_elems) {
     if (M <= 0) return hipSuccess;
-    dim3 grid(H, (M + 15) / 16);
+    if (hd != 64 && hd != 128) return hipErrorInvalidValue;
+    const int qb = (M + 15) / 16;
+    // key-range splits when the (head, query block) grid cannot fill the chip: at least 64
+    // keys per split, about 512 blocks in all (a 25-row streaming chunk over ~775 keys: 12)
+    int ks = q_pos0 - window + 1;
+    if (ks < k_first) ks = k_first;
+    const int keys = q_pos0 + M - ks;
+    int ns = 1;
+    if (ws && H * qb < 256) {
+        ns = std::min((keys + 63) / 64, std::max(1, 512 / (H * qb)));
+        while (ns > 1 && (size_t)H * M * ns * (hd + 2) > ws_elems) ns--;
+    }
+    dim3 grid(H, qb, ns);
     if (hd == 64)
-        hipLaunchKernelGGL(k_attn_tiled<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0, k_first, window, scale);
-    else if (hd == 128)
-        hipLaunchKernelGGL(k_attn_tiled<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0, k_first, window, scale);
+        hipLaunchKernelGGL(k_attn_tiled<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
+                           k_first, window, scale, ns, ws);
     else
-        return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_attn_tiled<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
+                           k_first, window, scale, ns, ws);
     LAUNCH_CHECK();
+    if (ns > 1) {
+        if (hd == 64)
+            hipLaunchKernelGGL(k_attn_tiled_combine<64>, dim3(H, M), dim3(64), 0, st, ws, ns, M, O, ldo);
+        else
+            hipLaunchKernelGGL(k_attn_tiled_combine<128>, dim3(H, M), dim3(128), 0, st, ws, ns, M, O, ldo);
+        LAUNCH_CHECK();
+    }
     return hipSuccess;
 }
 

@@ -1104,15 +1104,29 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     // ring slots: one modulo per wave, then a wrap test per key
     const int slot0 = k0 % cap;
 
-    // K quarter-rows and V dims for this wave's 16 keys
+    // K and V of this wave's 16 keys.  KROW (head_dim 128): load i covers 8 keys x one
+    // 128-B quarter row (lane = key (lane >> 3) + 8 (i & 1), 16 B at (lane & 7)), so a wave
+    // instruction touches 8 whole cache lines instead of 16 B of 64 lines: the CU's address
+    // path took 6400 cycles per wave for the quarter-row-per-lane pattern (tools/kbench DBG 4).
+    constexpr bool KROW = (HD == 128);
     float4 kv[DQ / 4];
     float vv[ATT_CH][DPL];
     {
-        int sk = slot0 + (kk < kn ? kk : 0);
-        sk = sk >= cap ? sk - cap : sk;
-        const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)sk * kvd + kvh * HD + dq * DQ);
+        if (KROW) {
 #pragma unroll
-        for (int i = 0; i < DQ / 4; i++) kv[i] = kr[i];
+            for (int i = 0; i < DQ / 4; i++) {
+                const int key = (lane >> 3) + 8 * (i & 1);
+                int sk = slot0 + (key < kn ? key : 0);
+                sk = sk >= cap ? sk - cap : sk;
+                kv[i] = *reinterpret_cast<const float4*>(Kc + (size_t)sk * kvd + kvh * HD + (i >> 1) * DQ + (lane & 7) * 4);
+            }
+        } else {
+            int sk = slot0 + (kk < kn ? kk : 0);
+            sk = sk >= cap ? sk - cap : sk;
+            const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)sk * kvd + kvh * HD + dq * DQ);
+#pragma unroll
+            for (int i = 0; i < DQ / 4; i++) kv[i] = kr[i];
+        }
 #pragma unroll
         for (int k = 0; k < ATT_CH; k++) {
             int sv = slot0 + (k < kn ? k : 0);
@@ -1173,11 +1187,17 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     __syncthreads();
     if (FUSE && holds_new && lp >= k0 && lp < k0 + ATT_CH) {
         // this wave holds the new key (wave-uniform test): its K / V from LDS
-        if (k0 + kk == lp) {
+        const int kl = lp - k0;
+        if (KROW) {
+            if ((lane >> 3) == (kl & 7)) {
+#pragma unroll
+                for (int i = 0; i < DQ / 4; i++)
+                    if ((i & 1) == (kl >> 3)) kv[i] = *reinterpret_cast<const float4*>(&sKn[(i >> 1) * DQ + (lane & 7) * 4]);
+            }
+        } else if (k0 + kk == lp) {
 #pragma unroll
             for (int i = 0; i < DQ / 4; i++) kv[i] = *reinterpret_cast<const float4*>(&sKn[dq * DQ + 4 * i]);
         }
-        const int kl = lp - k0;
 #pragma unroll
         for (int k = 0; k < ATT_CH; k++)
             if (k == kl)
@@ -1190,40 +1210,82 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
         return;
     }
 
-    float sc[HPB];
+    float m[HPB], l[HPB], p[HPB], pb[HPB], o[HPB][DPL];
+    if (KROW) {
+        // lane (key r = lane >> 3, chunk c = lane & 7) sums its 16 dims of keys r and r + 8;
+        // the 8 chunk lanes meet by DPP (xor 1, xor 2, half-row mirror), the 8 key groups by
+        // row mirror and two cross-row shuffles
+        const int r = lane >> 3, c = lane & 7;
 #pragma unroll
-    for (int h = 0; h < HPB; h++) {
-        float acc = 0.f;
-        if (h < nh) {
+        for (int h = 0; h < HPB; h++) {
+            float aa = 0.f, ab = 0.f;
+            if (h < nh) {
 #pragma unroll
-            for (int i = 0; i < DQ / 4; i++) {
-                const float4 qv = *reinterpret_cast<const float4*>(&sQ[h][dq * DQ + 4 * i]);
-                acc = fmaf(qv.x, kv[i].x, acc);
-                acc = fmaf(qv.y, kv[i].y, acc);
-                acc = fmaf(qv.z, kv[i].z, acc);
-                acc = fmaf(qv.w, kv[i].w, acc);
+                for (int i = 0; i < DQ / 4; i++) {
+                    const float4 qv = *reinterpret_cast<const float4*>(&sQ[h][(i >> 1) * DQ + c * 4]);
+                    float& acc = (i & 1) ? ab : aa;
+                    acc = fmaf(qv.x, kv[i].x, acc);
+                    acc = fmaf(qv.y, kv[i].y, acc);
+                    acc = fmaf(qv.z, kv[i].z, acc);
+                    acc = fmaf(qv.w, kv[i].w, acc);
+                }
             }
+            aa += dpp<0xB1>(aa); aa += dpp<0x4E>(aa); aa += dpp<0x141>(aa);
+            ab += dpp<0xB1>(ab); ab += dpp<0x4E>(ab); ab += dpp<0x141>(ab);
+            const float sa = (r < kn) ? aa * scale : -INFINITY, sbv = (r + 8 < kn) ? ab * scale : -INFINITY;
+            float mx = fmaxf(sa, sbv);
+            mx = fmaxf(mx, dpp<0x140>(mx));
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            m[h] = (kn > 0) ? mx : -1e30f;
+            p[h] = (r < kn) ? expf(sa - mx) : 0.f;
+            pb[h] = (r + 8 < kn) ? expf(sbv - mx) : 0.f;
+            float t = p[h] + pb[h];
+            t += dpp<0x140>(t);
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            l[h] = t;
+#pragma unroll
+            for (int e = 0; e < DPL; e++) o[h][e] = 0.f;
         }
-        acc += __shfl_xor(acc, 16, 64);
-        acc += __shfl_xor(acc, 32, 64);
-        sc[h] = (kk < kn) ? acc * scale : -INFINITY;
-    }
-    float m[HPB], l[HPB], p[HPB], o[HPB][DPL];
+    } else {
+        float sc[HPB];
 #pragma unroll
-    for (int h = 0; h < HPB; h++) {
-        const float mx = row_max16(sc[h]);
-        m[h] = (kn > 0) ? mx : -1e30f;
-        p[h] = (kk < kn) ? expf(sc[h] - mx) : 0.f;
-        l[h] = row_sum16(p[h]);
+        for (int h = 0; h < HPB; h++) {
+            float acc = 0.f;
+            if (h < nh) {
 #pragma unroll
-        for (int e = 0; e < DPL; e++) o[h][e] = 0.f;
+                for (int i = 0; i < DQ / 4; i++) {
+                    const float4 qv = *reinterpret_cast<const float4*>(&sQ[h][dq * DQ + 4 * i]);
+                    acc = fmaf(qv.x, kv[i].x, acc);
+                    acc = fmaf(qv.y, kv[i].y, acc);
+                    acc = fmaf(qv.z, kv[i].z, acc);
+                    acc = fmaf(qv.w, kv[i].w, acc);
+                }
+            }
+            acc += __shfl_xor(acc, 16, 64);
+            acc += __shfl_xor(acc, 32, 64);
+            sc[h] = (kk < kn) ? acc * scale : -INFINITY;
+        }
+#pragma unroll
+        for (int h = 0; h < HPB; h++) {
+            const float mx = row_max16(sc[h]);
+            m[h] = (kn > 0) ? mx : -1e30f;
+            p[h] = (kk < kn) ? expf(sc[h] - mx) : 0.f;
+            pb[h] = 0.f;
+            l[h] = row_sum16(p[h]);
+#pragma unroll
+            for (int e = 0; e < DPL; e++) o[h][e] = 0.f;
+        }
     }
 #pragma unroll
     for (int k = 0; k < ATT_CH; k++) {
 #pragma unroll
         for (int h = 0; h < HPB; h++) {
-            // lane k holds key k's weight (zero past the valid keys): a scalar broadcast
-            const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[h]), k));
+            // the lane holding key k's weight (zero past the valid keys): a scalar broadcast
+            const int src = KROW ? 8 * (k & 7) : k;
+            const float pv = (KROW && k >= 8) ? pb[h] : p[h];
+            const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), src));
 #pragma unroll
             for (int e = 0; e < DPL; e++) o[h][e] = fmaf(pk, vv[k][e], o[h][e]);
         }

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -108,6 +108,23 @@ int main(int argc, char** argv) {
     add("gemv wo   (3072x4096, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ * 2);
     add("gemv w13  (18432x3072, norm+swiglu)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
     add("gemv w2   (3072x9216, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH * 2);
+    g_gemv_rb = 4;
+    add("gemv qkv RB4 (grid 768, 2 groups)", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D * 2);
+    add("gemv w13 RB4", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
+    g_gemv_rb = 2;
+    add("gemv wo RB2 (1536 groups)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ * 2);
+    add("gemv w2 RB2 (1536 groups)", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH * 2);
+    add("gemv qkv RB2", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D * 2);
+    g_gemv_rb = 4;
+    add("gemv lm RB4", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D * 2);
+    qs = wsc;
+    add("q8 gemv qkv RB4", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D);
+    add("q8 gemv w13 RB4", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D);
+    g_gemv_rb = 2;
+    add("q8 gemv wo RB2", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ);
+    add("q8 gemv w2 RB2", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH);
+    qs = nullptr;
+    g_gemv_rb = 0;
     add("gemv w13 same buffer (MALL-hot)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[0], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
     add("gemv wo same buffer (MALL-hot)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[0], DQ, D); }, iters, st), (double)D * DQ * 2);
     add("gemv lm   (131072x3072, logits)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D * 2);

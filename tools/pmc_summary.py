@@ -13,12 +13,12 @@ import json
 import os
 import sys
 
-W13 = "k_gemv<2, 4, 8, 2, 0>"   # PRO_NORM_ADA, EPI_SWIGLU, RB 8, KQ 2, bf16
+W13 = "k_gemv<2, 4, 4, 2, 0>"   # PRO_NORM_ADA, EPI_SWIGLU, RB 4, KQ 2, bf16
 ALGO = {  # algorithmic bytes per launch (weights + activation vectors), DESIGN.md section 5
-    "k_gemv<2, 4, 8, 2, 0>": 2 * 9216 * 3072 * 2 + 3072 * 4 * 3 + 9216 * 4,
-    "k_gemv<0, 1, 4, 5, 0>": 3072 * 9216 * 2 + 9216 * 4 + 3072 * 8,
-    "k_gemv<1, 5, 8, 2, 0>": 6144 * 3072 * 2 + 3072 * 8 + 6144 * 4,
-    "k_gemv<0, 1, 4, 2, 0>": 3072 * 4096 * 2 + 4096 * 4 + 3072 * 8,
+    "k_gemv<2, 4, 4, 2, 0>": 2 * 9216 * 3072 * 2 + 3072 * 4 * 3 + 9216 * 4,
+    "k_gemv<0, 1, 2, 5, 0>": 3072 * 9216 * 2 + 9216 * 4 + 3072 * 8,
+    "k_gemv<1, 5, 4, 2, 0>": 6144 * 3072 * 2 + 3072 * 8 + 6144 * 4,
+    "k_gemv<0, 1, 2, 2, 0>": 3072 * 4096 * 2 + 4096 * 4 + 3072 * 8,
     "k_gemv<1, 6, 8, 2, 0>": 131072 * 3072 * 2 + 3072 * 8 + 131072 * 4,
 }
 

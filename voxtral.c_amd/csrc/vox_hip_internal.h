@@ -14,7 +14,7 @@ constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3
 enum { PRO_NONE = 0, PRO_NORM = 1, PRO_NORM_ADA = 2 };
 
 constexpr int GEMV_MAX_BLOCKS = 1024;  // 4 blocks of 256 threads per CU on 256 CUs
-constexpr int GEMV_RB = 4;             // rows per block iteration (even: rope / swiglu pairs)
+constexpr int GEMV_RB = 4;             // (unused by the launcher: gemv_rb picks 2, 4 or 8 rows per group)
 
 struct GemvArgs {
     const float* x;        // input vector [K] (device)

@@ -2374,7 +2374,18 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
     return hipSuccess;
 }
 
-static int gemv_rb(int rows) { return rows >= 4096 && rows % 8 == 0 ? 8 : 4; }
+int g_gemv_rb = 0;  // tools/kbench knob: force 4- or 8-row groups (0 = automatic)
+// Rows per group: each block should stream at least two groups, so that the next group's
+// loads overlap this group's reduction and epilogue (one group per block left every block
+// idle at its tail).  tools/kbench, bf16 / 768 blocks: QKV 10.2 -> 8.5 us with 4-row
+// groups, W1|W3 20.5 -> 20.0, W2 12.1 -> 11.4 and wo 6.7 -> 6.4 with 2-row groups; the LM
+// head (16 groups per block at 8 rows) keeps 8.
+static int gemv_rb(int rows) {
+    if (g_gemv_rb && rows % g_gemv_rb == 0) return g_gemv_rb;
+    if (rows >= 65536 && rows % 8 == 0) return 8;
+    if (rows >= 6144 && rows % 4 == 0) return 4;
+    return 2;
+}
 
 int gemv_grid(int rows) {
     // the largest divisor of the group count that fits 4 blocks per CU: every block then
@@ -2425,6 +2436,7 @@ const void* gemv_kernel(int pro, int epi, const GemvArgs& a) {
 #define GEMV_FN(P, E)                                                                     \
     if (pro == P && epi == E)                                                             \
         return rb == 8 ? (a.wscale ? gemv_fn<P, E, 8, 1>(kq) : gemv_fn<P, E, 8, 0>(kq))   \
+             : rb == 2 ? (a.wscale ? gemv_fn<P, E, 2, 1>(kq) : gemv_fn<P, E, 2, 0>(kq))   \
                        : (a.wscale ? gemv_fn<P, E, 4, 1>(kq) : gemv_fn<P, E, 4, 0>(kq));
     GEMV_FN(PRO_NONE, EPI_STORE) GEMV_FN(PRO_NONE, EPI_RESID) GEMV_FN(PRO_NORM, EPI_QKV)
     GEMV_FN(PRO_NORM_ADA, EPI_SWIGLU) GEMV_FN(PRO_NORM, EPI_LOGITS) GEMV_FN(PRO_NORM, EPI_LOGITS_ALT)
@@ -2454,7 +2466,8 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     if (a.K % (a.wscale ? 16 : 8) || a.rows % rb) return hipErrorInvalidValue;
     const int grid = gemv_grid(a.rows);
 #define GEMV_CASE(P, E) \
-    if (pro == P && epi == E) return rb == 8 ? gemv_q<P, E, 8>(a, grid, st) : gemv_q<P, E, 4>(a, grid, st);
+    if (pro == P && epi == E)                                                            \
+        return rb == 8 ? gemv_q<P, E, 8>(a, grid, st) : rb == 2 ? gemv_q<P, E, 2>(a, grid, st) : gemv_q<P, E, 4>(a, grid, st);
     GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_QKV)
     GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS) GEMV_CASE(PRO_NORM, EPI_LOGITS_ALT)
 #undef GEMV_CASE

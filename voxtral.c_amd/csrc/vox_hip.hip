@@ -148,6 +148,7 @@ struct DecLayerD {
 struct DecFragD {
     uint8_t *wqkv, *wo, *w13, *w2;
 };
+static int frag_copy(uint8_t** dst, const uint8_t* src, int N, int K, int q8);
 
 struct vox_hip_model {
     vox_hip_config_t c;
@@ -165,6 +166,7 @@ struct vox_hip_model {
     int rope_positions;
     int rope_gen;                  // bumped when the tables are reallocated (graphs hold the pointer)
     std::vector<DecFragD> dfrag;   // fragment-major decoder matrices (empty until a batch exists)
+    std::vector<DecFragD> efrag;   // fragment-major encoder matrices (empty until a short chunk)
     uint8_t* lm_frag;              // fragment-major LM head (tied embeddings)
 };
 
@@ -416,6 +418,9 @@ extern "C" void vox_hip_model_free(vox_hip_model_t* m) {
     for (auto& F : m->dfrag) {
         dfree(F.wqkv); dfree(F.wo); dfree(F.w13); dfree(F.w2);
     }
+    for (auto& F : m->efrag) {
+        dfree(F.wqkv); dfree(F.wo); dfree(F.w13); dfree(F.w2);
+    }
     dfree(m->lm_frag);
     dfree(m->enc_norm); dfree(m->ad0); dfree(m->ad1); dfree(m->tok_emb); dfree(m->dec_norm);
     dfree(m->ad0_s); dfree(m->ad1_s); dfree(m->tok_emb_s);
@@ -467,6 +472,8 @@ struct vox_hip_stream {
     float *part_alt, *alts;  // stream_fill_alts partials / per-step records [tokens_cap][ALT_REC]
     float* gws;              // split-K GEMM partials (encoder / prefill / adapter)
     size_t gws_n;
+    uint16_t* exp_;          // skinny encoder: row planes [4][3][16][max K] (fragment order)
+    float* eslab;            // skinny encoder: split-K slabs [4][S][16][N]
     int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
     float alt_cutoff;
     int graph_alt;           // alt mode the step graphs were captured with
@@ -598,7 +605,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->tokens);
-    dfree(s->part_alt); dfree(s->alts); dfree(s->gws);
+    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
     for (hipEvent_t e : s->pev) hipEventDestroy(e);
@@ -859,6 +866,92 @@ extern "C" int vox_hip_mel_read(vox_hip_mel_t* m, int global_first, int n, float
 // Encoder: 32 layers on rows [0, n) of x (logical positions pos0..), in place.
 // voxtral_encoder.c:562-686.  rope: rows for these positions (table slice or per-call).
 // ---------------------------------------------------------------------------
+// Short encoder chunks (streaming -I: ~25 rows per 0.5 s) sit far below the MFMA ridge:
+// their projections run as skinny GEMMs over fragment-major encoder weights (k_skl, the
+// batched decoder's kernel: rows = up to 2 B fragments of 16, every weight byte streamed
+// once per row block) with the consumers fused (residual + bias + RMSNorm into planes,
+// SwiGLU into planes, bias into the QKV rows).  Longer chunks keep k_gemm2.
+static const int ENC_SKINNY_ROWS = 32;
+
+static int model_enc_frag(vox_hip_model_t* m) {
+    if (!m->efrag.empty()) return 0;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, EQ = c.enc_heads * c.enc_head_dim, EKV = c.enc_kv_heads * c.enc_head_dim;
+    const int EH = c.enc_hidden;
+    std::vector<DecFragD> F(c.enc_layers, DecFragD{});
+    for (int l = 0; l < c.enc_layers; l++) {
+        const EncLayerD& L = m->enc[l];
+        if (frag_copy(&F[l].wqkv, L.wqkv, EQ + 2 * EKV, ED, L.sqkv != nullptr) ||
+            frag_copy(&F[l].wo, L.wo, ED, EQ, L.so != nullptr) ||
+            frag_copy(&F[l].w13, L.w13, 2 * EH, ED, L.s13 != nullptr) ||
+            frag_copy(&F[l].w2, L.w2, ED, EH, L.s2 != nullptr)) {
+            for (auto& f : F) { dfree(f.wqkv); dfree(f.wo); dfree(f.w13); dfree(f.w2); }
+            return -1;
+        }
+    }
+    m->efrag.swap(F);
+    return 0;
+}
+
+static bool enc_skinny_ok(const vox_hip_config_t& c) {
+    const int ED = c.enc_dim, EQ = c.enc_heads * c.enc_head_dim, EKV = c.enc_kv_heads * c.enc_head_dim;
+    const int EH = c.enc_hidden;
+    return skl_splits(ED) && skl_splits(EQ) && skl_splits(EH) && ED % 64 == 0 && (EQ + 2 * EKV) % 64 == 0 &&
+           (2 * EH) % 64 == 0 && ED <= 8 * 512;
+}
+
+static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long long pos0, const float* rope) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, H = c.enc_heads, KVH = c.enc_kv_heads, hd = c.enc_head_dim;
+    const int EQ = H * hd, EKV = KVH * hd, EH = c.enc_hidden, NQKV = EQ + 2 * EKV;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = s->st;
+    if (model_enc_frag(m)) return -1;
+    if (!s->exp_) {
+        const int kmax = std::max(ED, std::max(EQ, EH));
+        const size_t slab = std::max(std::max((size_t)skl_splits(ED) * NQKV, (size_t)skl_splits(EQ) * ED),
+                                     std::max((size_t)skl_splits(ED) * 2 * EH, (size_t)skl_splits(EH) * ED));
+        CK(dalloc(&s->exp_, (size_t)2 * 3 * SK_ROWS * kmax));
+        CK(dalloc(&s->eslab, (size_t)2 * SK_ROWS * slab));
+    }
+    uint16_t* xp = s->exp_;
+    float* sl = s->eslab;
+    for (int l = 0; l < c.enc_layers; l++) {
+        const EncLayerD& L = m->enc[l];
+        const DecFragD& F = m->efrag[l];
+        float* Kc = s->ek + (size_t)l * s->ecap * EKV;
+        float* Vc = s->ev + (size_t)l * s->ecap * EKV;
+        // previous layer's w2 residual (+ bias) then RMSNorm -> planes (encoder.c:562-566, 680-684)
+        CK(launch_rmsnorm_fplanes(x, n, ED, L.attn_norm, nullptr, c.enc_eps, xp, l ? sl : nullptr,
+                                  l ? skl_splits(EH) : 0, st, l ? m->enc[l - 1].b2 : nullptr));
+        CK(launch_gemm_skl(xp, ED, F.wqkv, L.sqkv, NQKV, n, sl, st));
+        CK(launch_slabs_rows(sl, skl_splits(ED), n, NQKV, L.bqkv, s->qkv, NQKV, st));
+        CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
+        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
+                             s->gws, s->gws_n));
+        CK(launch_split_fplanes(s->att, n, EQ, xp, st));
+        CK(launch_gemm_skl(xp, EQ, F.wo, L.so, ED, n, sl, st));
+        // wo residual (+ bias) then the FFN RMSNorm -> planes (encoder.c:640-650)
+        CK(launch_rmsnorm_fplanes(x, n, ED, L.ffn_norm, nullptr, c.enc_eps, xp, sl, skl_splits(EQ), st, L.bo));
+        CK(launch_gemm_skl(xp, ED, F.w13, L.s13, 2 * EH, n, sl, st));
+        CK(launch_swiglu_fplanes(sl, skl_splits(ED), EH, n, xp, st));
+        CK(launch_gemm_skl(xp, EH, F.w2, L.s2, ED, n, sl, st));
+    }
+    CK(launch_resid_slabs(x, n, ED, sl, skl_splits(EH), m->enc[c.enc_layers - 1].b2, st));
+    CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, n, ED, c.enc_eps, st));
+    return 0;
+}
+
+static int enc_skinny_env() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VOX_HIP_ENC_SKINNY");
+        v = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return v;
+}
+
 static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0, const float* rope) {
     vox_hip_model_t* m = s->m;
     const vox_hip_config_t& c = m->c;
@@ -867,6 +960,7 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
     const float scale = 1.0f / sqrtf((float)hd);
     hipStream_t st = s->st;
     if (n > ENC_SUB) return set_err("encoder pass of %d rows > %d", n, ENC_SUB);
+    if (n <= ENC_SKINNY_ROWS && enc_skinny_env() && enc_skinny_ok(c)) return run_encoder_rows_skinny(s, x, n, pos0, rope);
     for (int l = 0; l < c.enc_layers; l++) {
         const EncLayerD& L = m->enc[l];
         float* Kc = s->ek + (size_t)l * s->ecap * EKV;

@@ -125,10 +125,16 @@ hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, 
 // Batched decode GEMMs for M <= 16 rows held as three bf16 planes xs[3][16][K] (hi/mid/lo =
 // the exact f32 rows) in MFMA fragment order; weights packed by launch_frag_pack.
 constexpr int SK_ROWS = 16;
+constexpr int SK_MAX_ROWS = 64;  // rows of one skinny launch: up to 4 row blocks of 16
+                                 // (planes [rb][3][16][K], slabs [rb][S][16][N])
 hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hipStream_t st);
 // RMSNorm (+ ada) of nb rows into planes; S > 0: x += the S split slabs of part first
 hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
-                                  uint16_t* xs, const float* part, int S, hipStream_t st);
+                                  uint16_t* xs, const float* part, int S, hipStream_t st, const float* bias = nullptr);
+// x[j] += the S slabs of row j (+ bias); out[j] = the S slabs of row j (+ bias)
+hipError_t launch_resid_slabs(float* x, int nb, int D, const float* part, int S, const float* bias, hipStream_t st);
+hipError_t launch_slabs_rows(const float* part, int S, int nb, int N, const float* bias, float* out, int ldo,
+                             hipStream_t st);
 hipError_t launch_split_fplanes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st);
 // silu(W1 x) * (W3 x) from the split W1|W3 slabs (N = 2H rows) into planes
 hipError_t launch_swiglu_fplanes(const float* part, int S, int H, int nb, uint16_t* xs, hipStream_t st);

@@ -105,11 +105,19 @@ __device__ __forceinline__ size_t frag_off(int j, int k) {  // element (row j, c
     return ((size_t)(b * 2 + ((r >> 3) & 1)) * 64 + (r >> 4) * 16 + j) * 8 + (r & 7);
 }
 
-// element (stream j, column n) of a split-K result: the S partial slabs summed in order
+// element (row j, column n) of a split-K result: the S partial slabs summed in order.  Rows
+// come in blocks of 16 (k_skl's B operand): row j's slabs are those of row block j / 16,
+// laid out [row block][S][16][N].
 __device__ __forceinline__ float psum(const float* __restrict__ part, int S, int N, int j, int n) {
+    part += (size_t)(j >> 4) * S * SK_ROWS * N;
+    j &= 15;
     float v = part[(size_t)j * N + n];
     for (int s = 1; s < S; s++) v += part[((size_t)s * SK_ROWS + j) * N + n];
     return v;
+}
+// element (row j, col k) of the fragment-major planes of a row set: plane p of row block j / 16
+__device__ __forceinline__ size_t frag_at(int j, int K, int p, int k) {
+    return ((size_t)(j >> 4) * 3 + p) * SK_ROWS * K + frag_off(j & 15, k);
 }
 
 // dot of 8 bf16 weights (one uint4) with 8 f32 activations
@@ -1781,9 +1789,16 @@ __global__ __launch_bounds__(256) void k_frag_pack(const uint8_t* __restrict__ s
 
 // residual of a split projection: x[j][n] += sum of its S slabs (k_skl), one element per thread
 __global__ __launch_bounds__(256) void k_resid_slabs(float* __restrict__ x, int D, const float* __restrict__ part,
-                                                     int S) {
+                                                     int S, const float* __restrict__ bias) {
     const int j = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
-    if (n < D) x[(size_t)j * D + n] += psum(part, S, D, j, n);
+    if (n < D) x[(size_t)j * D + n] += bias ? psum(part, S, D, j, n) + bias[n] : psum(part, S, D, j, n);
+}
+
+// out[j][n] = the S slabs of row j + bias[n] (row-major result of a skinny projection)
+__global__ __launch_bounds__(256) void k_slabs_rows(const float* __restrict__ part, int S, int N,
+                                                    const float* __restrict__ bias, float* __restrict__ out, int ldo) {
+    const int j = blockIdx.y, n = blockIdx.x * 256 + threadIdx.x;
+    if (n < N) out[(size_t)j * ldo + n] = bias ? psum(part, S, N, j, n) + bias[n] : psum(part, S, N, j, n);
 }
 
 // RMSNorm (+ ada) of row blockIdx.y into fragment-major planes, columns chunk blockIdx.x of
@@ -1833,6 +1848,7 @@ __global__ __launch_bounds__(64) void k_rmsnorm_fplanes(const float* __restrict_
 // planes.  A thread owns 8 consecutive columns (D <= 8 * 512).
 __global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict__ x, int D,
                                                                const float* __restrict__ part, int S,
+                                                               const float* __restrict__ bias,
                                                                const float* __restrict__ w,
                                                                const float* __restrict__ ada, float eps,
                                                                uint16_t* __restrict__ xs) {
@@ -1848,12 +1864,17 @@ __global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
         if (S > 0) {
             float r[8];
+            const float* pb = part + (size_t)(j >> 4) * S * SK_ROWS * D;
             for (int s = 0; s < S; s++) {
-                const float* pp = part + ((size_t)s * SK_ROWS + j) * D + k;
+                const float* pp = pb + ((size_t)s * SK_ROWS + (j & 15)) * D + k;
                 const float4 c = *reinterpret_cast<const float4*>(pp), d = *reinterpret_cast<const float4*>(pp + 4);
                 const float t[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
 #pragma unroll
                 for (int e = 0; e < 8; e++) r[e] = s ? r[e] + t[e] : t[e];
+            }
+            if (bias) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) r[e] += bias[k + e];
             }
 #pragma unroll
             for (int e = 0; e < 8; e++) v[e] += r[e];
@@ -1886,10 +1907,9 @@ __global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict
         mp[e / 2] = m0 | ((uint32_t)m1 << 16);
         lq[e / 2] = l0 | ((uint32_t)l1 << 16);
     }
-    const size_t P = (size_t)SK_ROWS * D, o = frag_off(j, k);
-    *reinterpret_cast<uint4*>(xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
-    *reinterpret_cast<uint4*>(xs + P + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
-    *reinterpret_cast<uint4*>(xs + 2 * P + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+    *reinterpret_cast<uint4*>(xs + frag_at(j, D, 0, k)) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+    *reinterpret_cast<uint4*>(xs + frag_at(j, D, 1, k)) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+    *reinterpret_cast<uint4*>(xs + frag_at(j, D, 2, k)) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
 }
 
 // rows of x (f32) into fragment-major planes
@@ -1911,10 +1931,9 @@ __global__ __launch_bounds__(256) void k_split_fplanes(const float* __restrict__
         mp[e / 2] = m0 | ((uint32_t)m1 << 16);
         lp[e / 2] = l0 | ((uint32_t)l1 << 16);
     }
-    const size_t P = (size_t)SK_ROWS * K, o = frag_off(j, k);
-    *reinterpret_cast<uint4*>(xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
-    *reinterpret_cast<uint4*>(xs + P + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
-    *reinterpret_cast<uint4*>(xs + 2 * P + o) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
+    *reinterpret_cast<uint4*>(xs + frag_at(j, K, 0, k)) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+    *reinterpret_cast<uint4*>(xs + frag_at(j, K, 1, k)) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+    *reinterpret_cast<uint4*>(xs + frag_at(j, K, 2, k)) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
 }
 
 __device__ __forceinline__ bf16x8 i8x8_bf16(uint32_t lo, uint32_t hi) {
@@ -2062,6 +2081,10 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
     const int KB = K >> 6, s = blockIdx.y, kb0 = s * KS;
     const int g = blockIdx.x * NW + wave;
     const size_t P = (size_t)SK_ROWS * K;
+    // row block blockIdx.z: its planes and slabs ([rb][3][16][K], [rb][S][16][N])
+    xs += (size_t)blockIdx.z * 3 * P;
+    part += (size_t)blockIdx.z * gridDim.y * SK_ROWS * N;
+    nb -= blockIdx.z * SK_ROWS;
     // planes first: vmcnt retires in issue order, so the weights issued after them stay in
     // flight while the plane pieces are written to LDS
     uint4 f[NF];
@@ -2125,10 +2148,10 @@ __global__ __launch_bounds__(256) void k_swiglu_fplanes(const float* __restrict_
         const float gv = psum(part, S, N, j, rg + q), uv = psum(part, S, N, j, rg + 16 + q);
         split3(silu(gv) * uv, hh[q], mm[q], ll[q]);
     }
-    const size_t P = (size_t)SK_ROWS * H, o = frag_off(j, h0);  // h0 even: one 4-B piece
-    *reinterpret_cast<uint32_t*>(xs + o) = hh[0] | ((uint32_t)hh[1] << 16);
-    *reinterpret_cast<uint32_t*>(xs + P + o) = mm[0] | ((uint32_t)mm[1] << 16);
-    *reinterpret_cast<uint32_t*>(xs + 2 * P + o) = ll[0] | ((uint32_t)ll[1] << 16);
+    // h0 even: one 4-B piece per plane
+    *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 0, h0)) = hh[0] | ((uint32_t)hh[1] << 16);
+    *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 1, h0)) = mm[0] | ((uint32_t)mm[1] << 16);
+    *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 2, h0)) = ll[0] | ((uint32_t)ll[1] << 16);
 }
 
 // im2col for the causal conv stem (voxtral_kernels.c:430-447):
@@ -2613,15 +2636,16 @@ hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hi
 }
 
 hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
-                                  uint16_t* xs, const float* part, int S, hipStream_t st) {
-    if (nb < 1 || nb > SK_ROWS || D % 64) return hipErrorInvalidValue;
+                                  uint16_t* xs, const float* part, int S, hipStream_t st, const float* bias) {
+    if (nb < 1 || nb > SK_MAX_ROWS || D % 64) return hipErrorInvalidValue;
     if (D <= 8 * 512) {
-        hipLaunchKernelGGL(k_resid_rmsnorm_fplanes, dim3(nb), dim3(512), 0, st, x, D, part, S, w, ada, eps, xs);
+        hipLaunchKernelGGL(k_resid_rmsnorm_fplanes, dim3(nb), dim3(512), 0, st, x, D, part, S, bias, w, ada, eps, xs);
         LAUNCH_CHECK();
         return hipSuccess;
     }
+    if (nb > SK_ROWS) return hipErrorInvalidValue;
     if (S > 0) {
-        hipLaunchKernelGGL(k_resid_slabs, dim3((D + 255) / 256, nb), dim3(256), 0, st, x, D, part, S);
+        hipLaunchKernelGGL(k_resid_slabs, dim3((D + 255) / 256, nb), dim3(256), 0, st, x, D, part, S, bias);
         LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_rmsnorm_fplanes, dim3((D / 8 + 63) / 64, nb), dim3(64), 0, st, x, D, w, ada, eps, xs);
@@ -2629,15 +2653,30 @@ hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const
     return hipSuccess;
 }
 
+hipError_t launch_resid_slabs(float* x, int nb, int D, const float* part, int S, const float* bias, hipStream_t st) {
+    if (nb < 1 || nb > SK_MAX_ROWS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_resid_slabs, dim3((D + 255) / 256, nb), dim3(256), 0, st, x, D, part, S, bias);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_slabs_rows(const float* part, int S, int nb, int N, const float* bias, float* out, int ldo,
+                             hipStream_t st) {
+    if (nb < 1 || nb > SK_MAX_ROWS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_slabs_rows, dim3((N + 255) / 256, nb), dim3(256), 0, st, part, S, N, bias, out, ldo);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t launch_split_fplanes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st) {
-    if (nb < 1 || nb > SK_ROWS || K % 64) return hipErrorInvalidValue;
+    if (nb < 1 || nb > SK_MAX_ROWS || K % 64) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_split_fplanes, dim3((K / 8 + 255) / 256, nb), dim3(256), 0, st, x, K, xs);
     LAUNCH_CHECK();
     return hipSuccess;
 }
 
 hipError_t launch_swiglu_fplanes(const float* part, int S, int H, int nb, uint16_t* xs, hipStream_t st) {
-    if (nb < 1 || nb > SK_ROWS || H % 64) return hipErrorInvalidValue;
+    if (nb < 1 || nb > SK_MAX_ROWS || H % 64) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_swiglu_fplanes, dim3((H / 2 + 255) / 256, nb), dim3(256), 0, st, part, S, H, xs);
     LAUNCH_CHECK();
     return hipSuccess;
@@ -2682,8 +2721,8 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
 template <int Q, int NW, int KS>
 static hipError_t skl_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
                              float* part, hipStream_t st) {
-    hipLaunchKernelGGL((k_skl<Q, NW, KS>), dim3(N / (16 * NW), K / (64 * KS)), dim3(NW * 64), 0, st, xs, K,
-                       static_cast<const uint8_t*>(W), wscale, N, nb, part);
+    hipLaunchKernelGGL((k_skl<Q, NW, KS>), dim3(N / (16 * NW), K / (64 * KS), (nb + SK_ROWS - 1) / SK_ROWS),
+                       dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W), wscale, N, nb, part);
     return hipGetLastError();
 }
 
@@ -2695,7 +2734,7 @@ int skl_splits(int K) {
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
                            float* part, hipStream_t st) {
     const int S = skl_splits(K);
-    if (nb < 1 || nb > SK_ROWS || K % 64 || !S) return hipErrorInvalidValue;
+    if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S) return hipErrorInvalidValue;
     const int ks = K / 64 / S;
     // waves (row groups) per block: 4, or 8 when that still gives >= 256 blocks
     int nw = g_skl_nw ? g_skl_nw : ((N / 128) * S >= 256 && N % 128 == 0 ? 8 : 4);

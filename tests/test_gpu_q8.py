@@ -112,3 +112,41 @@ def test_q8_full_jfk_transcription(jfk_samples):
     os_.close()
     hm.close()
     om.close()
+
+
+def test_q8_streaming_skinny_encoder_and_batch(q8_models, tiny_cfg, jfk_samples):
+    """Q8 through the short-chunk paths: raw samples at -I 0.5 (device mel, 25-row encoder
+    chunks on the skinny int8 GEMMs) against the oracle's q8 path, then the same streams
+    decoded as one batch (int8 fragment-major weights) against single-stream decoding."""
+    import vox_hip
+    import vox_oracle
+    _, hm, om = q8_models
+    hs = vox_hip.Stream(hm)
+    sess = vox_hip.AudioSession(hs, interval_s=0.5)
+    for i in range(0, len(jfk_samples), 8000):
+        sess.feed_samples(jfk_samples[i:i + 8000], stop_at_eos=False)
+    sess.finish_samples(stop_at_eos=False)
+    os_ = vox_oracle.OracleStream(om)
+    osess = vox_oracle.OracleSession(os_, interval_s=0.5)
+    for kind, mel in vox_oracle.transcribe_mel_schedule(jfk_samples, feed_size=8000):
+        getattr(osess, kind)(mel, stop_at_eos=False)
+    ha, oa = hs.read_adapter(), os_.read_adapter()
+    assert ha.shape == oa.shape and rel(ha, oa) < TOL, rel(ha, oa)
+    assert sess.tokens == osess.tokens and len(sess.tokens) > 100
+    sess.close(); hs.close(); os_.close()
+    # batch: 3 streams at different lengths, decoded together, vs each alone
+    rng = np.random.default_rng(21)
+    mels = [rng.uniform(-0.6, 1.4, size=(n, tiny_cfg.mel_bins)).astype(np.float32) for n in (420, 500, 460)]
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 4)
+    got = b.decode(ss, max_steps=1000, stop_at_eos=False)
+    for i, mel in enumerate(mels):
+        one = vox_hip.Stream(hm)
+        one.encode_mel(mel)
+        assert got[i].tolist() == one.decode(stop_at_eos=False).tolist(), i
+        one.close()
+    for s in ss:
+        s.close()
+    b.close()

@@ -1,0 +1,70 @@
+/*
+ * vox_hip_host.h -- C host side of the MI355X backend: the reference's model loading and
+ * streaming API (voxtral.h:251-337, voxtral.c) rewritten over the C ABI of
+ * voxtral_hip.h, in the reference's own language (C99).  A C program that used
+ * vox_load / vox_stream_init / vox_stream_feed / vox_stream_finish / vox_stream_get can
+ * switch to the vh_* calls one for one; everything between the samples and the token ids
+ * (log-mel, conv stem, encoder, adapter, decoder, argmax) runs on the GPU.
+ *
+ * Differences from the reference API:
+ *   - vh_stream_get returns token ids (every generated id, control ids included); the
+ *     tokenizer (voxtral_tokenizer.c) stays out of scope;
+ *   - WAV input must be 16 kHz mono 16-bit PCM (the reference's loader also converts
+ *     other formats, voxtral_audio.c:49-165);
+ *   - continuous (live) mode restarts and alternatives are not wired here (the C ABI has
+ *     vox_hip_stream_reset_decoder and vox_hip_stream_set_alt for them).
+ */
+#ifndef VOX_HIP_HOST_H
+#define VOX_HIP_HOST_H
+
+#include "voxtral_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vh_ctx vh_ctx_t;       /* vox_ctx_t twin: one model on one GPU */
+typedef struct vh_stream vh_stream_t; /* vox_stream_t twin */
+
+/* Read a consolidated.safetensors header (BF16, or the Q8/F32 layout quantize.py writes)
+ * and derive the model dimensions from the tensor shapes, with the reference's fixed
+ * constants for what the file does not hold (head dims 64 / 128, windows 750 / 8192,
+ * theta 1e6, eps 1e-5; voxtral.h:26-50).  No GPU work.  0 on success. */
+int vh_inspect(const char *path, vox_hip_config_t *cfg);
+
+/* vox_load (voxtral.c:131-284): mmap the checkpoint, convert the small tensors to f32 as
+ * the reference does, hand the weight table to vox_hip_model_create (which uploads and
+ * packs everything into HBM), unmap.  NULL on failure (vh_last_error). */
+vh_ctx_t *vh_load(const char *path);
+void vh_free(vh_ctx_t *ctx);
+const vox_hip_config_t *vh_config(const vh_ctx_t *ctx);
+/* vox_set_delay (voxtral.c:1681-1687): clamp to 80..2400 ms, 80 ms per token */
+int vh_set_delay(vh_ctx_t *ctx, int delay_ms);
+const char *vh_last_error(void);
+
+/* vox_stream_init (voxtral.c:1242-1286) */
+vh_stream_t *vh_stream_init(vh_ctx_t *ctx);
+void vh_stream_free(vh_stream_t *s);
+/* vox_set_processing_interval (voxtral.c:1669-1675) */
+void vh_set_processing_interval(vh_stream_t *s, float seconds);
+/* vox_stream_feed / vox_stream_flush / vox_stream_finish (voxtral.c:1288-1316,
+ * 1640-1667): 0 on success, -1 on error or after finish */
+int vh_stream_feed(vh_stream_t *s, const float *samples, int n_samples);
+int vh_stream_flush(vh_stream_t *s);
+int vh_stream_finish(vh_stream_t *s);
+/* vox_stream_get (voxtral.c:1319-1327), ids instead of strings: up to max queued ids */
+int vh_stream_get(vh_stream_t *s, int *ids, int max);
+/* the stats vox_stream_free prints (voxtral.c:1358-1370) */
+typedef struct {
+    int mel_frames, adapter_tokens, generated, chunks;
+    double encoder_ms, decoder_ms, prefill_ms;
+} vh_stats_t;
+void vh_stream_stats(const vh_stream_t *s, vh_stats_t *out);
+
+/* vox_load_wav (voxtral_audio.c:143-166) for 16 kHz mono 16-bit PCM: malloc'd samples */
+float *vh_load_wav(const char *path, int *n_samples);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

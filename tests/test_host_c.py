@@ -1,0 +1,94 @@
+"""The C host side (include/vox_hip_host.h, voxtral.c_amd/host/): the reference's loader and
+streaming API in C99 over the C ABI, and the main.c-style CLI.
+
+CPU: the safetensors header parser derives the model dimensions from a checkpoint written by
+vox_weights.write_safetensors (bf16 and the quantize.py Q8 layout), and the WAV reader
+returns the samples the oracle's reader does.  GPU: the CLI transcribes jfk.wav from a
+TINY_LONG checkpoint file with the ids of the Python AudioSession and of the CPU oracle."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+PKG = os.path.join(ROOT, "voxtral.c_amd")
+HOSTLIB = os.path.join(PKG, "libvox_hip_host.so")
+CLI = os.path.join(PKG, "vox_hip_transcribe")
+
+
+@pytest.fixture(scope="module")
+def ckpt(tmp_path_factory, tiny_weights):
+    from vox_weights import write_safetensors
+    d = tmp_path_factory.mktemp("ckpt")
+    path = str(d / "consolidated.safetensors")
+    write_safetensors(tiny_weights, path)
+    return path
+
+
+def _host():
+    import vox_hip
+    L = ctypes.CDLL(HOSTLIB)
+    L.vh_inspect.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    L.vh_load_wav.restype = ctypes.POINTER(ctypes.c_float)
+    L.vh_load_wav.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    return L, vox_hip.ConfigC
+
+
+@pytest.mark.cpu
+@pytest.mark.parametrize("q8", [False, True])
+def test_inspect_derives_the_config(ckpt, tiny_weights, tmp_path, q8):
+    from vox_weights import TINY_LONG, quantize_q8, write_safetensors
+    path = ckpt
+    if q8:
+        path = str(tmp_path / "q8.safetensors")
+        write_safetensors(quantize_q8(tiny_weights), path)
+    L, ConfigC = _host()
+    c = ConfigC()
+    assert L.vh_inspect(path.encode(), ctypes.byref(c)) == 0
+    want = TINY_LONG.ctypes_struct(ConfigC)
+    for name, _ in ConfigC._fields_:
+        assert getattr(c, name) == pytest.approx(getattr(want, name)), name
+
+
+@pytest.mark.cpu
+def test_wav_reader_matches(jfk_samples):
+    L, _ = _host()
+    n = ctypes.c_int(0)
+    p = L.vh_load_wav(os.path.join(GOLDEN, "jfk.wav").encode(), ctypes.byref(n))
+    got = np.ctypeslib.as_array(p, (n.value,)).copy()
+    assert np.array_equal(got, jfk_samples)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("interval", [None, 0.5])
+def test_cli_transcribes_like_python_and_oracle(ckpt, tiny_weights, jfk_samples, interval):
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    cmd = [CLI, "-d", ckpt, "-i", os.path.join(GOLDEN, "jfk.wav")]
+    if interval:
+        cmd += ["-I", str(interval)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    ids = [int(t) for t in r.stdout.split()]
+    assert "Encoder:" in r.stderr and "Decoder:" in r.stderr and "Audio: 176000 samples" in r.stderr
+    # the same schedule through the Python mirror and the CPU oracle (EOS stops both)
+    piece = int(min(interval or 1.0, 1.0) * 16000)
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    hs = vox_hip.Stream(hm)
+    sess = vox_hip.AudioSession(hs, interval_s=interval or 2.0)
+    for i in range(0, len(jfk_samples), piece):
+        sess.feed_samples(jfk_samples[i:i + piece])
+    sess.finish_samples()
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    os_ = vox_oracle.OracleStream(om)
+    osess = vox_oracle.OracleSession(os_, interval_s=interval or 2.0)
+    for kind, mel in vox_oracle.transcribe_mel_schedule(jfk_samples, feed_size=piece):
+        getattr(osess, kind)(mel)
+    assert len(ids) > 0
+    assert ids == sess.tokens == osess.tokens
+    sess.close()
+    hs.close(); hm.close(); os_.close(); om.close()

@@ -1,0 +1,774 @@
+/*
+ * vox_hip_host.c -- the reference's loader and streaming driver in C99 over the MI355X C
+ * ABI (include/voxtral_hip.h).  See include/vox_hip_host.h.
+ *
+ * Model load: voxtral.c:131-284 + voxtral_safetensors.c (header parse, bf16 / Q8 / F32
+ * tensors).  Streaming: stream_run_encoder gating (voxtral.c:827-851), stream_run_decoder
+ * draining (1013-1145, non-continuous), vox_stream_feed / flush / finish (1288-1316,
+ * 1640-1667).  The mel front-end, encoder and decoder all run on the device
+ * (vox_hip_mel_*, vox_hip_stream_encode_mel, vox_hip_stream_decode).
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "../../include/vox_hip_host.h"
+
+#include <fcntl.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#define STREAM_FIRST_CHUNK_MIN_MEL 312  /* voxtral.c:405 */
+#define STREAM_DEFAULT_INTERVAL 2.0f    /* voxtral.c:408 */
+#define RAW_AUDIO_LENGTH_PER_TOK 1280   /* voxtral.c:400 */
+#define OFFLINE_STREAMING_BUFFER_TOKENS 10 /* voxtral.c:401 */
+#define ENC_PREFIX "mm_streams_embeddings.embedding_module.whisper_encoder"
+#define EMB_PREFIX "mm_streams_embeddings.embedding_module"
+
+static char g_err[512];
+
+static int fail(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "vox_hip_host: %s\n", g_err);
+    return -1;
+}
+
+const char *vh_last_error(void) { return g_err; }
+
+static double now_ms(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec / 1e6;
+}
+
+/* ------------------------------------------------------------------------
+ * safetensors: 8-byte little-endian header length, JSON object
+ * {name: {"dtype": s, "shape": [..], "data_offsets": [begin, end]}, "__metadata__": {..}}
+ * ------------------------------------------------------------------------ */
+enum { DT_BF16, DT_F32, DT_Q8, DT_OTHER };
+typedef struct {
+    char name[160];
+    int dtype, ndim;
+    long long shape[4];
+    size_t begin, end;
+} st_tensor_t;
+
+typedef struct {
+    int fd;
+    uint8_t *map;
+    size_t size, base;
+    st_tensor_t *t;
+    int n;
+} st_file_t;
+
+static void ws(const char **p) {
+    while (**p == ' ' || **p == '\n' || **p == '\r' || **p == '\t') (*p)++;
+}
+
+/* a JSON string into buf (no escapes occur in tensor names or dtypes) */
+static int jstr(const char **p, char *buf, size_t cap) {
+    ws(p);
+    if (**p != '"') return -1;
+    (*p)++;
+    size_t n = 0;
+    while (**p && **p != '"') {
+        if (**p == '\\' && (*p)[1]) (*p)++;
+        if (n + 1 < cap) buf[n++] = **p;
+        (*p)++;
+    }
+    if (**p != '"') return -1;
+    (*p)++;
+    buf[n] = 0;
+    return 0;
+}
+
+static int jskip(const char **p);
+
+static int jskip_container(const char **p, char open, char close) {
+    if (**p != open) return -1;
+    (*p)++;
+    ws(p);
+    if (**p == close) {
+        (*p)++;
+        return 0;
+    }
+    for (;;) {
+        if (open == '{') {
+            char k[256];
+            if (jstr(p, k, sizeof k)) return -1;
+            ws(p);
+            if (**p != ':') return -1;
+            (*p)++;
+        }
+        if (jskip(p)) return -1;
+        ws(p);
+        if (**p == ',') {
+            (*p)++;
+            continue;
+        }
+        if (**p == close) {
+            (*p)++;
+            return 0;
+        }
+        return -1;
+    }
+}
+
+static int jskip(const char **p) {
+    ws(p);
+    if (**p == '{') return jskip_container(p, '{', '}');
+    if (**p == '[') return jskip_container(p, '[', ']');
+    if (**p == '"') {
+        char tmp[512];
+        return jstr(p, tmp, sizeof tmp);
+    }
+    while (**p && **p != ',' && **p != '}' && **p != ']') (*p)++;
+    return 0;
+}
+
+static int jints(const char **p, long long *out, int cap) {
+    ws(p);
+    if (**p != '[') return -1;
+    (*p)++;
+    int n = 0;
+    for (;;) {
+        ws(p);
+        if (**p == ']') {
+            (*p)++;
+            return n;
+        }
+        char *e;
+        long long v = strtoll(*p, &e, 10);
+        if (e == *p) return -1;
+        if (n < cap) out[n] = v;
+        n++;
+        *p = e;
+        ws(p);
+        if (**p == ',') (*p)++;
+    }
+}
+
+static void st_close(st_file_t *f) {
+    if (f->map && f->map != MAP_FAILED) munmap(f->map, f->size);
+    if (f->fd >= 0) close(f->fd);
+    free(f->t);
+    memset(f, 0, sizeof *f);
+    f->fd = -1;
+}
+
+static int st_open(st_file_t *f, const char *path) {
+    memset(f, 0, sizeof *f);
+    f->fd = open(path, O_RDONLY);
+    if (f->fd < 0) return fail("cannot open %s", path);
+    struct stat sb;
+    if (fstat(f->fd, &sb) || sb.st_size < 16) return fail("%s: not a safetensors file", path);
+    f->size = (size_t)sb.st_size;
+    f->map = mmap(NULL, f->size, PROT_READ, MAP_PRIVATE, f->fd, 0);
+    if (f->map == MAP_FAILED) return fail("%s: mmap failed", path);
+    uint64_t hl = 0;
+    memcpy(&hl, f->map, 8);
+    if (hl + 8 > f->size) return fail("%s: bad header length", path);
+    char *hdr = malloc(hl + 1);
+    memcpy(hdr, f->map + 8, hl);
+    hdr[hl] = 0;
+    f->base = 8 + hl;
+    int cap = 1024;
+    f->t = calloc(cap, sizeof *f->t);
+    const char *p = hdr;
+    int rc = -1;
+    ws(&p);
+    if (*p != '{') goto done;
+    p++;
+    for (;;) {
+        ws(&p);
+        if (*p == '}') {
+            rc = 0;
+            break;
+        }
+        char name[160];
+        if (jstr(&p, name, sizeof name)) goto done;
+        ws(&p);
+        if (*p != ':') goto done;
+        p++;
+        ws(&p);
+        if (!strcmp(name, "__metadata__")) {
+            if (jskip(&p)) goto done;
+        } else {
+            if (*p != '{') goto done;
+            p++;
+            if (f->n == cap) {
+                cap *= 2;
+                f->t = realloc(f->t, cap * sizeof *f->t);
+            }
+            st_tensor_t *t = &f->t[f->n];
+            memset(t, 0, sizeof *t);
+            snprintf(t->name, sizeof t->name, "%s", name);
+            for (;;) {
+                ws(&p);
+                if (*p == '}') {
+                    p++;
+                    break;
+                }
+                char key[64];
+                if (jstr(&p, key, sizeof key)) goto done;
+                ws(&p);
+                if (*p != ':') goto done;
+                p++;
+                if (!strcmp(key, "dtype")) {
+                    char dt[32];
+                    if (jstr(&p, dt, sizeof dt)) goto done;
+                    t->dtype = !strcmp(dt, "BF16") ? DT_BF16 : !strcmp(dt, "F32") ? DT_F32 : !strcmp(dt, "Q8") ? DT_Q8 : DT_OTHER;
+                } else if (!strcmp(key, "shape")) {
+                    t->ndim = jints(&p, t->shape, 4);
+                    if (t->ndim < 0 || t->ndim > 4) goto done;
+                } else if (!strcmp(key, "data_offsets")) {
+                    long long o[2];
+                    if (jints(&p, o, 2) != 2) goto done;
+                    t->begin = (size_t)o[0];
+                    t->end = (size_t)o[1];
+                } else if (jskip(&p)) {
+                    goto done;
+                }
+                ws(&p);
+                if (*p == ',') p++;
+            }
+            if (f->base + t->end > f->size || t->end < t->begin) goto done;
+            f->n++;
+        }
+        ws(&p);
+        if (*p == ',') p++;
+    }
+done:
+    free(hdr);
+    if (rc) return fail("%s: malformed safetensors header", path);
+    return 0;
+}
+
+static const st_tensor_t *st_find(const st_file_t *f, const char *name) {
+    for (int i = 0; i < f->n; i++)
+        if (!strcmp(f->t[i].name, name)) return &f->t[i];
+    return NULL;
+}
+
+static long long st_numel(const st_tensor_t *t) {
+    long long n = 1;
+    for (int i = 0; i < t->ndim; i++) n *= t->shape[i];
+    return n;
+}
+
+/* ------------------------------------------------------------------------
+ * Model dimensions from the shapes (voxtral.h:26-50 constants for the rest)
+ * ------------------------------------------------------------------------ */
+static int count_layers(const st_file_t *f, const char *fmt) {
+    char nm[200];
+    int n = 0;
+    for (;;) {
+        snprintf(nm, sizeof nm, fmt, n);
+        if (!st_find(f, nm)) return n;
+        n++;
+    }
+}
+
+static int infer_config(const st_file_t *f, vox_hip_config_t *c) {
+    memset(c, 0, sizeof *c);
+    const st_tensor_t *conv0 = st_find(f, ENC_PREFIX ".conv_layers.0.conv.weight");
+    const st_tensor_t *ewq = st_find(f, ENC_PREFIX ".transformer.layers.0.attention.wq.weight");
+    const st_tensor_t *ewk = st_find(f, ENC_PREFIX ".transformer.layers.0.attention.wk.weight");
+    const st_tensor_t *ew1 = st_find(f, ENC_PREFIX ".transformer.layers.0.feed_forward.w1.weight");
+    const st_tensor_t *ad0 = st_find(f, EMB_PREFIX ".audio_language_projection.0.weight");
+    const st_tensor_t *emb = st_find(f, EMB_PREFIX ".tok_embeddings.weight");
+    const st_tensor_t *dwq = st_find(f, "layers.0.attention.wq.weight");
+    const st_tensor_t *dwk = st_find(f, "layers.0.attention.wk.weight");
+    const st_tensor_t *dw1 = st_find(f, "layers.0.feed_forward.w1.weight");
+    const st_tensor_t *ada = st_find(f, "layers.0.ada_rms_norm_t_cond.0.weight");
+    if (!conv0 || !ewq || !ewk || !ew1 || !ad0 || !emb || !dwq || !dwk || !dw1 || !ada || conv0->ndim != 3)
+        return fail("checkpoint lacks the Voxtral tensors (voxtral_safetensors.c names)");
+    c->enc_dim = (int)conv0->shape[0];
+    c->mel_bins = (int)conv0->shape[1];
+    c->enc_layers = count_layers(f, ENC_PREFIX ".transformer.layers.%d.attention.wq.weight");
+    c->enc_head_dim = 64;                      /* VOX_ENC_HEAD_DIM */
+    c->enc_heads = (int)ewq->shape[0] / 64;
+    c->enc_kv_heads = (int)ewk->shape[0] / 64;
+    c->enc_hidden = (int)ew1->shape[0];
+    c->enc_window = 750;                       /* VOX_ENC_WINDOW */
+    c->downsample = (int)(ad0->shape[1] / c->enc_dim);
+    c->dec_dim = (int)emb->shape[1];
+    c->vocab = (int)emb->shape[0];
+    c->dec_layers = count_layers(f, "layers.%d.attention.wq.weight");
+    c->dec_head_dim = 128;                     /* VOX_DEC_HEAD_DIM */
+    c->dec_heads = (int)dwq->shape[0] / 128;
+    c->dec_kv_heads = (int)dwk->shape[0] / 128;
+    c->dec_hidden = (int)dw1->shape[0];
+    c->dec_window = 8192;                      /* VOX_DEC_WINDOW */
+    c->ada_dim = (int)ada->shape[0];
+    c->rope_theta = 1e6f;
+    c->enc_eps = 1e-5f;
+    c->dec_eps = 1e-5f;
+    c->gelu_erf = 0;
+    return 0;
+}
+
+int vh_inspect(const char *path, vox_hip_config_t *cfg) {
+    st_file_t f;
+    if (st_open(&f, path)) {
+        st_close(&f);
+        return -1;
+    }
+    int rc = infer_config(&f, cfg);
+    st_close(&f);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------
+ * Weight table (voxtral.c:131-284): matrices straight off the mapping (bf16), or int8
+ * data + copied f32 row scales (Q8, quantize.py packs them unaligned); small tensors as f32
+ * ------------------------------------------------------------------------ */
+typedef struct {
+    void **allocs;
+    int n, cap;
+} arena_t;
+
+static void *arena_add(arena_t *a, void *p) {
+    if (!p) return NULL;
+    if (a->n == a->cap) {
+        a->cap = a->cap ? 2 * a->cap : 256;
+        a->allocs = realloc(a->allocs, a->cap * sizeof(void *));
+    }
+    a->allocs[a->n++] = p;
+    return p;
+}
+
+static void arena_free(arena_t *a) {
+    for (int i = 0; i < a->n; i++) free(a->allocs[i]);
+    free(a->allocs);
+    memset(a, 0, sizeof *a);
+}
+
+typedef struct {
+    const st_file_t *f;
+    arena_t *a;
+    int bad;
+} loader_t;
+
+/* tensor as f32 (bf16 widened exactly, Q8 dequantised as safetensors_get_f32 does) */
+static const float *load_f32(loader_t *L, const char *name) {
+    const st_tensor_t *t = st_find(L->f, name);
+    if (!t) {
+        L->bad = fail("missing tensor %s", name);
+        return NULL;
+    }
+    const uint8_t *src = L->f->map + L->f->base + t->begin;
+    const long long n = st_numel(t);
+    float *out = arena_add(L->a, malloc((size_t)n * 4));
+    if (t->dtype == DT_F32) {
+        memcpy(out, src, (size_t)n * 4);
+    } else if (t->dtype == DT_BF16) {
+        for (long long i = 0; i < n; i++) {
+            uint16_t b;
+            memcpy(&b, src + 2 * i, 2);
+            uint32_t u = (uint32_t)b << 16;
+            memcpy(&out[i], &u, 4);
+        }
+    } else if (t->dtype == DT_Q8 && t->ndim == 2) {
+        const long long rows = t->shape[0], cols = t->shape[1];
+        for (long long r = 0; r < rows; r++) {
+            float sc;
+            memcpy(&sc, src + 4 * r, 4);
+            const int8_t *q = (const int8_t *)(src + rows * 4 + r * cols);
+            for (long long k = 0; k < cols; k++) out[r * cols + k] = (float)q[k] * sc;
+        }
+    } else {
+        L->bad = fail("%s: unsupported dtype", name);
+        return NULL;
+    }
+    return out;
+}
+
+/* matrix: bf16 data pointer, or int8 data with its row scales (*scales set) */
+static const uint16_t *load_mat(loader_t *L, const char *name, const float **scales) {
+    const st_tensor_t *t = st_find(L->f, name);
+    *scales = NULL;
+    if (!t || t->ndim != 2) {
+        L->bad = fail("missing matrix %s", name);
+        return NULL;
+    }
+    const uint8_t *src = L->f->map + L->f->base + t->begin;
+    if (t->dtype == DT_BF16) return (const uint16_t *)src;
+    if (t->dtype == DT_Q8) {
+        const long long rows = t->shape[0];
+        float *sc = arena_add(L->a, malloc((size_t)rows * 4));
+        memcpy(sc, src, (size_t)rows * 4);
+        *scales = sc;
+        return (const uint16_t *)(src + rows * 4);
+    }
+    L->bad = fail("%s: matrices must be BF16 or Q8", name);
+    return NULL;
+}
+
+struct vh_ctx {
+    vox_hip_config_t cfg;
+    vox_hip_model_t *model;
+    int delay_tokens;
+};
+
+const vox_hip_config_t *vh_config(const vh_ctx_t *ctx) { return &ctx->cfg; }
+
+#define NAMEBUF 200
+
+vh_ctx_t *vh_load(const char *path) {
+    if (!vox_hip_init()) {
+        fail("no HIP device: %s", vox_hip_last_error());
+        return NULL;
+    }
+    st_file_t f;
+    if (st_open(&f, path)) {
+        st_close(&f);
+        return NULL;
+    }
+    vh_ctx_t *ctx = calloc(1, sizeof *ctx);
+    if (infer_config(&f, &ctx->cfg)) {
+        st_close(&f);
+        free(ctx);
+        return NULL;
+    }
+    const vox_hip_config_t *c = &ctx->cfg;
+    arena_t a = {0};
+    loader_t L = {&f, &a, 0};
+    vox_hip_weights_t w;
+    memset(&w, 0, sizeof w);
+    const int EL = c->enc_layers, DL = c->dec_layers;
+    char nm[NAMEBUF];
+    w.conv0_w = load_f32(&L, ENC_PREFIX ".conv_layers.0.conv.weight");
+    w.conv0_b = load_f32(&L, ENC_PREFIX ".conv_layers.0.conv.bias");
+    w.conv1_w = load_f32(&L, ENC_PREFIX ".conv_layers.1.conv.weight");
+    w.conv1_b = load_f32(&L, ENC_PREFIX ".conv_layers.1.conv.bias");
+#define PTRS(n) arena_add(&a, calloc((size_t)(n), sizeof(void *)))
+    /* per-layer matrices: data pointer array + scale array */
+    const char *enc_mats[7] = {"attention.wq.weight", "attention.wk.weight", "attention.wv.weight", "attention.wo.weight",
+                               "feed_forward.w1.weight", "feed_forward.w2.weight", "feed_forward.w3.weight"};
+    const uint16_t **ed[7];
+    const float **es[7];
+    for (int m = 0; m < 7; m++) {
+        ed[m] = PTRS(EL);
+        es[m] = PTRS(EL);
+        for (int l = 0; l < EL; l++) {
+            snprintf(nm, sizeof nm, ENC_PREFIX ".transformer.layers.%d.%s", l, enc_mats[m]);
+            ed[m][l] = load_mat(&L, nm, &es[m][l]);
+        }
+    }
+    const int q8 = es[0][0] != NULL;
+    w.enc_wq = ed[0]; w.enc_wk = ed[1]; w.enc_wv = ed[2]; w.enc_wo = ed[3];
+    w.enc_w1 = ed[4]; w.enc_w2 = ed[5]; w.enc_w3 = ed[6];
+    if (q8) {
+        w.enc_wq_s = es[0]; w.enc_wk_s = es[1]; w.enc_wv_s = es[2]; w.enc_wo_s = es[3];
+        w.enc_w1_s = es[4]; w.enc_w2_s = es[5]; w.enc_w3_s = es[6];
+    }
+    const char *enc_vecs[6] = {"attention.wq.bias", "attention.wv.bias", "attention.wo.bias",
+                               "feed_forward.w2.bias", "attention_norm.weight", "ffn_norm.weight"};
+    const float **ev[6];
+    for (int v = 0; v < 6; v++) {
+        ev[v] = PTRS(EL);
+        for (int l = 0; l < EL; l++) {
+            snprintf(nm, sizeof nm, ENC_PREFIX ".transformer.layers.%d.%s", l, enc_vecs[v]);
+            ev[v][l] = load_f32(&L, nm);
+        }
+    }
+    w.enc_wq_b = ev[0]; w.enc_wv_b = ev[1]; w.enc_wo_b = ev[2]; w.enc_w2_b = ev[3];
+    w.enc_attn_norm = ev[4]; w.enc_ffn_norm = ev[5];
+    w.enc_norm = load_f32(&L, ENC_PREFIX ".transformer.norm.weight");
+    w.ad0 = load_mat(&L, EMB_PREFIX ".audio_language_projection.0.weight", &w.ad0_s);
+    w.ad1 = load_mat(&L, EMB_PREFIX ".audio_language_projection.2.weight", &w.ad1_s);
+    w.tok_emb = load_mat(&L, EMB_PREFIX ".tok_embeddings.weight", &w.tok_emb_s);
+    const char *dec_mats[7] = {"attention.wq.weight", "attention.wk.weight", "attention.wv.weight", "attention.wo.weight",
+                               "feed_forward.w1.weight", "feed_forward.w2.weight", "feed_forward.w3.weight"};
+    const uint16_t **dd[7];
+    const float **dsc[7];
+    for (int m = 0; m < 7; m++) {
+        dd[m] = PTRS(DL);
+        dsc[m] = PTRS(DL);
+        for (int l = 0; l < DL; l++) {
+            snprintf(nm, sizeof nm, "layers.%d.%s", l, dec_mats[m]);
+            dd[m][l] = load_mat(&L, nm, &dsc[m][l]);
+        }
+    }
+    w.dec_wq = dd[0]; w.dec_wk = dd[1]; w.dec_wv = dd[2]; w.dec_wo = dd[3];
+    w.dec_w1 = dd[4]; w.dec_w2 = dd[5]; w.dec_w3 = dd[6];
+    if (q8) {
+        w.dec_wq_s = dsc[0]; w.dec_wk_s = dsc[1]; w.dec_wv_s = dsc[2]; w.dec_wo_s = dsc[3];
+        w.dec_w1_s = dsc[4]; w.dec_w2_s = dsc[5]; w.dec_w3_s = dsc[6];
+    }
+    const char *dec_vecs[4] = {"attention_norm.weight", "ffn_norm.weight", "ada_rms_norm_t_cond.0.weight",
+                               "ada_rms_norm_t_cond.2.weight"};
+    const float **dv[4];
+    for (int v = 0; v < 4; v++) {
+        dv[v] = PTRS(DL);
+        for (int l = 0; l < DL; l++) {
+            snprintf(nm, sizeof nm, "layers.%d.%s", l, dec_vecs[v]);
+            dv[v][l] = load_f32(&L, nm);
+        }
+    }
+    w.dec_attn_norm = dv[0]; w.dec_ffn_norm = dv[1]; w.dec_ada_down = dv[2]; w.dec_ada_up = dv[3];
+    w.dec_norm = load_f32(&L, "norm.weight");
+#undef PTRS
+    ctx->delay_tokens = 6;  /* default 480 ms (voxtral.c:136) */
+    if (!L.bad) {
+        ctx->model = vox_hip_model_create(c, &w, ctx->delay_tokens);
+        if (!ctx->model) fail("vox_hip_model_create: %s", vox_hip_last_error());
+    }
+    arena_free(&a);
+    st_close(&f);  /* every weight now lives in HBM */
+    if (!ctx->model) {
+        free(ctx);
+        return NULL;
+    }
+    return ctx;
+}
+
+void vh_free(vh_ctx_t *ctx) {
+    if (!ctx) return;
+    vox_hip_model_free(ctx->model);
+    free(ctx);
+}
+
+int vh_set_delay(vh_ctx_t *ctx, int delay_ms) {
+    if (delay_ms < 80) delay_ms = 80;
+    if (delay_ms > 2400) delay_ms = 2400;
+    ctx->delay_tokens = delay_ms / 80;
+    return vox_hip_model_set_delay(ctx->model, ctx->delay_tokens);
+}
+
+/* ------------------------------------------------------------------------
+ * Streaming (voxtral.c:827-851, 1013-1145, 1288-1316, 1640-1667)
+ * ------------------------------------------------------------------------ */
+struct vh_stream {
+    vh_ctx_t *ctx;
+    vox_hip_stream_t *st;
+    vox_hip_mel_t *mel;
+    int mel_cursor, conv_started, finished, min_new_mel;
+    long long real_samples;
+    int *queue;
+    int q_head, q_tail, q_cap;
+    int *dec_buf;
+    int generated, chunks, started_decoding;
+    double enc_ms, dec_ms, prefill_ms;
+};
+
+vh_stream_t *vh_stream_init(vh_ctx_t *ctx) {
+    vh_stream_t *s = calloc(1, sizeof *s);
+    s->ctx = ctx;
+    s->st = vox_hip_stream_create(ctx->model);
+    if (!s->st) {
+        fail("vox_hip_stream_create: %s", vox_hip_last_error());
+        free(s);
+        return NULL;
+    }
+    /* 32 left-pad tokens of silence (voxtral.c:1255) */
+    s->mel = vox_hip_mel_create(s->st, 32 * RAW_AUDIO_LENGTH_PER_TOK);
+    if (!s->mel) {
+        fail("vox_hip_mel_create: %s", vox_hip_last_error());
+        vox_hip_stream_free(s->st);
+        free(s);
+        return NULL;
+    }
+    s->min_new_mel = (int)(STREAM_DEFAULT_INTERVAL * 100.0f);
+    s->q_cap = 4096;
+    s->queue = malloc(sizeof(int) * s->q_cap);
+    s->dec_buf = malloc(sizeof(int) * 4096);
+    return s;
+}
+
+void vh_stream_free(vh_stream_t *s) {
+    if (!s) return;
+    vox_hip_mel_free(s->mel);
+    vox_hip_stream_free(s->st);
+    free(s->queue);
+    free(s->dec_buf);
+    free(s);
+}
+
+void vh_set_processing_interval(vh_stream_t *s, float seconds) {
+    if (seconds <= 0) seconds = 0;
+    s->min_new_mel = (int)(seconds * 100.0f);
+    if (s->min_new_mel < 1) s->min_new_mel = 1;
+}
+
+static void queue_push(vh_stream_t *s, const int *ids, int n) {
+    for (int i = 0; i < n; i++) {
+        const int next = (s->q_tail + 1) % s->q_cap;
+        if (next == s->q_head) {  /* full: grow (keeps order) */
+            int *nq = malloc(sizeof(int) * s->q_cap * 2);
+            int k = 0;
+            for (int j = s->q_head; j != s->q_tail; j = (j + 1) % s->q_cap) nq[k++] = s->queue[j];
+            free(s->queue);
+            s->queue = nq;
+            s->q_head = 0;
+            s->q_tail = k;
+            s->q_cap *= 2;
+        }
+        s->queue[s->q_tail] = ids[i];
+        s->q_tail = (s->q_tail + 1) % s->q_cap;
+    }
+}
+
+/* stream_run_encoder (voxtral.c:827-851) */
+static int run_encoder(vh_stream_t *s) {
+    int off = 0;
+    const int frames = vox_hip_mel_frames(s->mel, &off);
+    if (frames < 0) return fail("vox_hip_mel_frames failed");
+    const int total = off + frames;
+    if (s->mel_cursor < off) s->mel_cursor = off;
+    const int new_mel = total - s->mel_cursor;
+    const int need = s->conv_started ? s->min_new_mel : STREAM_FIRST_CHUNK_MIN_MEL;
+    if (new_mel < need && !s->finished) return 0;
+    if (new_mel <= 0) return 0;
+    const double t0 = now_ms();
+    const float *p = vox_hip_mel_frame_ptr(s->mel, s->mel_cursor);
+    if (!p || vox_hip_stream_encode_mel(s->st, p, new_mel, 1) < 0 || vox_hip_stream_sync(s->st))
+        return fail("encoder: %s", vox_hip_last_error());
+    s->enc_ms += now_ms() - t0;
+    s->conv_started = 1;
+    s->mel_cursor = total;
+    s->chunks++;
+    return vox_hip_mel_discard_before(s->mel, s->mel_cursor);
+}
+
+/* stream_run_decoder (voxtral.c:1013-1145), non-continuous: drain every adapter row;
+ * greedy decoding stops after EOS (token 2) */
+static int run_decoder(vh_stream_t *s) {
+    for (;;) {
+        const double t0 = now_ms();
+        const int first = !s->started_decoding;
+        /* the first call runs the prefill + first token alone, so its time is the
+         * reference's prefill_ms */
+        const int n = vox_hip_stream_decode(s->st, first ? 1 : 4096, 1, s->dec_buf, NULL);
+        if (n < 0) return fail("decoder: %s", vox_hip_last_error());
+        const double dt = now_ms() - t0;
+        if (n == 0) return 0;
+        if (first) {
+            s->prefill_ms += dt;
+            s->started_decoding = 1;
+        }
+        s->dec_ms += dt;
+        s->generated += n;
+        queue_push(s, s->dec_buf, n);
+    }
+}
+
+int vh_stream_feed(vh_stream_t *s, const float *samples, int n) {
+    if (!s || s->finished || n <= 0) return -1;
+    if (vox_hip_mel_feed(s->mel, samples, n) < 0) return fail("mel: %s", vox_hip_last_error());
+    s->real_samples += n;
+    if (run_encoder(s) || run_decoder(s)) return -1;
+    return 0;
+}
+
+int vh_stream_flush(vh_stream_t *s) {
+    if (!s || s->finished) return -1;
+    /* the right padding vox_stream_flush feeds (voxtral.c:1645-1656) */
+    const int align = (int)((RAW_AUDIO_LENGTH_PER_TOK - (s->real_samples % RAW_AUDIO_LENGTH_PER_TOK)) %
+                            RAW_AUDIO_LENGTH_PER_TOK);
+    const int pad = align + ((s->ctx->delay_tokens + 1) + OFFLINE_STREAMING_BUFFER_TOKENS) * RAW_AUDIO_LENGTH_PER_TOK;
+    float *zeros = calloc((size_t)pad, sizeof(float));
+    const int rc = vox_hip_mel_feed(s->mel, zeros, pad);
+    free(zeros);
+    if (rc < 0) return fail("mel: %s", vox_hip_last_error());
+    const int saved = s->min_new_mel;
+    s->min_new_mel = 1;
+    const int e = run_encoder(s) || run_decoder(s);
+    s->min_new_mel = saved;
+    return e ? -1 : 0;
+}
+
+int vh_stream_finish(vh_stream_t *s) {
+    if (!s || s->finished) return -1;
+    if (vh_stream_flush(s)) return -1;
+    s->finished = 1;
+    if (vox_hip_mel_finish(s->mel, 0) < 0) return fail("mel: %s", vox_hip_last_error());
+    if (run_encoder(s) || run_decoder(s)) return -1;
+    return 0;
+}
+
+int vh_stream_get(vh_stream_t *s, int *ids, int max) {
+    int n = 0;
+    while (n < max && s->q_head != s->q_tail) {
+        ids[n++] = s->queue[s->q_head];
+        s->q_head = (s->q_head + 1) % s->q_cap;
+    }
+    return n;
+}
+
+void vh_stream_stats(const vh_stream_t *s, vh_stats_t *o) {
+    memset(o, 0, sizeof *o);
+    o->mel_frames = s->mel_cursor;
+    o->adapter_tokens = vox_hip_stream_adapter_tokens(s->st);
+    o->generated = s->generated;
+    o->chunks = s->chunks;
+    o->encoder_ms = s->enc_ms;
+    o->decoder_ms = s->dec_ms;
+    o->prefill_ms = s->prefill_ms;
+}
+
+/* ------------------------------------------------------------------------
+ * WAV (voxtral_audio.c:49-166): RIFF / WAVE, "fmt " PCM 16-bit mono 16 kHz, "data"
+ * ------------------------------------------------------------------------ */
+float *vh_load_wav(const char *path, int *n_samples) {
+    FILE *fp = fopen(path, "rb");
+    if (!fp) {
+        fail("cannot open %s", path);
+        return NULL;
+    }
+    fseek(fp, 0, SEEK_END);
+    const long size = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    uint8_t *buf = malloc(size > 0 ? (size_t)size : 1);
+    const size_t got = size > 0 ? fread(buf, 1, (size_t)size, fp) : 0;
+    fclose(fp);
+    float *out = NULL;
+    if ((long)got != size) {
+        fail("%s: short read", path);
+        goto end;
+    }
+    if (size < 12 || memcmp(buf, "RIFF", 4) || memcmp(buf + 8, "WAVE", 4)) {
+        fail("%s: not a RIFF/WAVE file", path);
+        goto end;
+    }
+    int channels = 0, rate = 0, bits = 0, fmt = 0;
+    for (long p = 12; p + 8 <= size;) {
+        uint32_t len;
+        memcpy(&len, buf + p + 4, 4);
+        const uint8_t *d = buf + p + 8;
+        if (!memcmp(buf + p, "fmt ", 4) && len >= 16) {
+            fmt = d[0] | d[1] << 8;
+            channels = d[2] | d[3] << 8;
+            rate = d[4] | d[5] << 8 | d[6] << 16 | d[7] << 24;
+            bits = d[14] | d[15] << 8;
+        } else if (!memcmp(buf + p, "data", 4)) {
+            if (fmt != 1 || channels != 1 || rate != 16000 || bits != 16) {
+                fail("%s: need 16 kHz mono 16-bit PCM (fmt %d, %d ch, %d Hz, %d bit)", path, fmt, channels, rate, bits);
+                goto end;
+            }
+            if (p + 8 + (long)len > size) len = (uint32_t)(size - p - 8);
+            const int n = (int)(len / 2);
+            out = malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+            for (int i = 0; i < n; i++) {
+                int16_t v;
+                memcpy(&v, d + 2 * i, 2);
+                out[i] = v / 32768.0f;
+            }
+            *n_samples = n;
+            goto end;
+        }
+        p += 8 + len + (len & 1);
+    }
+    fail("%s: no data chunk", path);
+end:
+    free(buf);
+    return out;
+}

@@ -40,3 +40,13 @@ def test_library_is_gfx950_code_object():
     import vox_hip
     data = open(vox_hip.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_host_library_exports_vox_hip_host_h():
+    """libvox_hip_host.so (the C host side) exports every vh_* entry point its header declares."""
+    src = open(os.path.join(ROOT, "include", "vox_hip_host.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = sorted(set(re.findall(r"\b(vh_[a-z0-9_]+)\s*\(", src)))
+    assert len(names) >= 12
+    lib = ctypes.CDLL(os.path.join(ROOT, "voxtral.c_amd", "libvox_hip_host.so"))
+    assert not [n for n in names if not hasattr(lib, n)]

@@ -216,8 +216,8 @@ def main():
     avg_ms = prof["avg_ms"] if prof["launches"] else float("nan")
     achieved = w13_bytes / (avg_ms * 1e-3) / 1e9 if prof["launches"] else None
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_w13_traffic.json")
-    if os.path.exists(pmc):
+    pmc = os.path.join(ROOT, "profiles", "pmc_w13_traffic.json")  # bf16 W1|W3 (tools/pmc.sh)
+    if os.path.exists(pmc) and not args.q8:
         traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
 
     out = {

@@ -27,6 +27,7 @@ namespace vox {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 // streamed-once weights: non-temporal 16-B load (MI355X_MICROARCH.md row nt-weights)
@@ -654,23 +655,31 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
         __syncthreads();
         float s[4];
         float tmax = -INFINITY;
+        {
+            // the query slice is read once per 4 dims for all 4 keys (5 LDS reads per 16
+            // FMAs instead of 8), and the products run as packed f32 FMAs (v_pk_fma_f32)
+            f32x2 acc[4][2];
 #pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-            int key = j + 16 * jj;
-            int kp = kb + key;
-            bool valid = qvalid && kp <= qp && kp >= qp - window + 1 && kp >= k_first && kp <= kend;
-            float acc = 0.f;
+            for (int jj = 0; jj < 4; jj++) acc[jj][0] = acc[jj][1] = f32x2{0.f, 0.f};
 #pragma unroll 8
             for (int d = 0; d < HD; d += 4) {
-                float4 a = *reinterpret_cast<const float4*>(&sQ[qi][d]);
-                float4 b = *reinterpret_cast<const float4*>(&sK[key][d]);
-                acc = fmaf(a.x, b.x, acc);
-                acc = fmaf(a.y, b.y, acc);
-                acc = fmaf(a.z, b.z, acc);
-                acc = fmaf(a.w, b.w, acc);
+                const float4 a = *reinterpret_cast<const float4*>(&sQ[qi][d]);
+                const f32x2 alo = {a.x, a.y}, ahi = {a.z, a.w};
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    const float4 b = *reinterpret_cast<const float4*>(&sK[j + 16 * jj][d]);
+                    acc[jj][0] = __builtin_elementwise_fma(alo, f32x2{b.x, b.y}, acc[jj][0]);
+                    acc[jj][1] = __builtin_elementwise_fma(ahi, f32x2{b.z, b.w}, acc[jj][1]);
+                }
             }
-            s[jj] = valid ? acc * scale : -INFINITY;
-            tmax = fmaxf(tmax, s[jj]);
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const int kp = kb + j + 16 * jj;
+                const bool valid = qvalid && kp <= qp && kp >= qp - window + 1 && kp >= k_first && kp <= kend;
+                const float dot = (acc[jj][0].x + acc[jj][1].x) + (acc[jj][0].y + acc[jj][1].y);
+                s[jj] = valid ? dot * scale : -INFINITY;
+                tmax = fmaxf(tmax, s[jj]);
+            }
         }
 #pragma unroll
         for (int off = 8; off > 0; off >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, off, 16));
@@ -691,15 +700,20 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
 #pragma unroll
         for (int e = 0; e < DPT; e++) o[e] *= alpha;
         const int d0 = j * DPT;
-        for (int key = 0; key < KT; key++) {
-            float p = sP[qi][key];
+        for (int key = 0; key < KT; key += 4) {
+            const float4 p4 = *reinterpret_cast<const float4*>(&sP[qi][key]);
+            const float pk[4] = {p4.x, p4.y, p4.z, p4.w};
 #pragma unroll
-            for (int e = 0; e < DPT; e += 4) {
-                float4 v = *reinterpret_cast<const float4*>(&sV[key][d0 + e]);
-                o[e] = fmaf(p, v.x, o[e]);
-                o[e + 1] = fmaf(p, v.y, o[e + 1]);
-                o[e + 2] = fmaf(p, v.z, o[e + 2]);
-                o[e + 3] = fmaf(p, v.w, o[e + 3]);
+            for (int u = 0; u < 4; u++) {
+                const f32x2 pp = {pk[u], pk[u]};
+#pragma unroll
+                for (int e = 0; e < DPT; e += 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(&sV[key + u][d0 + e]);
+                    f32x2 lo = {o[e], o[e + 1]}, hi = {o[e + 2], o[e + 3]};
+                    lo = __builtin_elementwise_fma(pp, f32x2{v.x, v.y}, lo);
+                    hi = __builtin_elementwise_fma(pp, f32x2{v.z, v.w}, hi);
+                    o[e] = lo.x; o[e + 1] = lo.y; o[e + 2] = hi.x; o[e + 3] = hi.y;
+                }
             }
         }
     }

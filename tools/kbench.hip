@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
     float* Kc = (float*)dmalloc((size_t)cap * DKV * 4, 1);
     float* Vc = (float*)dmalloc((size_t)cap * DKV * 4, 1);
     float* rope = (float*)dmalloc((size_t)16384 * HD * 4, 1);
-    float* part = (float*)dmalloc((size_t)H * 64 * (HD + 2) * 4, 0);
+    float* part = (float*)dmalloc((size_t)H * 128 * (HD + 2) * 4, 0);
     float* pv = (float*)dmalloc(4096 * 4, 0);
     int* pi = (int*)dmalloc(4096 * 4, 0);
     int* state;
@@ -203,6 +203,20 @@ int main(int argc, char** argv) {
         while (splits * ATT_BLOCK_KEYS < L) splits *= 2;
         add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, splits, st)); }, iters, st),
             (double)L * DKV * 2 * 4);
+    }
+    {
+        // streaming encoder chunk (-I 0.5): 25 query rows over the 750-row window, 32 heads x 64
+        const int EHd = 64, EH = 32, M = 25, EQ = EH * EHd, ecap = 1024;
+        float* eq = (float*)dmalloc((size_t)M * EQ * 4, 1);
+        float* eo = (float*)dmalloc((size_t)M * EQ * 4, 0);
+        const size_t wsn = (size_t)EH * M * 16 * (EHd + 2);
+        float* ews = (float*)dmalloc(wsn * 4, 0);
+        for (int q0 : {750, 2000}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "attn tiled enc M=25 q0=%d", q0);
+            add(nm, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, q0, 0, 750, 0.125f, st, ews, wsn)); }, iters, st),
+                (double)std::min(q0 + M, 750 + M - 1) * EQ * 2 * 4);
+        }
     }
     {
         int st4[4] = {63, 0, 0, 0};

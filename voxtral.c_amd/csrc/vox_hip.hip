@@ -1168,13 +1168,13 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
 // Step graph g serves contexts of up to 2^g * ATT_BLOCK_KEYS keys (the last one: the whole
 // window); graph 0 runs one attention block per query head and no combine kernel.
 static int graph_splits(const vox_hip_stream_t* s, int g) {
-    return std::min(1 << g, attn_maxch(s->m->c.dec_window));
+    return std::min(1 << g, attn_maxsplits(s->m->c.dec_window));
 }
 
 static int graph_index(const vox_hip_stream_t* s, int ctx) {
     const int need = (ctx + ATT_BLOCK_KEYS - 1) / ATT_BLOCK_KEYS;
     int g = 0;
-    while ((1 << g) < need && (1 << g) < attn_maxch(s->m->c.dec_window)) g++;
+    while ((1 << g) < need && (1 << g) < attn_maxsplits(s->m->c.dec_window)) g++;
     return g;
 }
 

@@ -74,7 +74,8 @@ struct StepPtrs {
 constexpr int ARGB = 64;                // argmax partial blocks per row
 
 int gemv_grid(int rows);
-int attn_maxch(int window);
+int attn_maxch(int window);      // decode-attention partials per head (64-key blocks)
+int attn_maxsplits(int window);  // 256-key spans of a window (graph buckets)
 hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,
                                const float* ada, int M, int D, float eps, hipStream_t st);
 // ws: f32 workspace for split-K partials (ws_elems floats; nullptr = no split)

@@ -1078,14 +1078,21 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 // 256-key split, K/V read once.  With one split the block writes the attention output
 // directly; otherwise it writes an (o, m, l) partial and k_attn_combine merges the splits.
 // ============================================================================
+// NWV = waves per block: 16 (256 keys: one block per head covers short contexts, no
+// combine) or 4 (64-key blocks for long contexts: 4x the blocks, a quarter of the K/V
+// bytes per CU).
 constexpr int ATT_CH = 16;      // keys per wave
-constexpr int ATT_WAVES = 16;   // waves per block (1024 threads)
-constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per block
+constexpr int ATT_WAVES = 16;   // waves per short-context block (1024 threads)
+constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per short-context block
+constexpr int ATT_LWAVES = 4;   // waves per long-context block (256 threads)
+constexpr int ATT_LBK = ATT_CH * ATT_LWAVES;  // keys per long-context block
+constexpr int ATT_MAX_PARTS = 128;  // partials per head the combine kernel merges
 
-template <int HD, int HPB, int DBG = 0, int FUSE = 0>
-__global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap, int pos_host,
-                                                      int window, float scale, int H, int KVH,
-                                                      int maxs, const AttnFuse F = AttnFuse{}) {
+template <int HD, int HPB, int DBG = 0, int FUSE = 0, int NWV = ATT_WAVES>
+__global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int cap, int pos_host,
+                                                          int window, float scale, int H, int KVH,
+                                                          int maxs, const AttnFuse F = AttnFuse{}) {
+    constexpr int NT = NWV * 64, BK = NWV * ATT_CH;
     const int zb = blockIdx.z;  // stream of a batched step (0 for a single stream)
     const float* __restrict__ q = P.q[zb];
     const float* __restrict__ Kc = P.Kc[zb];
@@ -1096,9 +1103,9 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     constexpr int DQ = HD / 4;   // dims per lane for Q.K
     constexpr int DPL = HD / 64; // dims per lane for P.V
     __shared__ __attribute__((aligned(16))) float sQ[HPB][HD];
-    __shared__ float sM[ATT_WAVES][4], sL[ATT_WAVES][4], sF[ATT_WAVES][4];
+    __shared__ float sM[NWV][4], sL[NWV][4], sF[NWV][4];
     __shared__ float sDen[4], sMax[4];
-    __shared__ __attribute__((aligned(16))) float sO[ATT_WAVES][HPB][HD];
+    __shared__ __attribute__((aligned(16))) float sO[NWV][HPB][HD];
     __shared__ __attribute__((aligned(16))) float sKn[FUSE ? HD : 1], sVn[FUSE ? HD : 1];  // the new key's K / V
     const int hpk = H / KVH;
     const int kvh = HPB == 1 ? (int)blockIdx.y % KVH : (int)blockIdx.y;
@@ -1113,14 +1120,16 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
         ts[8] = __builtin_amdgcn_s_memrealtime();
     }
     // the query does not depend on the step state: its load goes out first
-    float qreg = 0.f;
-    if (!FUSE && tid < nh * HD) qreg = q[(size_t)h0 * HD + tid];
+    constexpr int QPT = (HPB * HD + NT - 1) / NT;
+    float qreg[QPT];
+#pragma unroll
+    for (int i = 0; i < QPT; i++) qreg[i] = (!FUSE && tid + i * NT < nh * HD) ? q[(size_t)h0 * HD + tid + i * NT] : 0.f;
     const int lp = state ? state[0] : pos_host;
     const int L = min(lp + 1, window);
     const int first = lp - L + 1;
-    const int S = (L + ATT_BK - 1) / ATT_BK;
+    const int S = (L + BK - 1) / BK;
     if (sb >= S) return;  // uniform per block
-    const int k0 = first + sb * ATT_BK + wave * ATT_CH;  // >= 0
+    const int k0 = first + sb * BK + wave * ATT_CH;  // >= 0
     const int kn = min(ATT_CH, lp + 1 - k0);  // may be <= 0 for trailing waves
     const int kk = lane & 15, dq = lane >> 4;
     // ring slots: one modulo per wave, then a wrap test per key
@@ -1172,16 +1181,18 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
         const int qd = H * HD;
         const float* rp = F.rope + (size_t)lp * HD;
         const size_t slot = (size_t)(lp % cap) * kvd + kvh * HD;
-        if (tid < nh * HD / 2) {
-            const int h = tid / (HD / 2), d = tid % (HD / 2);
-            const int col = (h0 + h) * HD + 2 * d;
-            const float x0 = psum(F.qkv, F.S, F.N, zb, col), x1 = psum(F.qkv, F.S, F.N, zb, col + 1);
-            const float c = rp[2 * d], sn = rp[2 * d + 1];
-            sQ[h][2 * d] = x0 * c - x1 * sn;
-            sQ[h][2 * d + 1] = x0 * sn + x1 * c;
-        } else if (tid >= 256 && tid < 256 + HD / 2) {
-            if (holds_new) {
-                const int d = tid - 256, col = qd + kvh * HD + 2 * d;
+        // jobs: query pairs [0, nq), then (split holding lp) new-key pairs and new-value dims
+        const int nq = nh * HD / 2, nj = nq + (holds_new ? HD / 2 + HD : 0);
+        for (int j = tid; j < nj; j += NT) {
+            if (j < nq) {
+                const int h = j / (HD / 2), d = j % (HD / 2);
+                const int col = (h0 + h) * HD + 2 * d;
+                const float x0 = psum(F.qkv, F.S, F.N, zb, col), x1 = psum(F.qkv, F.S, F.N, zb, col + 1);
+                const float c = rp[2 * d], sn = rp[2 * d + 1];
+                sQ[h][2 * d] = x0 * c - x1 * sn;
+                sQ[h][2 * d + 1] = x0 * sn + x1 * c;
+            } else if (j < nq + HD / 2) {
+                const int d = j - nq, col = qd + kvh * HD + 2 * d;
                 const float x0 = psum(F.qkv, F.S, F.N, zb, col), x1 = psum(F.qkv, F.S, F.N, zb, col + 1);
                 const float c = rp[2 * d], sn = rp[2 * d + 1];
                 const float k0v = x0 * c - x1 * sn, k1v = x0 * sn + x1 * c;
@@ -1190,17 +1201,17 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
                 float* kw = const_cast<float*>(Kc) + slot + 2 * d;
                 kw[0] = k0v;
                 kw[1] = k1v;
-            }
-        } else if (tid >= 512 && tid < 512 + HD) {
-            if (holds_new) {
-                const int e = tid - 512;
+            } else {
+                const int e = j - nq - HD / 2;
                 const float v = psum(F.qkv, F.S, F.N, zb, qd + kvd + kvh * HD + e);
                 sVn[e] = v;
                 const_cast<float*>(Vc)[slot + e] = v;
             }
         }
-    } else if (tid < nh * HD) {
-        sQ[tid / HD][tid % HD] = qreg;
+    } else {
+#pragma unroll
+        for (int i = 0; i < QPT; i++)
+            if (tid + i * NT < nh * HD) sQ[(tid + i * NT) / HD][(tid + i * NT) % HD] = qreg[i];
     }
     if (DBG == 4) {
         __builtin_amdgcn_s_waitcnt(0);
@@ -1333,18 +1344,18 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     __syncthreads();
     if (DBG == 4) ts[3] = __builtin_amdgcn_s_memtime();
     if (wave == 0) {
-        const int w = lane >> 2, h = lane & 3;  // 64 lanes = 16 waves x 4 head slots
+        const int w = lane >> 2, h = lane & 3;  // 64 lanes = 16 wave slots x 4 head slots
         if (h < HPB) {
             float M = -1e30f;
 #pragma unroll
-            for (int i = 0; i < ATT_WAVES; i++) M = fmaxf(M, sM[i][h]);
-            const float f = expf(sM[w][h] - M);
-            float den = f * sL[w][h];
+            for (int i = 0; i < NWV; i++) M = fmaxf(M, sM[i][h]);
+            const float f = w < NWV ? expf(sM[w][h] - M) : 0.f;
+            float den = w < NWV ? f * sL[w][h] : 0.f;
             den += __shfl_xor(den, 4, 64);
             den += __shfl_xor(den, 8, 64);
             den += __shfl_xor(den, 16, 64);
             den += __shfl_xor(den, 32, 64);
-            sF[w][h] = f;
+            if (w < NWV) sF[w][h] = f;
             if (w == 0) {
                 sDen[h] = den;
                 sMax[h] = M;
@@ -1356,7 +1367,7 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
     if (FUSE && S == 1) {
         // output row zb straight into the wo input planes: 8 consecutive dims per thread
         const size_t Pn = (size_t)SK_ROWS * H * HD;
-        for (int e = tid; e < nh * HD / 8; e += 1024) {
+        for (int e = tid; e < nh * HD / 8; e += NT) {
             const int h = e / (HD / 8), d0 = (e % (HD / 8)) * 8;
             const float den = sDen[h];
             uint32_t hp[4], mp[4], lq[4];
@@ -1367,7 +1378,7 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
                 for (int u = 0; u < 2; u++) {
                     float num = 0.f;
 #pragma unroll
-                    for (int w = 0; w < ATT_WAVES; w++) num = fmaf(sF[w][h], sO[w][h][d0 + i + u], num);
+                    for (int w = 0; w < NWV; w++) num = fmaf(sF[w][h], sO[w][h][d0 + i + u], num);
                     v2[u] = den > 0.f ? num * (1.0f / den) : 0.f;
                 }
                 uint16_t a0, b0, c0, a1, b1, c1;
@@ -1384,11 +1395,11 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
         }
         return;
     }
-    for (int e = tid; e < nh * HD; e += 1024) {
+    for (int e = tid; e < nh * HD; e += NT) {
         const int h = e / HD, d = e % HD;
         float num = 0.f;
 #pragma unroll
-        for (int w = 0; w < ATT_WAVES; w++) num = fmaf(sF[w][h], sO[w][h][d], num);
+        for (int w = 0; w < NWV; w++) num = fmaf(sF[w][h], sO[w][h][d], num);
         const float den = sDen[h];
         const int hh = h0 + h;
         if (S == 1) {
@@ -1413,17 +1424,17 @@ __global__ __launch_bounds__(1024) void k_attn_decode(const AttnPtrs P, int cap,
 }
 
 template <int HD>
-__global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int maxs, int pos_host, int window,
+__global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int maxs, int pos_host, int window, int bk,
                                                       uint16_t* __restrict__ xs = nullptr, int H = 0) {
     const float* __restrict__ part = ptrs.part[blockIdx.y];
     const int* __restrict__ state = ptrs.state[blockIdx.y];
     float* __restrict__ out = ptrs.out[blockIdx.y];
-    __shared__ float sf[64];
+    __shared__ float sf[ATT_MAX_PARTS];
     __shared__ float sden;
     const int h = blockIdx.x, tid = threadIdx.x;
     const int lp = state ? state[0] : pos_host;
     const int L = min(lp + 1, window);
-    const int P = (L + ATT_BK - 1) / ATT_BK;
+    const int P = (L + bk - 1) / bk;  // bk: keys per block of the attention launch
     if (P <= 1) return;  // the attention blocks already wrote the output
     const float* ph = part + (size_t)h * maxs * (HD + 2);
     if (tid < 64) {
@@ -2511,14 +2522,18 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-int attn_maxch(int window) { return (window + ATT_BK - 1) / ATT_BK; }
+int attn_maxch(int window) { return (window + ATT_LBK - 1) / ATT_LBK; }
+int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 
-// splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
-// step the launch serves); 1 -> one block per query head, no combine kernel.
+// splits = 256-key spans provided per head group (>= the context's ceil(L / 256) for every
+// step the launch serves).  1: 1024-thread blocks of 256 keys, no combine kernel.  > 1:
+// 256-thread blocks of 64 keys per (kv head, span quarter) and k_attn_combine -- a 256-key
+// block per CU had read K/V at the per-CU rate (L = 1000: 32 blocks, 12.3 us).
 static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int pos_host, int window, float scale,
                               int H, int KVH, int splits, hipStream_t st) {
     const int maxs = attn_maxch(window);
-    if (H % KVH || H / KVH > 4 || maxs > 64 || splits < 1 || splits > maxs || nb < 1 || nb > VOX_MAX_BATCH)
+    if (H % KVH || H / KVH > 4 || maxs > ATT_MAX_PARTS || splits < 1 || splits > attn_maxsplits(window) || nb < 1 ||
+        nb > VOX_MAX_BATCH)
         return hipErrorInvalidValue;
     // batches of >= 4 streams: one block per (stream, kv head), K/V read once for its query
     // heads (16 streams: 15.8 -> ~10 us per layer); a single stream needs the 32 blocks
@@ -2530,10 +2545,11 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
         hipLaunchKernelGGL((k_attn_decode<HD, 1>), dim3(1, H, nb), dim3(1024), 0, st, p, cap, pos_host,    \
                            window, scale, H, KVH, maxs);                                                   \
     } else {                                                                                               \
-        hipLaunchKernelGGL((k_attn_decode<HD, 4>), dim3(splits, KVH, nb), dim3(1024), 0, st, p, cap,       \
-                           pos_host, window, scale, H, KVH, maxs);                                         \
+        hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, ATT_LWAVES>), dim3(splits * (ATT_BK / ATT_LBK), KVH, nb), \
+                           dim3(ATT_LWAVES * 64), 0, st, p, cap, pos_host, window, scale, H, KVH, maxs);    \
         LAUNCH_CHECK();                                                                                    \
-        hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H, nb), dim3(256), 0, st, p, maxs, pos_host, window); \
+        hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H, nb), dim3(256), 0, st, p, maxs, pos_host, window,   \
+                           ATT_LBK);                                                                       \
     }
     if (hd == 128) {
         VOX_ATT(128)
@@ -2566,16 +2582,20 @@ hipError_t launch_attn_decode_batch(int hd, const AttnPtrs& p, int nb, int cap, 
 hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window,
                                    float scale, int H, int KVH, int splits, hipStream_t st) {
     const int maxs = attn_maxch(window);
-    if (hd != 128 || H % KVH || H / KVH > 4 || maxs > 64 || splits < 1 || splits > maxs || nb < 1 ||
-        nb > VOX_MAX_BATCH || !f.qkv || !f.rope || !f.xs || f.S < 1 || f.N != (H + 2 * KVH) * hd)
+    if (hd != 128 || H % KVH || H / KVH > 4 || maxs > ATT_MAX_PARTS || splits < 1 || splits > attn_maxsplits(window) ||
+        nb < 1 || nb > VOX_MAX_BATCH || !f.qkv || !f.rope || !f.xs || f.S < 1 || f.N != (H + 2 * KVH) * hd)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1>), dim3(splits, KVH, nb), dim3(1024), 0, st, p, cap, 0, window,
-                       scale, H, KVH, maxs, f);
-    LAUNCH_CHECK();
-    if (splits > 1) {
-        hipLaunchKernelGGL(k_attn_combine<128>, dim3(H, nb), dim3(256), 0, st, p, maxs, 0, window, f.xs, H);
+    if (splits == 1) {
+        hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, 0, window,
+                           scale, H, KVH, maxs, f);
         LAUNCH_CHECK();
+        return hipSuccess;
     }
+    hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_LWAVES>), dim3(splits * (ATT_BK / ATT_LBK), KVH, nb),
+                       dim3(ATT_LWAVES * 64), 0, st, p, cap, 0, window, scale, H, KVH, maxs, f);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_attn_combine<128>, dim3(H, nb), dim3(256), 0, st, p, maxs, 0, window, ATT_LBK, f.xs, H);
+    LAUNCH_CHECK();
     return hipSuccess;
 }
 // diagnostic variants for tools/kbench (not used by the engine)

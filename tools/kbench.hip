@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -194,7 +194,7 @@ int main(int argc, char** argv) {
         add("split fplanes 16x4096", timeit([&] { CK(launch_split_fplanes(xr, 16, DQ, xp, st)); }, iters, st), 16.0 * DQ * 10);
         add("swiglu(6) fplanes 16x9216", timeit([&] { CK(launch_swiglu_fplanes(part, 6, DH, 16, xp, st)); }, iters, st), 16.0 * DH * (6 * 8 + 6));
     }
-    for (int L : {64, 187, 256, 1000, 4096, 8192}) {
+    for (int L : {64, 187, 256, 1000, 2300, 4096, 8192}) {
         int st4[4] = {L - 1, 0, 0, 0};
         CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
         char nm[64];
@@ -203,6 +203,14 @@ int main(int argc, char** argv) {
         while (splits * ATT_BLOCK_KEYS < L) splits *= 2;
         add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, splits, st)); }, iters, st),
             (double)L * DKV * 2 * 4);
+        for (int lw : {2, 4}) {
+            if (L <= 256) continue;
+            g_attn_lw = lw;
+            snprintf(nm, sizeof nm, "attn decode L=%d %d-key blocks", L, lw * 16);
+            add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, splits, st)); }, iters, st),
+                (double)L * DKV * 2 * 4);
+            g_attn_lw = 0;
+        }
     }
     {
         // streaming encoder chunk (-I 0.5): 25 query rows over the 750-row window, 32 heads x 64
@@ -211,12 +219,20 @@ int main(int argc, char** argv) {
         float* eo = (float*)dmalloc((size_t)M * EQ * 4, 0);
         const size_t wsn = (size_t)EH * M * 16 * (EHd + 2);
         float* ews = (float*)dmalloc(wsn * 4, 0);
-        for (int q0 : {750, 2000}) {
-            char nm[64];
-            snprintf(nm, sizeof nm, "attn tiled enc M=25 q0=%d", q0);
-            add(nm, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, q0, 0, 750, 0.125f, st, ews, wsn)); }, iters, st),
-                (double)std::min(q0 + M, 750 + M - 1) * EQ * 2 * 4);
+        uint16_t* exs = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * EQ * 2, 0);
+        char nm0[64];
+        for (int qt : {16, 32}) {
+            g_attn_qt = qt;
+            for (int q0 : {750, 2000}) {
+                snprintf(nm0, sizeof nm0, "attn tiled enc M=25 q0=%d QT=%d", q0, qt);
+                add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, q0, 0, 750, 0.125f, st, ews, wsn)); }, iters, st),
+                    (double)std::min(q0 + M, 750 + M - 1) * EQ * 2 * 4);
+            }
+            snprintf(nm0, sizeof nm0, "attn tiled enc M=25 QT=%d -> planes", qt);
+            add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, 2000, 0, 750, 0.125f, st, ews, wsn, exs)); }, iters, st),
+                (double)(750 + M - 1) * EQ * 2 * 4);
         }
+        g_attn_qt = 0;
     }
     {
         int st4[4] = {63, 0, 0, 0};

@@ -926,11 +926,11 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
         CK(launch_rmsnorm_fplanes(x, n, ED, L.attn_norm, nullptr, c.enc_eps, xp, l ? sl : nullptr,
                                   l ? skl_splits(EH) : 0, st, l ? m->enc[l - 1].b2 : nullptr));
         CK(launch_gemm_skl(xp, ED, F.wqkv, L.sqkv, NQKV, n, sl, st));
-        CK(launch_slabs_rows(sl, skl_splits(ED), n, NQKV, L.bqkv, s->qkv, NQKV, st));
-        CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
+        // QKV slabs + biases -> RoPE -> K/V append (one pass), attention with its output
+        // merged straight into the wo planes
+        CK(launch_slabs_rope_kv(sl, skl_splits(ED), n, L.bqkv, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
         CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
-                             s->gws, s->gws_n));
-        CK(launch_split_fplanes(s->att, n, EQ, xp, st));
+                             s->gws, s->gws_n, xp));
         CK(launch_gemm_skl(xp, EQ, F.wo, L.so, ED, n, sl, st));
         // wo residual (+ bias) then the FFN RMSNorm -> planes (encoder.c:640-650)
         CK(launch_rmsnorm_fplanes(x, n, ED, L.ffn_norm, nullptr, c.enc_eps, xp, sl, skl_splits(EQ), st, L.bo));

@@ -88,7 +88,11 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
                              int k_first, int window, float scale, hipStream_t st, float* ws = nullptr,
-                             size_t ws_elems = 0);
+                             size_t ws_elems = 0, uint16_t* xs = nullptr);
+// xs: the output also (or only, through the combine kernel) as fragment-major planes
+// the skinny encoder's QKV slabs (+ bias) -> RoPE'd q rows and the K/V ring slots (one pass)
+hipError_t launch_slabs_rope_kv(const float* part, int S, int M, const float* bias, int qd, int kvd, int hd,
+                                const float* rope, int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st);
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st);
 const void* gemv_kernel(int pro, int epi, const GemvArgs& a);
 hipError_t launch_gemv_timed(int pro, int epi, const GemvArgs& a, hipEvent_t start, hipEvent_t stop,

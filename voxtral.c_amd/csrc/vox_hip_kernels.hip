@@ -593,9 +593,12 @@ __global__ __launch_bounds__(256) void k_rope_kv(const float* __restrict__ qkv, 
 // Tiled causal/windowed attention for M>1 queries (encoder chunks, decoder prefill).
 // Semantics of vox_causal_attention (voxtral_kernels.c:541-611) with logical positions:
 // query i sits at q_pos0+i and sees keys p with max(k_first, qp-window+1) <= p <= qp.
-// Block = (head, 16 queries); K/V tiles of 64 keys staged in LDS; online softmax.
+// Block = (head, QT queries): 16, or 32 for chunks of <= 32 rows (a streaming encoder
+// chunk: each K/V tile is then read once per head).  LQ = 256 / QT lanes per query hold
+// KPL keys of a tile for Q.K and DPT dims for P.V.  K/V tiles of 64 keys staged in LDS;
+// online softmax.
 // ============================================================================
-template <int HD>
+template <int HD, int QT>
 __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q, int ldq,
                                                     const float* __restrict__ Kc,
                                                     const float* __restrict__ Vc, int cap,
@@ -605,16 +608,17 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
     // ns > 1 (few query rows, long key range: streaming encoder chunks): blockIdx.z takes
     // the z-th of ns key ranges and writes an unnormalised (o, m, l) partial per query row
     // to part[(h * M + q) * ns + z][HD + 2]; k_attn_tiled_combine merges them in z order.
-    constexpr int QT = 16, KT = 64, DPT = HD / 16;
-    __shared__ __attribute__((aligned(16))) float sQ[QT][HD];
+    constexpr int KT = 64, LQ = 256 / QT, KPL = KT / LQ, DPT = HD / LQ;
+    // rows padded by 4 floats: the lanes of a wave read QT / 4 different query rows
+    __shared__ __attribute__((aligned(16))) float sQ[QT][HD + 4];
     __shared__ __attribute__((aligned(16))) float sK[KT][HD + 4];
     __shared__ __attribute__((aligned(16))) float sV[KT][HD];
-    __shared__ float sP[QT][KT];
+    __shared__ __attribute__((aligned(16))) float sP[QT][KT + 4];
     const int h = blockIdx.x, q0 = blockIdx.y * QT;
     const int kvh = h / (H / KVH);
     const int kvd = KVH * HD;
     const int nq = min(QT, M - q0);
-    const int tid = threadIdx.x, qi = tid >> 4, j = tid & 15;
+    const int tid = threadIdx.x, qi = tid / LQ, j = tid % LQ;
 
     for (int e = tid; e < QT * HD; e += 256) {
         int r = e / HD, d = e % HD;
@@ -653,28 +657,28 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
             *reinterpret_cast<float4*>(&sV[r][c4 * 4]) = vv;
         }
         __syncthreads();
-        float s[4];
+        float s[KPL];
         float tmax = -INFINITY;
         {
-            // the query slice is read once per 4 dims for all 4 keys (5 LDS reads per 16
-            // FMAs instead of 8), and the products run as packed f32 FMAs (v_pk_fma_f32)
-            f32x2 acc[4][2];
+            // the query slice is read once per 4 dims for all KPL keys, and the products run
+            // as packed f32 FMAs (v_pk_fma_f32)
+            f32x2 acc[KPL][2];
 #pragma unroll
-            for (int jj = 0; jj < 4; jj++) acc[jj][0] = acc[jj][1] = f32x2{0.f, 0.f};
-#pragma unroll 8
+            for (int jj = 0; jj < KPL; jj++) acc[jj][0] = acc[jj][1] = f32x2{0.f, 0.f};
+#pragma unroll(32 / KPL)
             for (int d = 0; d < HD; d += 4) {
                 const float4 a = *reinterpret_cast<const float4*>(&sQ[qi][d]);
                 const f32x2 alo = {a.x, a.y}, ahi = {a.z, a.w};
 #pragma unroll
-                for (int jj = 0; jj < 4; jj++) {
-                    const float4 b = *reinterpret_cast<const float4*>(&sK[j + 16 * jj][d]);
+                for (int jj = 0; jj < KPL; jj++) {
+                    const float4 b = *reinterpret_cast<const float4*>(&sK[j + LQ * jj][d]);
                     acc[jj][0] = __builtin_elementwise_fma(alo, f32x2{b.x, b.y}, acc[jj][0]);
                     acc[jj][1] = __builtin_elementwise_fma(ahi, f32x2{b.z, b.w}, acc[jj][1]);
                 }
             }
 #pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
-                const int kp = kb + j + 16 * jj;
+            for (int jj = 0; jj < KPL; jj++) {
+                const int kp = kb + j + LQ * jj;
                 const bool valid = qvalid && kp <= qp && kp >= qp - window + 1 && kp >= k_first && kp <= kend;
                 const float dot = (acc[jj][0].x + acc[jj][1].x) + (acc[jj][0].y + acc[jj][1].y);
                 s[jj] = valid ? dot * scale : -INFINITY;
@@ -682,17 +686,17 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
             }
         }
 #pragma unroll
-        for (int off = 8; off > 0; off >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, off, 16));
+        for (int off = LQ / 2; off > 0; off >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, off, LQ));
         const float mnew = fmaxf(m, tmax);
         float psum = 0.f;
 #pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
+        for (int jj = 0; jj < KPL; jj++) {
             float p = (s[jj] == -INFINITY) ? 0.f : expf(s[jj] - mnew);
-            sP[qi][j + 16 * jj] = p;
+            sP[qi][j + LQ * jj] = p;
             psum += p;
         }
 #pragma unroll
-        for (int off = 8; off > 0; off >>= 1) psum += __shfl_xor(psum, off, 16);
+        for (int off = LQ / 2; off > 0; off >>= 1) psum += __shfl_xor(psum, off, LQ);
         const float alpha = expf(m - mnew);
         l = l * alpha + psum;
         m = mnew;
@@ -733,10 +737,12 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
     }
 }
 
-// merge of k_attn_tiled's ns key-range partials: one block per (head, query row)
+// merge of k_attn_tiled's ns key-range partials: one block per (head, query row); with xs the
+// row goes straight into the fragment-major planes of the wo input (H * HD columns)
 template <int HD>
 __global__ __launch_bounds__(HD) void k_attn_tiled_combine(const float* __restrict__ part, int ns, int M,
-                                                           float* __restrict__ O, int ldo) {
+                                                           float* __restrict__ O, int ldo, uint16_t* __restrict__ xs) {
+    __shared__ __attribute__((aligned(16))) float sv[HD];
     const int h = blockIdx.x, q = blockIdx.y, d = threadIdx.x;
     const float* pp = part + (size_t)(h * M + q) * ns * (HD + 2);
     float mx = -1e30f;
@@ -748,7 +754,31 @@ __global__ __launch_bounds__(HD) void k_attn_tiled_combine(const float* __restri
         den = fmaf(f, pz[HD + 1], den);
         num = fmaf(f, pz[d], num);
     }
-    O[(size_t)q * ldo + h * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
+    const float v = den > 0.f ? num * (1.0f / den) : 0.f;
+    if (!xs) {
+        O[(size_t)q * ldo + h * HD + d] = v;
+        return;
+    }
+    sv[d] = v;
+    __syncthreads();
+    if (d < HD / 8) {
+        const float4 a = *reinterpret_cast<const float4*>(&sv[d * 8]), b = *reinterpret_cast<const float4*>(&sv[d * 8 + 4]);
+        const float w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t hp[4], mp[4], lp[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+            uint16_t h0, m0, l0, h1, m1, l1;
+            split3(w[e], h0, m0, l0);
+            split3(w[e + 1], h1, m1, l1);
+            hp[e / 2] = h0 | ((uint32_t)h1 << 16);
+            mp[e / 2] = m0 | ((uint32_t)m1 << 16);
+            lp[e / 2] = l0 | ((uint32_t)l1 << 16);
+        }
+        const int K = gridDim.x * HD, k = h * HD + d * 8;
+        *reinterpret_cast<uint4*>(xs + frag_at(q, K, 0, k)) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+        *reinterpret_cast<uint4*>(xs + frag_at(q, K, 1, k)) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+        *reinterpret_cast<uint4*>(xs + frag_at(q, K, 2, k)) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
+    }
 }
 
 // ============================================================================
@@ -1079,13 +1109,14 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 // directly; otherwise it writes an (o, m, l) partial and k_attn_combine merges the splits.
 // ============================================================================
 // NWV = waves per block: 16 (256 keys: one block per head covers short contexts, no
-// combine) or 4 (64-key blocks for long contexts: 4x the blocks, a quarter of the K/V
-// bytes per CU).
+// combine) or 8 (128-key blocks for long contexts: twice the blocks, half the K/V bytes per
+// CU; tools/kbench: L = 4096 11.9 us against 14.5 with 64-key and 19.2 with 32-key blocks).
 constexpr int ATT_CH = 16;      // keys per wave
 constexpr int ATT_WAVES = 16;   // waves per short-context block (1024 threads)
 constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per short-context block
-constexpr int ATT_LWAVES = 4;   // waves per long-context block (256 threads)
+constexpr int ATT_LWAVES = 8;   // waves per long-context block (512 threads)
 constexpr int ATT_LBK = ATT_CH * ATT_LWAVES;  // keys per long-context block
+constexpr int ATT_MIN_BK = 64;      // smallest block (kbench variant): sizes the partials
 constexpr int ATT_MAX_PARTS = 128;  // partials per head the combine kernel merges
 
 template <int HD, int HPB, int DBG = 0, int FUSE = 0, int NWV = ATT_WAVES>
@@ -1819,6 +1850,38 @@ __global__ __launch_bounds__(256) void k_resid_slabs(float* __restrict__ x, int 
     if (n < D) x[(size_t)j * D + n] += bias ? psum(part, S, D, j, n) + bias[n] : psum(part, S, D, j, n);
 }
 
+// QKV slabs of row blockIdx.x summed in split order (+ bias), RoPE of q and k, K/V append at
+// ring slot (pos0 + i) % cap: k_slabs_rows + k_rope_kv in one pass with the same operations
+// in the same order (voxtral_encoder.c:570-607).  rope: the row of position pos0.
+__global__ __launch_bounds__(256) void k_slabs_rope_kv(const float* __restrict__ part, int S,
+                                                       const float* __restrict__ bias, int qd, int kvd, int hd,
+                                                       const float* __restrict__ rope, int pos0,
+                                                       float* __restrict__ q, float* __restrict__ Kc,
+                                                       float* __restrict__ Vc, int cap) {
+    // one column pair per thread: q / k pairs (roped), then v pairs; grid (pairs / 256, rows)
+    const int i = blockIdx.y, N = qd + 2 * kvd;
+    const int p = blockIdx.x * 256 + threadIdx.x, n = 2 * p;
+    if (n >= N) return;
+    const int slot = (pos0 + i) % cap;
+    float x0 = psum(part, S, N, i, n), x1 = psum(part, S, N, i, n + 1);
+    if (bias) {
+        x0 += bias[n];
+        x1 += bias[n + 1];
+    }
+    if (n >= qd + kvd) {
+        float* vr = Vc + (size_t)slot * kvd + (n - qd - kvd);
+        vr[0] = x0;
+        vr[1] = x1;
+        return;
+    }
+    const float* rp = rope + (size_t)i * hd;
+    const int d = n % hd / 2;  // qd is a multiple of hd: the pair's rope index
+    const float c = rp[2 * d], s = rp[2 * d + 1];
+    float* dst = n < qd ? q + (size_t)i * qd + n : Kc + (size_t)slot * kvd + (n - qd);
+    dst[0] = x0 * c - x1 * s;
+    dst[1] = x0 * s + x1 * c;
+}
+
 // out[j][n] = the S slabs of row j + bias[n] (row-major result of a skinny projection)
 __global__ __launch_bounds__(256) void k_slabs_rows(const float* __restrict__ part, int S, int N,
                                                     const float* __restrict__ bias, float* __restrict__ out, int ldo) {
@@ -2388,14 +2451,21 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
     return hipSuccess;
 }
 
+int g_attn_qt = 0;  // tools/kbench knob: queries per k_attn_tiled block (16 or 32; 0 = automatic)
+
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
-                             int k_first, int window, float scale, hipStream_t st, float* ws, size_t ws_elems) {
+                             int k_first, int window, float scale, hipStream_t st, float* ws, size_t ws_elems,
+                             uint16_t* xs) {
     if (M <= 0) return hipSuccess;
     if (hd != 64 && hd != 128) return hipErrorInvalidValue;
-    const int qb = (M + 15) / 16;
+    if (xs && (M > SK_MAX_ROWS || ldo != H * hd)) return hipErrorInvalidValue;
+    // 16 queries per block: 32 (each K/V tile of a 25-row streaming chunk read once per head
+    // instead of twice) measured slower, 15.7 vs 14.6 us (tools/kbench)
+    const int QT = g_attn_qt ? g_attn_qt : 16;
+    const int qb = (M + QT - 1) / QT;
     // key-range splits when the (head, query block) grid cannot fill the chip: at least 64
-    // keys per split, about 512 blocks in all (a 25-row streaming chunk over ~775 keys: 12)
+    // keys per split, about 512 blocks in all (a 25-row streaming chunk over ~775 keys: 13)
     int ks = q_pos0 - window + 1;
     if (ks < k_first) ks = k_first;
     const int keys = q_pos0 + M - ks;
@@ -2405,20 +2475,38 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
         while (ns > 1 && (size_t)H * M * ns * (hd + 2) > ws_elems) ns--;
     }
     dim3 grid(H, qb, ns);
-    if (hd == 64)
-        hipLaunchKernelGGL(k_attn_tiled<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
-                           k_first, window, scale, ns, ws);
-    else
-        hipLaunchKernelGGL(k_attn_tiled<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
-                           k_first, window, scale, ns, ws);
+#define VOX_TILED(HD, QQ)                                                                                       \
+    hipLaunchKernelGGL((k_attn_tiled<HD, QQ>), grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, \
+                       q_pos0, k_first, window, scale, ns, ws)
+    if (hd == 64) {
+        if (QT == 32) VOX_TILED(64, 32);
+        else VOX_TILED(64, 16);
+    } else {
+        if (QT == 32) VOX_TILED(128, 32);
+        else VOX_TILED(128, 16);
+    }
+#undef VOX_TILED
     LAUNCH_CHECK();
     if (ns > 1) {
+        // with xs the combine writes the wo planes itself
         if (hd == 64)
-            hipLaunchKernelGGL(k_attn_tiled_combine<64>, dim3(H, M), dim3(64), 0, st, ws, ns, M, O, ldo);
+            hipLaunchKernelGGL(k_attn_tiled_combine<64>, dim3(H, M), dim3(64), 0, st, ws, ns, M, O, ldo, xs);
         else
-            hipLaunchKernelGGL(k_attn_tiled_combine<128>, dim3(H, M), dim3(128), 0, st, ws, ns, M, O, ldo);
+            hipLaunchKernelGGL(k_attn_tiled_combine<128>, dim3(H, M), dim3(128), 0, st, ws, ns, M, O, ldo, xs);
         LAUNCH_CHECK();
+    } else if (xs) {
+        return launch_split_fplanes(O, M, H * hd, xs, st);
     }
+    return hipSuccess;
+}
+
+hipError_t launch_slabs_rope_kv(const float* part, int S, int M, const float* bias, int qd, int kvd, int hd,
+                                const float* rope, int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (M > SK_MAX_ROWS || S < 1 || qd % hd || kvd % hd || hd % 2) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_slabs_rope_kv, dim3((qd / 2 + kvd + 255) / 256, M), dim3(256), 0, st, part, S, bias, qd, kvd,
+                       hd, rope, pos0, q, Kc, Vc, cap);
+    LAUNCH_CHECK();
     return hipSuccess;
 }
 
@@ -2522,13 +2610,23 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-int attn_maxch(int window) { return (window + ATT_LBK - 1) / ATT_LBK; }
+int attn_maxch(int window) { return (window + ATT_MIN_BK - 1) / ATT_MIN_BK; }
 int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
+int g_attn_lw = 0;  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
+
+// past 256 keys: blocks of NWV x 16 keys per (kv head, key range), then the combine kernel
+template <int HD, int NWV>
+static void attn_long(const AttnPtrs& p, int nb, int cap, int pos_host, int window, float scale, int H, int KVH,
+                      int splits, int maxs, hipStream_t st) {
+    hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, NWV>), dim3(splits * (ATT_BK / (NWV * ATT_CH)), KVH, nb),
+                       dim3(NWV * 64), 0, st, p, cap, pos_host, window, scale, H, KVH, maxs);
+    hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H, nb), dim3(256), 0, st, p, maxs, pos_host, window, NWV * ATT_CH);
+}
 
 // splits = 256-key spans provided per head group (>= the context's ceil(L / 256) for every
 // step the launch serves).  1: 1024-thread blocks of 256 keys, no combine kernel.  > 1:
-// 256-thread blocks of 64 keys per (kv head, span quarter) and k_attn_combine -- a 256-key
-// block per CU had read K/V at the per-CU rate (L = 1000: 32 blocks, 12.3 us).
+// 512-thread blocks of 128 keys per (kv head, span half) and k_attn_combine -- a 256-key
+// block per CU had read K/V at the per-CU rate (L = 1000: 32 blocks, 12.3 us; now 10.0).
 static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int pos_host, int window, float scale,
                               int H, int KVH, int splits, hipStream_t st) {
     const int maxs = attn_maxch(window);
@@ -2544,12 +2642,11 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
     } else if (splits == 1) {                                                                              \
         hipLaunchKernelGGL((k_attn_decode<HD, 1>), dim3(1, H, nb), dim3(1024), 0, st, p, cap, pos_host,    \
                            window, scale, H, KVH, maxs);                                                   \
+    } else if (g_attn_lw == 4 || (g_attn_lw == 2 && splits * 8 <= maxs)) {                                \
+        if (g_attn_lw == 4) attn_long<HD, 4>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st); \
+        else attn_long<HD, 2>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);              \
     } else {                                                                                               \
-        hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, ATT_LWAVES>), dim3(splits * (ATT_BK / ATT_LBK), KVH, nb), \
-                           dim3(ATT_LWAVES * 64), 0, st, p, cap, pos_host, window, scale, H, KVH, maxs);    \
-        LAUNCH_CHECK();                                                                                    \
-        hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H, nb), dim3(256), 0, st, p, maxs, pos_host, window,   \
-                           ATT_LBK);                                                                       \
+        attn_long<HD, ATT_LWAVES>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);          \
     }
     if (hd == 128) {
         VOX_ATT(128)

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -221,8 +221,10 @@ int main(int argc, char** argv) {
         float* ews = (float*)dmalloc(wsn * 4, 0);
         uint16_t* exs = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * EQ * 2, 0);
         char nm0[64];
-        for (int qt : {16, 32}) {
-            g_attn_qt = qt;
+        for (int qt : {0, 16, 32}) {
+            // 0: k_attn_mf (MFMA, 16 queries); 16 / 32: the VALU k_attn_tiled
+            g_attn_valu = qt != 0;
+            g_attn_qt = qt ? qt : 16;
             for (int q0 : {750, 2000}) {
                 snprintf(nm0, sizeof nm0, "attn tiled enc M=25 q0=%d QT=%d", q0, qt);
                 add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, q0, 0, 750, 0.125f, st, ews, wsn)); }, iters, st),
@@ -233,6 +235,20 @@ int main(int argc, char** argv) {
                 (double)(750 + M - 1) * EQ * 2 * 4);
         }
         g_attn_qt = 0;
+        g_attn_valu = 0;
+        // one-shot encoder pass (jfk: 677 rows, keys from 0): MFMA vs VALU
+        {
+            const int M1 = 677;
+            float* q1 = (float*)dmalloc((size_t)M1 * EQ * 4, 1);
+            float* o1 = (float*)dmalloc((size_t)M1 * EQ * 4, 0);
+            for (int valu : {0, 1}) {
+                g_attn_valu = valu;
+                snprintf(nm0, sizeof nm0, "attn tiled enc M=677 %s", valu ? "VALU" : "MFMA");
+                add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, q1, EQ, Kc, Vc, ecap, o1, EQ, M1, EH, EH, 0, 0, 750, 0.125f, st, ews, wsn)); }, iters / 4 + 1, st),
+                    (double)M1 * EQ * 2 * 4);
+            }
+            g_attn_valu = 0;
+        }
     }
     {
         int st4[4] = {63, 0, 0, 0};

@@ -737,6 +737,174 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
     }
 }
 
+// ============================================================================
+// The same attention on f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32
+// accumulation), with k_attn_tiled's semantics, grid and partial layout.  Block = (head, 16
+// queries, key range z) of 4 waves; wave w takes the range's 16-key chunks w, w+4, ...  Per
+// chunk: S^T = K Q^T, A = the K rows straight from the cache, B = the block's query rows held
+// in registers (lane l: row l & 15, dims [g HD/4, (g+1) HD/4) of group g = l >> 4); online
+// softmax on the accumulator (keys 4g + i in the registers, query l & 15 on the lane); then
+// O += P V with P taken from the S^T registers as the A operand (no LDS) and V as B (lane l:
+// dims [NB j, NB j + NB) of rows 4g + c).  The next chunk's K / V load while the current one
+// computes.  The four waves' (o, m, l) meet in LDS at the end.  The VALU kernel staged K / V
+// tiles in LDS and was bound by their reads (160 ds_read_b128 per thread per 64-key tile).
+// ============================================================================
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, int ldq, const float* __restrict__ Kc,
+                                                 const float* __restrict__ Vc, int cap, float* __restrict__ O,
+                                                 int ldo, int M, int H, int KVH, int q_pos0, int k_first, int window,
+                                                 float scale, int ns, float* __restrict__ part) {
+    constexpr int DG = HD / 4;   // S^T: dims per lane group
+    constexpr int NB = HD / 16;  // P V: output dims per lane (d = NB j + b)
+    __shared__ float sm[4][16], sl[4][16];
+    __shared__ __attribute__((aligned(16))) float so[4][16][HD + 4];
+    const int h = blockIdx.x, q0 = blockIdx.y * 16;
+    const int kvh = h / (H / KVH), kvd = KVH * HD;
+    const int nq = min(16, M - q0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int j = lane & 15, g = lane >> 4;
+    float qv[DG];
+    {
+        const float* qr = Q + (size_t)(q0 + j) * ldq + h * HD + g * DG;
+#pragma unroll
+        for (int t = 0; t < DG; t += 4) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j < nq) v = *reinterpret_cast<const float4*>(qr + t);
+            qv[t] = v.x; qv[t + 1] = v.y; qv[t + 2] = v.z; qv[t + 3] = v.w;
+        }
+    }
+    const int qfirst = q_pos0 + q0, qlast = q_pos0 + q0 + nq - 1;
+    int kstart = max(qfirst - window + 1, k_first);
+    int kend = qlast;
+    if (ns > 1) {
+        const int span = ((kend - kstart + 1 + ns - 1) / ns + 15) / 16 * 16;
+        kstart += blockIdx.z * span;
+        kend = min(kend, kstart + span - 1);
+    }
+    const int qp = q_pos0 + q0 + j;  // the query of this lane's S^T column
+    float m = -1e30f, l = 0.f;
+    f32x4 acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K row kb + j (dims of group g) and V rows kb + 4g + c (dims [NB j, NB j + NB)); rows
+    // past kend are clamped to it (their scores are masked)
+    float kv[DG], vv[4][NB];
+    auto load = [&](int kb, float* kd, float (*vd)[NB]) {
+        const float* kr = Kc + (size_t)(min(kb + j, kend) % cap) * kvd + kvh * HD + g * DG;
+#pragma unroll
+        for (int t = 0; t < DG; t += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(kr + t);
+            kd[t] = v.x; kd[t + 1] = v.y; kd[t + 2] = v.z; kd[t + 3] = v.w;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float* vr = Vc + (size_t)(min(kb + 4 * g + c, kend) % cap) * kvd + kvh * HD + NB * j;
+#pragma unroll
+            for (int b = 0; b < NB; b += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(vr + b);
+                vd[c][b] = v.x; vd[c][b + 1] = v.y; vd[c][b + 2] = v.z; vd[c][b + 3] = v.w;
+            }
+        }
+    };
+    int kb = kstart + wave * 16;
+    if (kb <= kend) load(kb, kv, vv);
+    for (; kb <= kend; kb += 64) {
+        float kn[DG], vn[4][NB];
+        if (kb + 64 <= kend) load(kb + 64, kn, vn);
+        // S^T = K Q^T over two accumulators (alternate dims)
+        f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+#pragma unroll
+        for (int t = 0; t < DG; t += 2) {
+            s0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[t], qv[t], s0, 0, 0, 0);
+            s1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kv[t + 1], qv[t + 1], s1, 0, 0, 0);
+        }
+        float p[4];
+        float cmax = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int kp = kb + 4 * g + i;
+            const bool valid = j < nq && kp <= kend && kp <= qp && kp >= qp - window + 1 && kp >= k_first;
+            p[i] = valid ? (s0[i] + s1[i]) * scale : -INFINITY;
+            cmax = fmaxf(cmax, p[i]);
+        }
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+        const float mnew = fmaxf(m, cmax);
+        float ps = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            p[i] = (p[i] == -INFINITY) ? 0.f : expf(p[i] - mnew);
+            ps += p[i];
+        }
+        ps += __shfl_xor(ps, 16, 64);
+        ps += __shfl_xor(ps, 32, 64);
+        const float alpha = expf(m - mnew);
+        l = l * alpha + ps;
+        m = mnew;
+        // output rows 4g + i are queries 4g + i: their rescale factor sits on lane 4g + i
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const float a = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+            for (int b = 0; b < NB; b++) acc[b][i] *= a;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int b = 0; b < NB; b++) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(p[c], vv[c][b], acc[b], 0, 0, 0);
+        if (kb + 64 <= kend) {
+#pragma unroll
+            for (int t = 0; t < DG; t++) kv[t] = kn[t];
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+#pragma unroll
+                for (int b = 0; b < NB; b++) vv[c][b] = vn[c][b];
+        }
+    }
+    // merge the waves: query r = tid >> 4, dims [(tid & 15) NB, +NB)
+    if (g == 0) {
+        sm[wave][j] = m;
+        sl[wave][j] = l;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int b = 0; b < NB; b++) so[wave][4 * g + i][NB * j + b] = acc[b][i];
+    __syncthreads();
+    const int r = tid >> 4, d0 = (tid & 15) * NB;
+    if (r >= nq) return;
+    float mx = -1e30f;
+#pragma unroll
+    for (int w = 0; w < 4; w++) mx = fmaxf(mx, sm[w][r]);
+    float f[4], den = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        f[w] = expf(sm[w][r] - mx);
+        den = fmaf(f[w], sl[w][r], den);
+    }
+    float num[NB];
+#pragma unroll
+    for (int e = 0; e < NB; e++) {
+        num[e] = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; w++) num[e] = fmaf(f[w], so[w][r][d0 + e], num[e]);
+    }
+    if (ns > 1) {
+        float* pp = part + ((size_t)(h * M + q0 + r) * ns + blockIdx.z) * (HD + 2);
+#pragma unroll
+        for (int e = 0; e < NB; e++) pp[d0 + e] = num[e];
+        if ((tid & 15) == 0) {
+            pp[HD] = mx;
+            pp[HD + 1] = den;
+        }
+    } else {
+        const float inv = den > 0.f ? 1.0f / den : 0.f;
+        float* op = O + (size_t)(q0 + r) * ldo + h * HD + d0;
+#pragma unroll
+        for (int e = 0; e < NB; e++) op[e] = num[e] * inv;
+    }
+}
+
 // merge of k_attn_tiled's ns key-range partials: one block per (head, query row); with xs the
 // row goes straight into the fragment-major planes of the wo input (H * HD columns)
 template <int HD>
@@ -2451,7 +2619,8 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
     return hipSuccess;
 }
 
-int g_attn_qt = 0;  // tools/kbench knob: queries per k_attn_tiled block (16 or 32; 0 = automatic)
+int g_attn_qt = 0;    // tools/kbench knob: queries per k_attn_tiled block (16 or 32; 0 = automatic)
+int g_attn_valu = 0;  // tools/kbench knob: 1 = the VALU k_attn_tiled instead of k_attn_mf
 
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
@@ -2478,7 +2647,14 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
 #define VOX_TILED(HD, QQ)                                                                                       \
     hipLaunchKernelGGL((k_attn_tiled<HD, QQ>), grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, \
                        q_pos0, k_first, window, scale, ns, ws)
-    if (hd == 64) {
+    if (!g_attn_valu && QT == 16) {
+        if (hd == 64)
+            hipLaunchKernelGGL(k_attn_mf<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
+                               k_first, window, scale, ns, ws);
+        else
+            hipLaunchKernelGGL(k_attn_mf<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
+                               k_first, window, scale, ns, ws);
+    } else if (hd == 64) {
         if (QT == 32) VOX_TILED(64, 32);
         else VOX_TILED(64, 16);
     } else {

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -236,6 +236,13 @@ int main(int argc, char** argv) {
         }
         g_attn_qt = 0;
         g_attn_valu = 0;
+        for (int nbk : {128, 256, 1024}) {
+            g_attn_blocks = nbk;
+            snprintf(nm0, sizeof nm0, "attn mf enc M=25 -> planes, ~%d blocks", nbk);
+            add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, 2000, 0, 750, 0.125f, st, ews, wsn, exs)); }, iters, st),
+                (double)(750 + M - 1) * EQ * 2 * 4);
+        }
+        g_attn_blocks = 0;
         // one-shot encoder pass (jfk: 677 rows, keys from 0): MFMA vs VALU
         {
             const int M1 = 677;

@@ -2621,6 +2621,7 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
 
 int g_attn_qt = 0;    // tools/kbench knob: queries per k_attn_tiled block (16 or 32; 0 = automatic)
 int g_attn_valu = 0;  // tools/kbench knob: 1 = the VALU k_attn_tiled instead of k_attn_mf
+int g_attn_blocks = 0;  // tools/kbench knob: target grid size of the key-range split (0 = 512)
 
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
@@ -2634,13 +2635,15 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
     const int QT = g_attn_qt ? g_attn_qt : 16;
     const int qb = (M + QT - 1) / QT;
     // key-range splits when the (head, query block) grid cannot fill the chip: at least 64
-    // keys per split, about 512 blocks in all (a 25-row streaming chunk over ~775 keys: 13)
+    // keys per split, about 256 blocks in all (a 25-row streaming chunk over ~775 keys: 4)
     int ks = q_pos0 - window + 1;
     if (ks < k_first) ks = k_first;
     const int keys = q_pos0 + M - ks;
     int ns = 1;
     if (ws && H * qb < 256) {
-        ns = std::min((keys + 63) / 64, std::max(1, 512 / (H * qb)));
+        // (k_attn_mf, 25 rows x 775 keys: 256 blocks 10.4 us, 512 11.8, 128 13.9, 1024 12.0)
+        const int target = g_attn_blocks ? g_attn_blocks : (g_attn_valu ? 512 : 256);
+        ns = std::min((keys + 63) / 64, std::max(1, target / (H * qb)));
         while (ns > 1 && (size_t)H * M * ns * (hd + 2) > ws_elems) ns--;
     }
     dim3 grid(H, qb, ns);

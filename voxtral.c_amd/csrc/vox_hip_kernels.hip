@@ -113,6 +113,8 @@ __device__ __forceinline__ float psum(const float* __restrict__ part, int S, int
     part += (size_t)(j >> 4) * S * SK_ROWS * N;
     j &= 15;
     float v = part[(size_t)j * N + n];
+    // unrolled: four slab loads in flight before their (in-order) adds
+#pragma unroll 4
     for (int s = 1; s < S; s++) v += part[((size_t)s * SK_ROWS + j) * N + n];
     return v;
 }
@@ -2121,6 +2123,7 @@ __global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict
         if (S > 0) {
             float r[8];
             const float* pb = part + (size_t)(j >> 4) * S * SK_ROWS * D;
+#pragma unroll 4
             for (int s = 0; s < S; s++) {
                 const float* pp = pb + ((size_t)s * SK_ROWS + (j & 15)) * D + k;
                 const float4 c = *reinterpret_cast<const float4*>(pp), d = *reinterpret_cast<const float4*>(pp + 4);

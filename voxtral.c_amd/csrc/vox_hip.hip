@@ -1422,6 +1422,8 @@ static hipStream_t g_twin_st = nullptr;
 static float* g_twin_ws = nullptr;  // split-K partials of the twin GEMMs
 static float *g_tA = nullptr, *g_tC = nullptr, *g_tQ = nullptr, *g_tK = nullptr, *g_tV = nullptr, *g_tO = nullptr;
 static size_t g_tA_n = 0, g_tC_n = 0, g_tQ_n = 0, g_tK_n = 0, g_tV_n = 0, g_tO_n = 0;
+static float* g_tWs = nullptr;  // attention key-range partials
+static size_t g_tWs_n = 0;
 
 static int twin_buf(float** p, size_t* cap, size_t n) {
     if (n <= *cap) return 0;
@@ -1537,8 +1539,16 @@ extern "C" void vox_hip_encoder_attention(float* out, const float* Q, const floa
     hipMemcpyAsync(g_tK, K, kn * 4, hipMemcpyHostToDevice, g_twin_st);
     hipMemcpyAsync(g_tV, V, kn * 4, hipMemcpyHostToDevice, g_twin_st);
     int W = window_size > 0 ? window_size : (1 << 30);
+    // few query rows: the key-range split + combine path the streaming encoder takes
+    float* ws = nullptr;
+    size_t wsn = 0;
+    if (n_heads * ((seq_q + 15) / 16) < 256) {
+        wsn = (size_t)n_heads * seq_q * 16 * (head_dim + 2);
+        if (twin_buf(&g_tWs, &g_tWs_n, wsn)) return;
+        ws = g_tWs;
+    }
     if (launch_attn_tiled(head_dim, g_tQ, n_heads * head_dim, g_tK, g_tV, seq_k, g_tO, n_heads * head_dim,
-                          seq_q, n_heads, n_kv_heads, q_offset, 0, W, scale, g_twin_st) != hipSuccess) {
+                          seq_q, n_heads, n_kv_heads, q_offset, 0, W, scale, g_twin_st, ws, wsn) != hipSuccess) {
         set_err("encoder_attention launch failed");
         return;
     }

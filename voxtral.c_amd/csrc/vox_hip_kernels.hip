@@ -3049,9 +3049,12 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
     const int S = skl_splits(K);
     if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S) return hipErrorInvalidValue;
     const int ks = K / 64 / S;
-    // waves (row groups) per block: 8 for the narrow outputs (wo / w2: 3072 x 4096 7.8 -> 7.1
-    // us at 16 rows), 4 for the wide ones (QKV 6144 x 3072: 11.4 -> 10.2 us; W1|W3 even)
-    int nw = g_skl_nw ? g_skl_nw : (N <= 4096 && N % 128 == 0 ? 8 : 4);
+    // waves (row groups) per block, by the 8-wave grid size (N / 128) * S: narrow outputs take
+    // 8 from 128 blocks (decoder wo 3072 x 4096: 7.8 -> 7.1 us at 16 rows; the encoder's wo /
+    // w2 at 40 / 100 blocks stay at 4), wide ones from 384 (decoder QKV 6144 x 3072 at 288:
+    // 11.4 -> 10.2 us with 4; encoder W1|W3 at 400 keeps 8)
+    const int nb8 = (N / 128) * S;
+    int nw = g_skl_nw ? g_skl_nw : (N % 128 == 0 && nb8 >= (N <= 4096 ? 128 : 384) ? 8 : 4);
     if (N % (16 * nw)) nw = 4;
     if (N % (16 * nw)) return hipErrorInvalidValue;
 #define SKL_X(Q, NWW, KSS) \

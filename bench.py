@@ -15,13 +15,19 @@ Metric: value = decoder tokens/s summed over ranks (prefill excluded, as voxtral
 1363-1368 reports it) = total greedy steps / max over ranks of decode time.
 encoder_rtf = encoder time / audio time (conv stem + encoder + adapter, voxtral.c:842-940).
 
-Multi-GPU: one process per GPU (torch.distributed.run), each an independent replica with
-its own stream (streams shard embarrassingly, SURVEY.md 8e: no collective on the data
-path); gloo carries only the barrier and the max-over-ranks timing.
+Multi-GPU: one process per GPU, each an independent replica with its own stream(s)
+(streams shard embarrassingly, SURVEY.md 8e: no collective on the data path); gloo carries
+only the barrier and the max/sum over ranks.  Under torch.distributed.run the ranks come
+from the environment (WORLD_SIZE must equal --gpus); `python bench.py --gpus N` without it
+starts the N rank processes itself (before anything touches a GPU) and relays rank 0's line.
+`--dry-run` runs the same harness with a host-only placeholder step (no GPU, no model): it
+exists so the CPU tests can exercise the launcher and the over-ranks reduction.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +39,7 @@ import numpy as np  # noqa: E402
 JFK_CHUNKS = [1355, 140, 1]      # mel frames per encoder call
 AUDIO_SECONDS = 176000 / 16000.0  # samples/jfk.wav
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+MFMA_BF16_TFLOPS = 2500.0        # dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 MPS_TOK_S = 1000.0 / 23.5        # M3 Max MPS decoder step, short clip (README.md:323)
 
 
@@ -52,7 +59,34 @@ def parse():
                     help="config 3: raw audio fed in -I-sized pieces through the device mel + chunked encoder")
     ap.add_argument("--audio-seconds", type=float, default=180.0, help="config 3 audio length")
     ap.add_argument("--interval", type=float, default=0.5, help="config 3 -I interval (s)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="harness check without a GPU: placeholder host step, same launcher and JSON")
     return ap.parse_args()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """One process per GPU, started here before any GPU call in this process (a parent
+    that touched the GPU must not fork/exec workers).  Each child gets RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* like torch.distributed.run would set; rank 0 prints the line."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    return rc
 
 
 class Dist:
@@ -60,6 +94,8 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != n:
+            raise SystemExit(f"bench.py: WORLD_SIZE={self.world} but --gpus {n}")
         self.torch = None
         if self.world > 1:
             import torch
@@ -127,7 +163,7 @@ def cpu_baseline(cfg, weights, mel, n_steps, q8=False):
     bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import vox_oracle
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     om = vox_oracle.OracleModel(cfg, weights)
     st = vox_oracle.OracleStream(om)
     vox_oracle.set_threads(threads)        # sgemm threads for the M>1 encoder/prefill
@@ -152,12 +188,59 @@ def cpu_baseline(cfg, weights, mel, n_steps, q8=False):
                        + f"); encoder = the 3 jfk chunks with {threads}-thread OpenBLAS sgemm"),
             "ms_per_token": round(ms_step, 2),
             "encoder_rtf": round((t1 - t0) / AUDIO_SECONDS, 4),
-            "encoder_threads": threads}
+            "encoder_threads": threads, "cpu_model": cpu_model(), "host_cpus": len(os.sched_getaffinity(0))}
+
+
+def host_threads():
+    """nproc (the CPUs this process may run on), capped by OMP_NUM_THREADS when the host
+    sets it: the GPU box exports 16, its share of a machine whose nproc counts every CPU."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(cap))) if cap.isdigit() and int(cap) > 0 else n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def encoder_flops(cfg, mel_chunks):
+    """Useful FLOPs of one stream_run_encoder pass over the given mel chunks (conv stem,
+    encoder layers incl. windowed attention, adapter), following the
+    stride-2 residual and the 4-row downsample carry of voxtral.c:653-692, 868-934."""
+    MB, ED, H, hd, EH = cfg.mel_bins, cfg.enc_dim, cfg.enc_heads, cfg.enc_head_dim, cfg.enc_hidden
+    EQ, EKV, D = H * hd, cfg.enc_kv_heads * hd, cfg.dec_dim
+    per_row = 2 * ED * (EQ + 2 * EKV) + 2 * EQ * ED + 2 * ED * 2 * EH + 2 * EH * ED
+    res = pos = carry = 0
+    fl = 0.0
+    for n in mel_chunks:
+        fl += 2.0 * n * (MB * 3) * ED                      # conv0 (k3 s1)
+        tot = res + n
+        res = tot & 1
+        t1 = (tot - res) // 2
+        fl += 2.0 * t1 * (ED * 3) * ED                     # conv1 (k3 s2)
+        for i in range(t1):                                # layers: projections + attention
+            keys = min(pos + i + 1, cfg.enc_window)
+            fl += cfg.enc_layers * (per_row + 4.0 * H * hd * keys)
+        pos += t1
+        usable = (carry + t1) // 4
+        carry = (carry + t1) % 4
+        fl += 2.0 * usable * (4 * ED * D + D * D)          # adapter
+    return fl
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     d = Dist(args.gpus)
+    if args.dry_run:
+        return dry_run(args, d)
     import vox_hip
     from vox_weights import VOXTRAL_4B, quantize_q8, synth_weights
     vox_hip.init(device=d.local)
@@ -250,6 +333,25 @@ def main():
                      "avg_launch_us": round(avg_ms * 1000.0, 3) if prof["launches"] else None,
                      "launches_timed": prof["launches"]},
     }
+    # per-token roofline of the whole decode step: weights + the KV rows attention reads
+    # (f32 K and V, positions 39..186 of the jfk schedule), SURVEY.md 8d
+    L_avg = (39 + 38 + steps_local // args.steps) / 2.0
+    w_tok = (6857687040 // 2) if args.q8 else 6857687040
+    tok_bytes = w_tok + 2 * cfg.dec_layers * cfg.dec_kv_heads * cfg.dec_head_dim * 4 * L_avg
+    ms_tok = dec_s * 1000.0 / max(1, steps_local)
+    out["decoder_roofline"] = {"bound": "hbm", "bytes_per_token": int(tok_bytes),
+                               "achieved": round(tok_bytes / (ms_tok * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(tok_bytes / (ms_tok * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    # encoder (one-shot 1355/140/1 chunks, M = 677 rows: above the MFMA ridge): useful FLOPs
+    # over the whole conv + encoder + adapter time vs the dense bf16 MFMA peak.  The GEMMs
+    # issue 3 bf16 MFMAs per product (hi/mid/lo split of the f32 activations), so the
+    # issued-MFMA fraction is ~3x the useful one.
+    efl = encoder_flops(cfg, JFK_CHUNKS)
+    enc_tf = efl / (enc_s / args.steps) / 1e12
+    out["encoder_roofline"] = {"bound": "mfma", "flops_per_pass": int(efl), "achieved": round(enc_tf, 1),
+                               "peak": MFMA_BF16_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(enc_tf / MFMA_BF16_TFLOPS, 4), "mfma_planes": 3,
+                               "issued_frac": round(3 * enc_tf / MFMA_BF16_TFLOPS, 4)}
     if keep_host:
         out["cpu_baseline"] = cpu_baseline(cfg, w, mel, args.cpu_steps, q8=args.q8)
     if d.rank == 0:
@@ -257,6 +359,31 @@ def main():
     mel_dev.free()
     st.close()
     model.close()
+
+
+def dry_run(args, d):
+    """The launcher / reduction path without a GPU: every rank times `steps` placeholder
+    host steps (a small numpy matmul standing in for a transcription) between the same
+    barriers and reports the same aggregate fields.  Not a measurement of the engine."""
+    a = np.random.default_rng(d.rank).standard_normal((256, 256)).astype(np.float32)
+    for _ in range(args.warmup):
+        a @ a
+    d.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a = (a @ a) / np.float32(16.0)
+    t1 = time.perf_counter()
+    d.barrier()
+    wall = d.max(t1 - t0)
+    steps_all = d.sum(args.steps * args.streams)
+    out = {"metric": "bench.py harness dry run (no GPU; placeholder host step)", "value": round(steps_all / wall, 2),
+           "unit": "steps/s", "n_gpus": d.world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(wall * 1000.0 / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic", "dry_run": True,
+           "config": {"workload": "placeholder", "global_batch": d.world * args.streams,
+                      "streams_per_gpu": args.streams, "parallelism": f"replicas x{d.world} (no collective)"}}
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def synth_audio(seconds, seed):

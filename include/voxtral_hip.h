@@ -41,7 +41,8 @@ int vox_hip_init(void);          /* voxtral_metal.h:20  vox_metal_init: 1 on suc
 int vox_hip_available(void);     /* voxtral_metal.h:23  vox_metal_available */
 void vox_hip_shutdown(void);     /* voxtral_metal.h:26  vox_metal_shutdown */
 size_t vox_hip_memory_used(void);/* voxtral_metal.h:282 vox_metal_memory_used */
-const char *vox_hip_last_error(void);
+const char *vox_hip_last_error(void);  /* "" when no error since the last clear */
+void vox_hip_clear_error(void);          /* the void twins below report only through last_error */
 int vox_hip_set_device(int device);
 
 /* ------------------------------------------------------------------------

@@ -206,6 +206,18 @@ class OracleStream:
         mel = np.ascontiguousarray(mel, np.float32)
         return lib().vo_stream_encode_mel(self.h, f(mel), mel.shape[0])
 
+    def decoder_prefill(self, embeds):
+        """vox_decoder_prefill (voxtral_decoder.c:447-612) on embeds [n, dec_dim]"""
+        e = np.ascontiguousarray(embeds, np.float32)
+        lib().vo_decoder_prefill(self.h, f(e), e.shape[0])
+
+    def decoder_forward(self, embed):
+        """vox_decoder_forward (voxtral_decoder.c:640-780): (argmax id, logits)"""
+        e = np.ascontiguousarray(embed, np.float32)
+        logits = np.empty(self.cfg.vocab, np.float32)
+        tok = lib().vo_decoder_forward(self.h, f(e), f(logits))
+        return tok, logits
+
     @property
     def adapter_tokens(self):
         return lib().vo_stream_adapter_tokens(self.h)

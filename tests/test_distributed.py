@@ -44,3 +44,28 @@ def test_bench_dist_world2(tmp_path):
     assert sorted(o["rank"] for o in outs) == [0, 1]
     for o in outs:
         assert o["world"] == 2 and o["max"] == 2.5 and o["sum"] == 30.0
+
+
+def test_bench_launcher_dry_run_world2():
+    """`python bench.py --gpus 2` starts its own two ranks (no torch.distributed.run) and
+    rank 0 prints one line with n_gpus 2 and the summed value (host placeholder step)."""
+    import json
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
+                        "--warmup", "1", "--dry-run", "--streams", "8"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    o = lines[0]
+    assert o["n_gpus"] == 2 and o["dry_run"] and o["config"]["global_batch"] == 16
+    assert o["value"] == pytest.approx(2 * 4 * 8 / (o["ms_per_step"] * 4 / 1000.0), rel=0.02)
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -3,7 +3,7 @@ CPU oracle on the reference's jfk.wav one-shot transcription (vox_transcribe_aud
 1355/140/1 mel-frame encoder chunks, 38-row prefill, 149 greedy tokens.
 
 Tolerances (north_star: "identical greedy token ids and logits within a stated fp
-tolerance"): token ids identical; adapter rows and logits within 1e-3 of the largest
+tolerance"): token ids identical; adapter rows and logits within 5e-5 of the largest
 magnitude (f32 arithmetic, different summation order)."""
 import os
 
@@ -12,7 +12,7 @@ import pytest
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
-TOL = 1e-3
+TOL = 5e-5
 
 
 def rel(a, b):

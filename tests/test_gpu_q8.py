@@ -5,7 +5,7 @@ voxtral_kernels.c:277-393, voxtral.c:443-451; oracle pinned in tests/test_q8_cpu
 The HIP kernels compute scale * sum(x * q) (int8 exact in bf16 / f32); the reference's
 M>1 path sums x * (q * scale) after rounding each dequantised weight to f32, so results
 agree to f32 rounding, not bitwise.  Tolerances: greedy ids identical; adapter rows and
-logits within 1e-3 of the largest magnitude (as the bf16 tests)."""
+logits within 5e-5 of the largest magnitude (as the bf16 tests)."""
 import os
 
 import numpy as np
@@ -13,7 +13,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-TOL = 1e-3
+TOL = 5e-5
 
 
 def rel(a, b):

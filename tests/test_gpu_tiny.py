@@ -1,7 +1,7 @@
 """End-to-end parity of the HIP path against the CPU oracle on the TINY configuration
 (same structure and head dims as Voxtral-4B, short windows so the rolling KV wraps).
 
-Tolerances: greedy ids must be identical; logits within 1e-3 relative to the largest
+Tolerances: greedy ids must be identical; logits within 5e-5 relative to the largest
 logit magnitude (f32 arithmetic with a different summation order; the MFMA GEMMs use the
 exact 3-term bf16 split of the activations)."""
 import numpy as np
@@ -9,8 +9,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-LOGIT_TOL = 1e-3
-ADAPTER_TOL = 1e-3
+LOGIT_TOL = 5e-5
+ADAPTER_TOL = 5e-5
 
 
 def rel(a, b):

@@ -17,6 +17,7 @@
 
 #include <stddef.h>
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -77,6 +78,7 @@ static void dfree(T*& p) {
 }
 
 extern "C" const char* vox_hip_last_error(void) { return g_err.c_str(); }
+extern "C" void vox_hip_clear_error(void) { g_err.clear(); }
 
 extern "C" int vox_hip_init(void) {
     int n = 0;
@@ -449,6 +451,7 @@ static const size_t GEMM_WS_ELEMS = (size_t)8 << 20;  // split-K workspace (32 M
 struct vox_hip_stream {
     vox_hip_stream() { memset((void*)this, 0, offsetof(vox_hip_stream, pev)); }
     vox_hip_model_t* m;
+    unsigned long long uid;  // unique per stream object ever created (batch graph keys)
     hipStream_t st;
     // rolling KV caches [layers][cap][kv_dim]
     float *ek, *ev, *dk, *dv;
@@ -478,7 +481,8 @@ struct vox_hip_stream {
     float alt_cutoff;
     int graph_alt;           // alt mode the step graphs were captured with
     int graph_rope_gen;      // model rope table generation the step graphs were captured with
-    int *pidx, *state, *tokens;
+    int *pidx, *state, *tokens;   // tokens: ring of tokens_cap ids, index = step % tokens_cap
+    int* twin_state;              // decoder_full_step's argmax state (the graph state stays untouched)
     int dec_rows_cap, tokens_cap;
     hipGraphExec_t step_exec[STEP_GRAPHS];  // [g]: attention with 2^g key splits (g = 0: no combine)
     int graph_ready;              // bit mask of built graphs
@@ -547,8 +551,10 @@ static int stream_alloc_dec_rows(vox_hip_stream_t* s, int rows) {
 extern "C" void vox_hip_stream_free(vox_hip_stream_t* s);
 
 extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
+    static std::atomic<unsigned long long> next_uid{1};
     vox_hip_stream_t* s = new vox_hip_stream_t();
     s->m = m;
+    s->uid = next_uid++;
     const vox_hip_config_t& c = m->c;
     auto fail = [&]() -> vox_hip_stream_t* { vox_hip_stream_free(s); return nullptr; };
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
@@ -580,6 +586,7 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->pval, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->state, 4));
+    TRYH(dalloc(&s->twin_state, 4));
     s->tokens_cap = 1 << 16;
     TRYH(dalloc(&s->tokens, s->tokens_cap));
     TRYH(dalloc(&s->alts, (size_t)s->tokens_cap * ALT_REC));
@@ -604,7 +611,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->im2col); dfree(s->x_enc); dfree(s->xn); dfree(s->qkv); dfree(s->q); dfree(s->att);
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
-    dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->tokens);
+    dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
     dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
@@ -1261,6 +1268,20 @@ static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
     return 0;
 }
 
+// copy ring entries [first, first + n) of a per-step device log (rec ints / floats per entry)
+template <class T>
+static int ring_read(const T* ring, int cap, int rec, long long first, int n, T* out, hipStream_t st) {
+    while (n > 0) {
+        const int slot = (int)(first % cap);
+        const int k = std::min(n, cap - slot);
+        CK(hipMemcpyAsync(out, ring + (size_t)slot * rec, (size_t)k * rec * sizeof(T), hipMemcpyDeviceToHost, st));
+        out += (size_t)k * rec;
+        first += k;
+        n -= k;
+    }
+    return 0;
+}
+
 extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int stop_at_eos,
                                      int* tokens_out, float* logits_out) {
     vox_hip_model_t* m = s->m;
@@ -1296,7 +1317,6 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
     // step input for the first step of this call (later inputs are built by the previous
     // step's argmax kernel)
     if (avail > 0) CK(launch_embed_step(s->adapter, m->tok_emb, m->tok_emb_s, s->state, D, s->xd, s->st));
-    if (s->n_generated + avail > s->tokens_cap) avail = s->tokens_cap - s->n_generated;
     int todo = std::min(max_steps, avail);
     std::vector<int> tok;
     while (produced < todo) {
@@ -1304,8 +1324,8 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
         if (logits_out) b = 1;
         if (run_steps(s, b, s->h_state[0] + produced)) return -1;
         tok.resize(produced + b);
-        CK(hipMemcpyAsync(tok.data() + produced, s->tokens + step_base + produced, (size_t)b * 4,
-                          hipMemcpyDeviceToHost, s->st));
+        if (ring_read(s->tokens, s->tokens_cap, 1, (long long)step_base + produced, b, tok.data() + produced, s->st))
+            return -1;
         if (logits_out)
             CK(hipMemcpyAsync(logits_out + (size_t)produced * V, s->logits, (size_t)V * 4, hipMemcpyDeviceToHost, s->st));
         CK(hipStreamSynchronize(s->st));
@@ -1352,12 +1372,14 @@ extern "C" int vox_hip_stream_set_alt(vox_hip_stream_t* s, int n_alt, float cuto
 // beyond n_alt).  probs_out (optional) holds the matching softmax probabilities.
 extern "C" int vox_hip_stream_read_alts(vox_hip_stream_t* s, int first, int n, int* ids_out,
                                         float* probs_out) {
-    if (!s || first < 0 || n < 0 || first + n > s->n_generated) return set_err("alt range out of bounds");
+    if (!s || first < 0 || n < 0 || first + n > s->n_generated || first < s->n_generated - s->tokens_cap)
+        return set_err("alt range out of bounds (the last %d steps are kept)", s->tokens_cap);
     if (n == 0) return 0;
     std::vector<float> rec((size_t)n * ALT_REC);
     std::vector<int> tok(n);
-    CK(hipMemcpyAsync(rec.data(), s->alts + (size_t)first * ALT_REC, rec.size() * 4, hipMemcpyDeviceToHost, s->st));
-    CK(hipMemcpyAsync(tok.data(), s->tokens + first, (size_t)n * 4, hipMemcpyDeviceToHost, s->st));
+    if (ring_read(s->alts, s->tokens_cap, ALT_REC, first, n, rec.data(), s->st) ||
+        ring_read(s->tokens, s->tokens_cap, 1, first, n, tok.data(), s->st))
+        return -1;
     CK(hipStreamSynchronize(s->st));
     for (int i = 0; i < n; i++) {
         int* ids = ids_out + (size_t)i * VOX_HIP_MAX_ALT;
@@ -1415,9 +1437,30 @@ extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
 
 // ---------------------------------------------------------------------------
 // Reference-boundary twins (host pointers; voxtral_metal.h)
+//
+// Any M, N, K: a weight is uploaded once per (host pointer, N, K) into a zero-padded
+// [Np, Kp] device copy (Np a multiple of 128, Kp of 64: the k_gemm2 tile), the activation
+// rows go into [M, Kp] with zero columns, and C comes back through a pitched copy, so the
+// padding never reaches the caller.  M = 1 takes the GEMV when the padded shape suits it.
+// Every HIP call is checked; the void functions report through vox_hip_last_error().
 // ---------------------------------------------------------------------------
+struct TwinW {
+    uint8_t* w;   // [Np, Kp] bf16 or int8
+    float* s;     // Q8 row scales [Np] (null: bf16)
+    int N, K, Np, Kp;
+};
+struct TwinKey {
+    const void* p;
+    int n, k;
+    bool operator==(const TwinKey& o) const { return p == o.p && n == o.n && k == o.k; }
+};
+struct TwinKeyHash {
+    size_t operator()(const TwinKey& t) const {
+        return std::hash<const void*>()(t.p) ^ ((size_t)t.n * 0x9e3779b97f4a7c15ull) ^ ((size_t)t.k << 1);
+    }
+};
 static std::mutex g_twin_mu;
-static std::unordered_map<const void*, uint8_t*> g_wcache;  // host weight ptr -> device copy
+static std::unordered_map<TwinKey, TwinW, TwinKeyHash> g_wcache;  // (host ptr, N, K) -> device copy
 static hipStream_t g_twin_st = nullptr;
 static float* g_twin_ws = nullptr;  // split-K partials of the twin GEMMs
 static float *g_tA = nullptr, *g_tC = nullptr, *g_tQ = nullptr, *g_tK = nullptr, *g_tV = nullptr, *g_tO = nullptr;
@@ -1425,75 +1468,134 @@ static size_t g_tA_n = 0, g_tC_n = 0, g_tQ_n = 0, g_tK_n = 0, g_tV_n = 0, g_tO_n
 static float* g_tWs = nullptr;  // attention key-range partials
 static size_t g_tWs_n = 0;
 
+static int pad_to(int v, int a) { return (v + a - 1) / a * a; }
+
 static int twin_buf(float** p, size_t* cap, size_t n) {
     if (n <= *cap) return 0;
     dfree(*p);
+    *cap = 0;
     CK(dalloc(p, n));
     *cap = n;
     return 0;
 }
 
-static uint8_t* twin_weight(const void* host, size_t bytes) {
-    auto it = g_wcache.find(host);
-    if (it != g_wcache.end()) return it->second;
-    uint8_t* d = nullptr;
-    if (dalloc(&d, bytes) != hipSuccess) { set_err("weight alloc failed"); return nullptr; }
-    if (h2d(d, host, bytes) != hipSuccess) { set_err("weight upload failed"); return nullptr; }
-    g_wcache[host] = d;
-    return d;
+// device copy of a host weight [N, K] (+ Q8 row scales), zero-padded to the GEMM tile
+static const TwinW* twin_weight(const void* host, const float* scales, int N, int K) {
+    if (!host || N <= 0 || K <= 0) {
+        set_err("twin weight: null pointer or empty shape (%d x %d)", N, K);
+        return nullptr;
+    }
+    const TwinKey key{host, N, K};
+    auto it = g_wcache.find(key);
+    if (it != g_wcache.end()) return &it->second;
+    TwinW t{nullptr, nullptr, N, K, pad_to(N, 128), pad_to(K, 64)};
+    const size_t esz = scales ? 1 : 2;
+    hipError_t e = dalloc(&t.w, (size_t)t.Np * t.Kp * esz);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(t.w, (size_t)t.Kp * esz, host, (size_t)K * esz, (size_t)K * esz, N,
+                             hipMemcpyHostToDevice, g_twin_st);
+    if (e == hipSuccess && scales) {
+        e = dalloc(&t.s, (size_t)t.Np);
+        if (e == hipSuccess) e = hipMemcpyAsync(t.s, scales, (size_t)N * 4, hipMemcpyHostToDevice, g_twin_st);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(g_twin_st);
+    if (e != hipSuccess) {
+        dfree(t.w);
+        dfree(t.s);
+        set_err("twin weight upload (%d x %d): %s", N, K, hipGetErrorString(e));
+        return nullptr;
+    }
+    return &(g_wcache[key] = t);
 }
 
 static int twin_init() {
     if (!g_inited && !vox_hip_init()) return -1;
     if (!g_twin_st) CK(hipStreamCreateWithFlags(&g_twin_st, hipStreamNonBlocking));
+    if (!g_twin_ws) CK(dalloc(&g_twin_ws, GEMM_WS_ELEMS));
     return 0;
 }
 
-static int twin_gemm(int M, int N, int K, const float* dA, const void* dW, const float* dS, float* dC) {
-    if (M == 1 && N % GEMV_RB == 0 && K % (dS ? 16 : 8) == 0 && K <= 5 * 2048) {
+// host rows [M, K] -> device [M, Kp] (zero columns past K)
+static int twin_put_rows(float** buf, size_t* cap, const float* host, int M, int K, int Kp) {
+    if (!host) return set_err("twin: null input");
+    if (twin_buf(buf, cap, (size_t)M * Kp)) return -1;
+    if (Kp != K) {
+        CK(hipMemsetAsync(*buf, 0, (size_t)M * Kp * 4, g_twin_st));
+        CK(hipMemcpy2DAsync(*buf, (size_t)Kp * 4, host, (size_t)K * 4, (size_t)K * 4, M, hipMemcpyHostToDevice,
+                            g_twin_st));
+    } else {
+        CK(hipMemcpyAsync(*buf, host, (size_t)M * K * 4, hipMemcpyHostToDevice, g_twin_st));
+    }
+    return 0;
+}
+
+// device [M, Np] -> host [M, N]
+static int twin_get_rows(float* host, const float* dev, int M, int N, int Np) {
+    if (!host) return set_err("twin: null output");
+    CK(hipMemcpy2DAsync(host, (size_t)N * 4, dev, (size_t)Np * 4, (size_t)N * 4, M, hipMemcpyDeviceToHost, g_twin_st));
+    return 0;
+}
+
+// dC[M, W.Np] = dA[M, W.Kp] . W^T on the twin stream
+static int twin_gemm_dev(int M, const float* dA, const TwinW& W, float* dC) {
+    if (M == 1 && gemv_ok(W.Np, W.Kp, W.s != nullptr)) {
         GemvArgs a;
         memset(&a, 0, sizeof a);
-        a.x = dA; a.K = K; a.W = dW; a.wscale = dS; a.rows = N; a.y = dC;
+        a.x = dA; a.K = W.Kp; a.W = W.w; a.wscale = W.s; a.rows = W.Np; a.y = dC;
         CK(launch_gemv(PRO_NONE, EPI_STORE, a, g_twin_st));
         return 0;
     }
-    if (!g_twin_ws) CK(dalloc(&g_twin_ws, GEMM_WS_ELEMS));
-    CK(launch_gemm(EPI_STORE, 3, dA, K, dW, dS, K, M, N, nullptr, dC, N, g_twin_st, g_twin_ws, GEMM_WS_ELEMS));
+    CK(launch_gemm(EPI_STORE, 3, dA, W.Kp, W.w, W.s, W.Kp, M, W.Np, nullptr, dC, W.Np, g_twin_st, g_twin_ws,
+                   GEMM_WS_ELEMS));
+    return 0;
+}
+
+static int twin_sgemm(int M, int N, int K, const float* A, const void* B, const float* scales, float* C) {
+    if (M <= 0 || N <= 0 || K <= 0) return M == 0 ? 0 : set_err("sgemm: bad shape %d x %d x %d", M, N, K);
+    if (twin_init()) return -1;
+    const TwinW* W = twin_weight(B, scales, N, K);
+    if (!W) return -1;
+    if (twin_put_rows(&g_tA, &g_tA_n, A, M, K, W->Kp) || twin_buf(&g_tC, &g_tC_n, (size_t)M * W->Np) ||
+        twin_gemm_dev(M, g_tA, *W, g_tC) || twin_get_rows(C, g_tC, M, N, W->Np))
+        return -1;
+    CK(hipStreamSynchronize(g_twin_st));
     return 0;
 }
 
 extern "C" void vox_hip_sgemm_bf16(int M, int N, int K, const float* A, const uint16_t* B, float* C) {
     std::lock_guard<std::mutex> lk(g_twin_mu);
-    if (twin_init()) return;
-    uint8_t* dW = twin_weight(B, (size_t)N * K * 2);
-    if (!dW) return;
-    if (twin_buf(&g_tA, &g_tA_n, (size_t)M * K) || twin_buf(&g_tC, &g_tC_n, (size_t)M * N)) return;
-    if (hipMemcpyAsync(g_tA, A, (size_t)M * K * 4, hipMemcpyHostToDevice, g_twin_st) != hipSuccess) { set_err("upload"); return; }
-    if (twin_gemm(M, N, K, g_tA, dW, nullptr, g_tC)) return;
-    if (hipMemcpyAsync(C, g_tC, (size_t)M * N * 4, hipMemcpyDeviceToHost, g_twin_st) != hipSuccess) { set_err("download"); return; }
-    hipStreamSynchronize(g_twin_st);
+    twin_sgemm(M, N, K, A, B, nullptr, C);
 }
 
 extern "C" void vox_hip_sgemm_q8(int M, int N, int K, const float* A, const int8_t* B, const float* scales,
                                  float* C) {
     std::lock_guard<std::mutex> lk(g_twin_mu);
-    if (twin_init()) return;
-    uint8_t* dW = twin_weight(B, (size_t)N * K);
-    uint8_t* dS = twin_weight(scales, (size_t)N * 4);
-    if (!dW || !dS) return;
-    if (twin_buf(&g_tA, &g_tA_n, (size_t)M * K) || twin_buf(&g_tC, &g_tC_n, (size_t)M * N)) return;
-    if (hipMemcpyAsync(g_tA, A, (size_t)M * K * 4, hipMemcpyHostToDevice, g_twin_st) != hipSuccess) { set_err("upload"); return; }
-    if (twin_gemm(M, N, K, g_tA, dW, reinterpret_cast<const float*>(dS), g_tC)) return;
-    if (hipMemcpyAsync(C, g_tC, (size_t)M * N * 4, hipMemcpyDeviceToHost, g_twin_st) != hipSuccess) { set_err("download"); return; }
-    hipStreamSynchronize(g_twin_st);
+    if (!scales) { set_err("sgemm_q8: null scales"); return; }
+    twin_sgemm(M, N, K, A, B, scales, C);
 }
 
+// voxtral_metal.m:1274-1414: the input uploaded once, three projections into three arrays
 extern "C" void vox_hip_fused_qkv_bf16(int M, int K, const float* input, const uint16_t* wq, int Nq,
                                        const uint16_t* wk, int Nk, const uint16_t* wv, int Nv,
                                        float* q, float* k, float* v) {
-    vox_hip_sgemm_bf16(M, Nq, K, input, wq, q);
-    vox_hip_sgemm_bf16(M, Nk, K, input, wk, k);
-    vox_hip_sgemm_bf16(M, Nv, K, input, wv, v);
+    std::lock_guard<std::mutex> lk(g_twin_mu);
+    if (M <= 0) return;
+    if (twin_init()) return;
+    const TwinW* W[3] = {twin_weight(wq, nullptr, Nq, K), twin_weight(wk, nullptr, Nk, K),
+                         twin_weight(wv, nullptr, Nv, K)};
+    if (!W[0] || !W[1] || !W[2]) return;
+    float* outs[3] = {q, k, v};
+    float* dO[3] = {nullptr, nullptr, nullptr};
+    size_t* caps[3] = {&g_tQ_n, &g_tK_n, &g_tV_n};
+    float** bufs[3] = {&g_tQ, &g_tK, &g_tV};
+    if (twin_put_rows(&g_tA, &g_tA_n, input, M, K, W[0]->Kp)) return;
+    for (int i = 0; i < 3; i++) {
+        if (twin_buf(bufs[i], caps[i], (size_t)M * W[i]->Np) || twin_gemm_dev(M, g_tA, *W[i], *bufs[i])) return;
+        dO[i] = *bufs[i];
+    }
+    for (int i = 0; i < 3; i++)
+        if (twin_get_rows(outs[i], dO[i], M, W[i]->N, W[i]->Np)) return;
+    if (hipStreamSynchronize(g_twin_st) != hipSuccess) set_err("fused_qkv: sync failed");
 }
 
 __global__ void k_silu_mul(float* g, const float* u, size_t n) {
@@ -1504,56 +1606,67 @@ __global__ void k_silu_mul(float* g, const float* u, size_t n) {
     }
 }
 
+// voxtral_metal.m:1416-1572: (silu(x w1^T) * x w3^T) w2^T; the caller adds the w2 bias
 extern "C" void vox_hip_fused_ffn_bf16(int M, int dim, int hidden, const float* input,
                                        const uint16_t* w1, const uint16_t* w3, const uint16_t* w2,
                                        float* output) {
     std::lock_guard<std::mutex> lk(g_twin_mu);
+    if (M <= 0) return;
     if (twin_init()) return;
-    uint8_t* d1 = twin_weight(w1, (size_t)hidden * dim * 2);
-    uint8_t* d3 = twin_weight(w3, (size_t)hidden * dim * 2);
-    uint8_t* d2 = twin_weight(w2, (size_t)dim * hidden * 2);
+    const TwinW* d1 = twin_weight(w1, nullptr, hidden, dim);
+    const TwinW* d3 = twin_weight(w3, nullptr, hidden, dim);
+    const TwinW* d2 = twin_weight(w2, nullptr, dim, hidden);
     if (!d1 || !d3 || !d2) return;
-    if (twin_buf(&g_tA, &g_tA_n, (size_t)M * dim) || twin_buf(&g_tQ, &g_tQ_n, (size_t)M * hidden) ||
-        twin_buf(&g_tK, &g_tK_n, (size_t)M * hidden) || twin_buf(&g_tC, &g_tC_n, (size_t)M * dim))
+    // gate / up rows [M, Hp]; the padded hidden columns are silu(0) * 0 = 0 and meet the
+    // zero K padding of w2
+    const int Hp = d1->Np;
+    if (d2->Kp != Hp) { set_err("fused_ffn: padded hidden %d != %d", d2->Kp, Hp); return; }
+    if (twin_put_rows(&g_tA, &g_tA_n, input, M, dim, d1->Kp) || twin_buf(&g_tQ, &g_tQ_n, (size_t)M * Hp) ||
+        twin_buf(&g_tK, &g_tK_n, (size_t)M * Hp) || twin_buf(&g_tC, &g_tC_n, (size_t)M * d2->Np) ||
+        twin_gemm_dev(M, g_tA, *d1, g_tQ) || twin_gemm_dev(M, g_tA, *d3, g_tK))
         return;
-    hipMemcpyAsync(g_tA, input, (size_t)M * dim * 4, hipMemcpyHostToDevice, g_twin_st);
-    if (twin_gemm(M, hidden, dim, g_tA, d1, nullptr, g_tQ) || twin_gemm(M, hidden, dim, g_tA, d3, nullptr, g_tK)) return;
-    size_t n = (size_t)M * hidden;
-    hipLaunchKernelGGL(k_silu_mul, dim3((n + 255) / 256), dim3(256), 0, g_twin_st, g_tQ, g_tK, n);
-    if (twin_gemm(M, dim, hidden, g_tQ, d2, nullptr, g_tC)) return;
-    hipMemcpyAsync(output, g_tC, (size_t)M * dim * 4, hipMemcpyDeviceToHost, g_twin_st);
-    hipStreamSynchronize(g_twin_st);
+    const size_t n = (size_t)M * Hp;
+    hipLaunchKernelGGL(k_silu_mul, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, g_twin_st, g_tQ, g_tK, n);
+    if (hipGetLastError() != hipSuccess) { set_err("fused_ffn: silu_mul launch failed"); return; }
+    if (twin_gemm_dev(M, g_tQ, *d2, g_tC) || twin_get_rows(output, g_tC, M, dim, d2->Np)) return;
+    if (hipStreamSynchronize(g_twin_st) != hipSuccess) set_err("fused_ffn: sync failed");
+}
+
+static int twin_attention(float* out, const float* Q, const float* K, const float* V, int seq_q, int seq_k,
+                          int n_heads, int n_kv_heads, int head_dim, float scale, int window_size, int q_offset) {
+    if (twin_init()) return -1;
+    if (seq_q <= 0) return 0;
+    if (!out || !Q || !K || !V) return set_err("encoder_attention: null pointer");
+    if (q_offset < 0 || q_offset + seq_q > seq_k) return set_err("encoder_attention: queries beyond keys");
+    if (n_kv_heads <= 0 || n_heads % n_kv_heads) return set_err("encoder_attention: heads %d / kv heads %d", n_heads, n_kv_heads);
+    const size_t qn = (size_t)seq_q * n_heads * head_dim, kn = (size_t)seq_k * n_kv_heads * head_dim;
+    if (twin_buf(&g_tQ, &g_tQ_n, qn) || twin_buf(&g_tK, &g_tK_n, kn) || twin_buf(&g_tV, &g_tV_n, kn) ||
+        twin_buf(&g_tO, &g_tO_n, qn))
+        return -1;
+    CK(hipMemcpyAsync(g_tQ, Q, qn * 4, hipMemcpyHostToDevice, g_twin_st));
+    CK(hipMemcpyAsync(g_tK, K, kn * 4, hipMemcpyHostToDevice, g_twin_st));
+    CK(hipMemcpyAsync(g_tV, V, kn * 4, hipMemcpyHostToDevice, g_twin_st));
+    const int W = window_size > 0 ? window_size : (1 << 30);
+    // few query rows: the key-range split + combine path the streaming encoder takes
+    float* ws = nullptr;
+    size_t wsn = 0;
+    if (n_heads * ((seq_q + 15) / 16) < 256) {
+        wsn = (size_t)n_heads * seq_q * 16 * (head_dim + 2);
+        if (twin_buf(&g_tWs, &g_tWs_n, wsn)) return -1;
+        ws = g_tWs;
+    }
+    CK(launch_attn_tiled(head_dim, g_tQ, n_heads * head_dim, g_tK, g_tV, seq_k, g_tO, n_heads * head_dim, seq_q,
+                         n_heads, n_kv_heads, q_offset, 0, W, scale, g_twin_st, ws, wsn));
+    CK(hipMemcpyAsync(out, g_tO, qn * 4, hipMemcpyDeviceToHost, g_twin_st));
+    CK(hipStreamSynchronize(g_twin_st));
+    return 0;
 }
 
 extern "C" void vox_hip_encoder_attention(float* out, const float* Q, const float* K, const float* V,
                                           int seq_q, int seq_k, int n_heads, int n_kv_heads,
                                           int head_dim, float scale, int window_size, int q_offset) {
     std::lock_guard<std::mutex> lk(g_twin_mu);
-    if (twin_init()) return;
-    if (q_offset + seq_q > seq_k) { set_err("encoder_attention: queries beyond keys"); return; }
-    const size_t qn = (size_t)seq_q * n_heads * head_dim, kn = (size_t)seq_k * n_kv_heads * head_dim;
-    if (twin_buf(&g_tQ, &g_tQ_n, qn) || twin_buf(&g_tK, &g_tK_n, kn) || twin_buf(&g_tV, &g_tV_n, kn) ||
-        twin_buf(&g_tO, &g_tO_n, qn))
-        return;
-    hipMemcpyAsync(g_tQ, Q, qn * 4, hipMemcpyHostToDevice, g_twin_st);
-    hipMemcpyAsync(g_tK, K, kn * 4, hipMemcpyHostToDevice, g_twin_st);
-    hipMemcpyAsync(g_tV, V, kn * 4, hipMemcpyHostToDevice, g_twin_st);
-    int W = window_size > 0 ? window_size : (1 << 30);
-    // few query rows: the key-range split + combine path the streaming encoder takes
-    float* ws = nullptr;
-    size_t wsn = 0;
-    if (n_heads * ((seq_q + 15) / 16) < 256) {
-        wsn = (size_t)n_heads * seq_q * 16 * (head_dim + 2);
-        if (twin_buf(&g_tWs, &g_tWs_n, wsn)) return;
-        ws = g_tWs;
-    }
-    if (launch_attn_tiled(head_dim, g_tQ, n_heads * head_dim, g_tK, g_tV, seq_k, g_tO, n_heads * head_dim,
-                          seq_q, n_heads, n_kv_heads, q_offset, 0, W, scale, g_twin_st, ws, wsn) != hipSuccess) {
-        set_err("encoder_attention launch failed");
-        return;
-    }
-    hipMemcpyAsync(out, g_tO, qn * 4, hipMemcpyDeviceToHost, g_twin_st);
-    hipStreamSynchronize(g_twin_st);
+    twin_attention(out, Q, K, V, seq_q, seq_k, n_heads, n_kv_heads, head_dim, scale, window_size, q_offset);
 }
 
 static int upload_rope_rows(vox_hip_stream_t* s, const float* rope, size_t n) {
@@ -1598,11 +1711,17 @@ extern "C" int vox_hip_decoder_prefill_step(vox_hip_stream_t* s, float* x, int s
 }
 
 extern "C" void vox_hip_decoder_start(vox_hip_stream_t* s, const float* x, int dim) {
+    if (!s || !x || dim != s->m->c.dec_dim) {
+        set_err("decoder_start: dim %d != dec_dim", dim);
+        return;
+    }
     if (hipMemcpyAsync(s->xd, x, (size_t)dim * 4, hipMemcpyHostToDevice, s->st) != hipSuccess)
         set_err("decoder_start upload failed");
 }
 
-extern "C" void vox_hip_decoder_end(vox_hip_stream_t* s) { hipStreamSynchronize(s->st); }
+extern "C" void vox_hip_decoder_end(vox_hip_stream_t* s) {
+    if (s && hipStreamSynchronize(s->st) != hipSuccess) set_err("decoder_end: stream sync failed");
+}
 
 extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_freqs, int logical_pos,
                                          float* logits) {
@@ -1611,8 +1730,8 @@ extern "C" int vox_hip_decoder_full_step(vox_hip_stream_t* s, const float* rope_
     const int ctx = std::min(logical_pos + 1, c.dec_window);
     if (enqueue_step_layers(s, nullptr, logical_pos, s->rope_rows, (ctx + ATT_BLOCK_KEYS - 1) / ATT_BLOCK_KEYS))
         return -1;
-    // argmax into a scratch state so the graph-mode device state is untouched
-    int* tmp_state = s->tokens + s->tokens_cap - 8;
+    // argmax into the twin's own state so the graph-mode device state is untouched
+    int* tmp_state = s->twin_state;
     int st4[4] = {0, 0, 0, 0};
     CK(hipMemcpyAsync(tmp_state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
     CK(launch_argmax_final(s->pval, s->pidx, gemv_grid(c.vocab), tmp_state, nullptr, 0, nullptr, 0,
@@ -1655,7 +1774,7 @@ struct vox_hip_batch {
     // table stay the same
     hipGraphExec_t gexec;
     int gnb, gsplits;
-    vox_hip_stream_t* gkey[VOX_MAX_BATCH];
+    unsigned long long gkey[VOX_MAX_BATCH];  // stream uids (a freed stream's address can be reused)
     const float* gadapter[VOX_MAX_BATCH];
     int gadapter_cap[VOX_MAX_BATCH];
     const float* grope;
@@ -1815,7 +1934,7 @@ static int batch_run(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, in
     }
     bool same = b->gexec && b->gnb == nb && b->gsplits == splits && b->grope == b->m->rope_dec;
     for (int i = 0; same && i < nb; i++)
-        same = b->gkey[i] == ss[i] && b->gadapter[i] == ss[i]->adapter && b->gadapter_cap[i] == ss[i]->adapter_cap;
+        same = b->gkey[i] == ss[i]->uid && b->gadapter[i] == ss[i]->adapter && b->gadapter_cap[i] == ss[i]->adapter_cap;
     if (!same) {
         if (b->gexec) {
             hipGraphExecDestroy(b->gexec);
@@ -1836,7 +1955,7 @@ static int batch_run(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, in
         b->gsplits = splits;
         b->grope = b->m->rope_dec;
         for (int i = 0; i < nb; i++) {
-            b->gkey[i] = ss[i];
+            b->gkey[i] = ss[i]->uid;
             b->gadapter[i] = ss[i]->adapter;
             b->gadapter_cap[i] = ss[i]->adapter_cap;
         }
@@ -1889,7 +2008,7 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
         for (int i = 0; i < n; i++) {
             vox_hip_stream_t* s = streams[i];
             const int avail = s->total_adapter - s->h_state[1];
-            const int left = std::min(max_steps - counts_out[i], s->tokens_cap - s->n_generated);
+            const int left = max_steps - counts_out[i];
             if (!s->started || s->eos_seen || avail <= 0 || left <= 0) continue;
             act.push_back(s);
             idx.push_back(i);
@@ -1912,7 +2031,8 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
         for (int i = 0; i < nb; i++) {
             vox_hip_stream_t* s = act[i];
             tok.resize(steps);
-            CK(hipMemcpy(tok.data(), s->tokens + s->n_generated, (size_t)steps * 4, hipMemcpyDeviceToHost));
+            if (ring_read(s->tokens, s->tokens_cap, 1, s->n_generated, steps, tok.data(), b->st)) return -1;
+            CK(hipStreamSynchronize(b->st));
             int produced = steps;
             if (stop_at_eos)
                 for (int k = 0; k < steps; k++)

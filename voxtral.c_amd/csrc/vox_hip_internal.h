@@ -14,7 +14,6 @@ constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3
 enum { PRO_NONE = 0, PRO_NORM = 1, PRO_NORM_ADA = 2 };
 
 constexpr int GEMV_MAX_BLOCKS = 1024;  // 4 blocks of 256 threads per CU on 256 CUs
-constexpr int GEMV_RB = 4;             // (unused by the launcher: gemv_rb picks 2, 4 or 8 rows per group)
 
 struct GemvArgs {
     const float* x;        // input vector [K] (device)
@@ -74,6 +73,7 @@ struct StepPtrs {
 constexpr int ARGB = 64;                // argmax partial blocks per row
 
 int gemv_grid(int rows);
+bool gemv_ok(int rows, int K, int q8);  // shapes launch_gemv accepts (rows, K multiple of the chunk)
 int attn_maxch(int window);      // decode-attention partials per head (64-key blocks)
 int attn_maxsplits(int window);  // 256-key spans of a window (graph buckets)
 hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const float* w,

@@ -1852,7 +1852,8 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
         int tok = si[0];
         if (tok == 0x7fffffff) tok = 0;
         int step = state[3];
-        if (tokens && step < tokens_cap) tokens[step] = tok;
+        // the token log is a ring of tokens_cap entries (the host drains it every <= 16 steps)
+        if (tokens) tokens[step % tokens_cap] = tok;
         state[0] += 1;
         state[1] += 1;
         state[2] = tok;
@@ -1866,7 +1867,7 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
         const float* a = adapter + (size_t)srow * D;
         for (int i = threadIdx.x; i < D; i += 256) x[i] = a[i] + emb_at(emb, esc, stok, D, i);
     }
-    if (alts && sstep < tokens_cap) alt_merge(part_alt, n, stok, sv[0], sstep, alts);
+    if (alts) alt_merge(part_alt, n, stok, sv[0], sstep % tokens_cap, alts);
 }
 
 // ============================================================================
@@ -1958,7 +1959,7 @@ __global__ __launch_bounds__(256) void k_argmax_batch_final(const float* __restr
             int tok = bi == 0x7fffffff ? 0 : bi;
             int* st = sp.state[i];
             const int step = st[3];
-            if (step < tokens_cap) sp.tokens[i][step] = tok;
+            sp.tokens[i][step % tokens_cap] = tok;  // ring, as k_argmax_final
             st[0] += 1;
             st[1] += 1;
             st[2] = tok;
@@ -2779,9 +2780,16 @@ hipError_t launch_gemv_timed(int pro, int epi, const GemvArgs& a, hipEvent_t sta
     return hipExtLaunchKernel(fn, dim3(gemv_grid(a.rows)), dim3(256), kargs, 0, st, start, stop, 0);
 }
 
+// the shapes launch_gemv accepts: whole 16-B chunks per row, whole row groups, and at most
+// 5 rounds of 256 chunks per row (the instantiated KQ)
+bool gemv_ok(int rows, int K, int q8) {
+    const int kc = q8 ? K >> 4 : K >> 3;
+    return rows > 0 && K > 0 && K % (q8 ? 16 : 8) == 0 && rows % gemv_rb(rows) == 0 && (kc + 255) / 256 <= 5;
+}
+
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     const int rb = gemv_rb(a.rows);
-    if (a.K % (a.wscale ? 16 : 8) || a.rows % rb) return hipErrorInvalidValue;
+    if (!gemv_ok(a.rows, a.K, a.wscale != nullptr)) return hipErrorInvalidValue;
     const int grid = gemv_grid(a.rows);
 #define GEMV_CASE(P, E) \
     if (pro == P && epi == E)                                                            \

@@ -155,6 +155,27 @@ static int jints(const char **p, long long *out, int cap) {
     }
 }
 
+/* byte length must match shape and dtype: BF16 2 B / F32 4 B per element; Q8 (quantize.py
+ * layout, voxtral_safetensors.c:457-468) rows f32 scales + rows * cols int8 */
+static int st_check_bytes(const st_tensor_t *t) {
+    long long n = 1;
+    for (int i = 0; i < t->ndim; i++) {
+        if (t->shape[i] < 0 || (t->shape[i] && n > (1LL << 40) / t->shape[i])) return -1;
+        n *= t->shape[i];
+    }
+    const size_t len = t->end - t->begin;
+    switch (t->dtype) {
+        case DT_BF16: return len == (size_t)n * 2 ? 0 : -1;
+        case DT_F32: return len == (size_t)n * 4 ? 0 : -1;
+        case DT_Q8: {
+            if (t->ndim < 1 || t->shape[0] <= 0) return -1;
+            const long long rows = t->shape[0];
+            return len == (size_t)rows * 4 + (size_t)n ? 0 : -1;
+        }
+        default: return 0; /* other dtypes are never read */
+    }
+}
+
 static void st_close(st_file_t *f) {
     if (f->map && f->map != MAP_FAILED) munmap(f->map, f->size);
     if (f->fd >= 0) close(f->fd);
@@ -174,7 +195,8 @@ static int st_open(st_file_t *f, const char *path) {
     if (f->map == MAP_FAILED) return fail("%s: mmap failed", path);
     uint64_t hl = 0;
     memcpy(&hl, f->map, 8);
-    if (hl + 8 > f->size) return fail("%s: bad header length", path);
+    /* overflow-safe (voxtral_safetensors.c:236-240 tests header_size > file_size - 8) */
+    if (hl == 0 || hl > f->size - 8) return fail("%s: bad header length", path);
     char *hdr = malloc(hl + 1);
     memcpy(hdr, f->map + 8, hl);
     hdr[hl] = 0;
@@ -239,7 +261,8 @@ static int st_open(st_file_t *f, const char *path) {
                 ws(&p);
                 if (*p == ',') p++;
             }
-            if (f->base + t->end > f->size || t->end < t->begin) goto done;
+            if (t->end < t->begin || t->end > f->size - f->base) goto done;
+            if (st_check_bytes(t)) goto done;
             f->n++;
         }
         ws(&p);

@@ -34,7 +34,7 @@ WeightsC = weights_struct_class()
 # exported symbols, as declared in include/voxtral_hip.h
 EXPORTS = [
     "vox_hip_init", "vox_hip_available", "vox_hip_shutdown", "vox_hip_memory_used",
-    "vox_hip_last_error", "vox_hip_set_device", "vox_hip_config_voxtral_4b",
+    "vox_hip_last_error", "vox_hip_clear_error", "vox_hip_set_device", "vox_hip_config_voxtral_4b",
     "vox_hip_model_create", "vox_hip_model_free", "vox_hip_model_set_delay",
     "vox_hip_model_ada_scale", "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
@@ -65,6 +65,7 @@ def lib():
     sig = {
         "vox_hip_init": (I, []), "vox_hip_available": (I, []), "vox_hip_shutdown": (None, []),
         "vox_hip_memory_used": (ctypes.c_size_t, []), "vox_hip_last_error": (ctypes.c_char_p, []),
+        "vox_hip_clear_error": (None, []),
         "vox_hip_set_device": (I, [I]),
         "vox_hip_config_voxtral_4b": (None, [P]),
         "vox_hip_model_create": (P, [P, P, I]), "vox_hip_model_free": (None, [P]),
@@ -227,6 +228,43 @@ class Stream:
                                           fptr(pr)) != 0:
             _err("read_alts")
         return ids, pr
+
+    # ---- reference-boundary twins on this stream's device state (host arrays in / out;
+    # the calls INTEGRATION.md sections 4-5 bind into voxtral_encoder.c / voxtral_decoder.c)
+    def twin_encoder_full_step(self, x: np.ndarray, rope: np.ndarray, logical_start: int) -> np.ndarray:
+        """vox_metal_encoder_full_step twin: all encoder layers + final norm on x [n, enc_dim]
+        (a copy is returned), K/V appended at logical positions logical_start.."""
+        x = np.array(x, np.float32, copy=True, order="C")
+        rope = np.ascontiguousarray(rope, np.float32)
+        if lib().vox_hip_encoder_full_step(self.h, fptr(x), x.shape[0], fptr(rope), logical_start) != 0:
+            _err("encoder_full_step")
+        return x
+
+    def twin_decoder_prefill_step(self, x: np.ndarray, rope: np.ndarray, logical_start: int) -> np.ndarray:
+        """vox_metal_decoder_prefill_step twin: decoder layers on x [n, dec_dim], KV written."""
+        x = np.array(x, np.float32, copy=True, order="C")
+        rope = np.ascontiguousarray(rope, np.float32)
+        if lib().vox_hip_decoder_prefill_step(self.h, fptr(x), x.shape[0], fptr(rope), logical_start) != 0:
+            _err("decoder_prefill_step")
+        return x
+
+    def twin_decoder_step(self, x: np.ndarray, rope_row: np.ndarray, logical_pos: int, want_logits=True):
+        """decoder_start + decoder_full_step + decoder_end, as voxtral_decoder.c:686-699
+        drives the Metal twins: returns (token, logits or None)."""
+        x = np.ascontiguousarray(x, np.float32)
+        rope_row = np.ascontiguousarray(rope_row, np.float32)
+        L = lib()
+        L.vox_hip_clear_error()
+        L.vox_hip_decoder_start(self.h, fptr(x), x.shape[-1])
+        if L.vox_hip_last_error():
+            _err("decoder_start")
+        logits = np.empty(self.cfg.vocab, np.float32) if want_logits else None
+        tok = L.vox_hip_decoder_full_step(self.h, fptr(rope_row), logical_pos,
+                                          fptr(logits) if want_logits else None)
+        L.vox_hip_decoder_end(self.h)
+        if tok < 0:
+            _err("decoder_full_step")
+        return tok, logits
 
     def set_profiling(self, on: bool):
         lib().vox_hip_stream_set_profiling(self.h, int(on))
@@ -440,12 +478,27 @@ class Batch:
             self.h = None
 
 
+def _void_call(what, fn, *args):
+    """The reference-boundary twins return void (voxtral_metal.h); a failure is reported
+    through vox_hip_last_error(), cleared before the call."""
+    L = lib()
+    L.vox_hip_clear_error()
+    fn(*args)
+    msg = L.vox_hip_last_error()
+    if msg:
+        raise RuntimeError(f"{what}: {msg.decode()}")
+
+
 def sgemm_bf16(A: np.ndarray, B_bf16: np.ndarray) -> np.ndarray:
+    """C = A @ B^T (vox_metal_sgemm_bf16 twin); B is cached on the device by host pointer
+    and shape, so keep it alive and unmodified."""
     A = np.ascontiguousarray(A, np.float32)
+    B_bf16 = np.ascontiguousarray(B_bf16, np.uint16)
     M, K = A.shape
     N = B_bf16.shape[0]
+    assert B_bf16.shape[1] == K
     C = np.empty((M, N), np.float32)
-    lib().vox_hip_sgemm_bf16(M, N, K, fptr(A), B_bf16.ctypes.data, fptr(C))
+    _void_call("sgemm_bf16", lib().vox_hip_sgemm_bf16, M, N, K, fptr(A), B_bf16.ctypes.data, fptr(C))
     return C
 
 
@@ -456,14 +509,35 @@ def sgemm_q8(A: np.ndarray, B_q8: np.ndarray, scales: np.ndarray) -> np.ndarray:
     M, K = A.shape
     N = B_q8.shape[0]
     C = np.empty((M, N), np.float32)
-    lib().vox_hip_sgemm_q8(M, N, K, fptr(A), B_q8.ctypes.data, fptr(scales), fptr(C))
+    _void_call("sgemm_q8", lib().vox_hip_sgemm_q8, M, N, K, fptr(A), B_q8.ctypes.data, fptr(scales), fptr(C))
     return C
+
+
+def fused_qkv_bf16(x: np.ndarray, wq: np.ndarray, wk: np.ndarray, wv: np.ndarray):
+    """vox_metal_fused_qkv_bf16 twin: (x wq^T, x wk^T, x wv^T), biases left to the caller."""
+    x = np.ascontiguousarray(x, np.float32)
+    M, K = x.shape
+    outs = [np.empty((M, w.shape[0]), np.float32) for w in (wq, wk, wv)]
+    _void_call("fused_qkv_bf16", lib().vox_hip_fused_qkv_bf16, M, K, fptr(x), wq.ctypes.data, wq.shape[0],
+               wk.ctypes.data, wk.shape[0], wv.ctypes.data, wv.shape[0], *[fptr(o) for o in outs])
+    return tuple(outs)
+
+
+def fused_ffn_bf16(x: np.ndarray, w1: np.ndarray, w3: np.ndarray, w2: np.ndarray) -> np.ndarray:
+    """vox_metal_fused_ffn_bf16 twin: (silu(x w1^T) * x w3^T) w2^T, w2 bias left to the caller."""
+    x = np.ascontiguousarray(x, np.float32)
+    M, dim = x.shape
+    hidden = w1.shape[0]
+    out = np.empty((M, dim), np.float32)
+    _void_call("fused_ffn_bf16", lib().vox_hip_fused_ffn_bf16, M, dim, hidden, fptr(x), w1.ctypes.data,
+               w3.ctypes.data, w2.ctypes.data, fptr(out))
+    return out
 
 
 def encoder_attention(Q, K, V, n_heads, n_kv_heads, head_dim, window, q_offset):
     Q, K, V = (np.ascontiguousarray(x, np.float32) for x in (Q, K, V))
     out = np.empty_like(Q)
-    lib().vox_hip_encoder_attention(fptr(out), fptr(Q), fptr(K), fptr(V), Q.shape[0], K.shape[0],
-                                    n_heads, n_kv_heads, head_dim, float(1.0 / np.sqrt(head_dim)),
-                                    window, q_offset)
+    _void_call("encoder_attention", lib().vox_hip_encoder_attention, fptr(out), fptr(Q), fptr(K), fptr(V),
+               Q.shape[0], K.shape[0], n_heads, n_kv_heads, head_dim, float(1.0 / np.sqrt(head_dim)),
+               window, q_offset)
     return out

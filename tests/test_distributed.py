@@ -31,7 +31,9 @@ def test_bench_dist_world2(tmp_path):
         d.barrier()
         mx = d.max(1.5 + d.rank)
         sm = d.sum(10 * (d.rank + 1))
-        print(json.dumps({{"rank": d.rank, "world": d.world, "max": mx, "sum": sm}}))
+        # one file per rank: two ranks printing to one pipe can interleave their lines
+        open(os.path.join({str(tmp_path)!r}, f"r{{d.rank}}.json"), "w").write(
+            json.dumps({{"rank": d.rank, "world": d.world, "max": mx, "sum": sm}}))
     """))
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
@@ -40,7 +42,7 @@ def test_bench_dist_world2(tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     import json
-    outs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    outs = [json.loads((tmp_path / f"r{i}.json").read_text()) for i in range(2)]
     assert sorted(o["rank"] for o in outs) == [0, 1]
     for o in outs:
         assert o["world"] == 2 and o["max"] == 2.5 and o["sum"] == 30.0

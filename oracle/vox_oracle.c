@@ -25,6 +25,10 @@ enum { RowMajor = 101, NoTrans = 111, Trans = 112 };
 #define TOKEN_STREAMING_PAD 32
 
 static int g_threads = 1;
+/* test-only invariance knob (tests/test_oracle_cpu.py): 1 = never compact the KV caches
+ * (grow instead), so a run with physical compaction can be compared with one without */
+static int g_no_compact = 0;
+void vo_set_no_compaction(int on) { g_no_compact = on; }
 
 void vo_set_threads(int n) {
     g_threads = n < 1 ? 1 : n;
@@ -554,7 +558,7 @@ int vo_encoder_incremental(vo_stream_t *s, float *x, int new_len) {
     int dim = c->enc_dim, H = c->enc_heads, KVH = c->enc_kv_heads, hd = c->enc_head_dim;
     int hidden = c->enc_hidden, qd = H * hd, kvd = KVH * hd;
     if (new_len <= 0) return 0;
-    if (s->e_len + new_len > c->enc_window) enc_kv_compact(s);
+    if (s->e_len + new_len > c->enc_window && !g_no_compact) enc_kv_compact(s);
     enc_kv_grow(s, s->e_len + new_len);
     int cache_len = s->e_len;
 
@@ -796,7 +800,7 @@ int vo_decoder_forward(vo_stream_t *s, const float *embed, float *logits) {
     if (!s->dk) dec_kv_init(s, c->dec_window + 1 + 1024);
     int pos = s->d_len;
     if (pos >= s->d_max) {
-        if (s->d_len > c->dec_window) { dec_kv_compact(s); pos = s->d_len; }
+        if (s->d_len > c->dec_window && !g_no_compact) { dec_kv_compact(s); pos = s->d_len; }
         if (pos >= s->d_max) dec_kv_grow(s, pos + 1024);
     }
     int lp = s->d_off + pos;

@@ -61,6 +61,8 @@ typedef struct vo_stream vo_stream_t;
 
 /* ---- per-op restatements (voxtral_kernels.c) ---- */
 void vo_set_threads(int n);
+/* test-only: 1 = grow the KV caches instead of compacting them (invariance tests) */
+void vo_set_no_compaction(int on);
 void vo_linear_bf16(float *y, const float *x, const uint16_t *W, const float *b,
                     int M, int in_dim, int out_dim);
 /* vox_linear_q8 / vox_linear_nobias_q8 / vox_matmul_t_q8 (voxtral_kernels.c:277-393) */

@@ -39,7 +39,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         sig = {
-            "vo_set_threads": (None, [I]),
+            "vo_set_threads": (None, [I]), "vo_set_no_compaction": (None, [I]),
             "vo_linear_bf16": (None, [fp, fp, P, fp, I, I, I]),
             "vo_linear_q8": (None, [fp, fp, P, fp, fp, I, I, I]),
             "vo_rms_norm": (None, [fp, fp, fp, I, I, F]),
@@ -74,6 +74,11 @@ def lib():
 
 def set_threads(n: int):
     lib().vo_set_threads(n)
+
+
+def set_no_compaction(on: bool):
+    """test-only: grow the KV caches instead of compacting them (invariance tests)"""
+    lib().vo_set_no_compaction(int(on))
 
 
 # ---- per-op restatements -------------------------------------------------

@@ -5,8 +5,9 @@ checkpoint written by vox_weights.write_safetensors.  Two rows of one matrix are
 hand so that the quantizer's edge cases appear: an all-zero row (scale 0, quantize.py:38-40)
 and a row whose scaled values fall exactly on .5 ties (np.round is round-half-to-even,
 quantize.py:43).  The fixture keeps, per output tensor, its dtype, shape and the sha256 of
-its data bytes (Q8: f32 scales then int8 rows, quantize.py:121; F32: the values), plus the
-two crafted rows in full.  tests/test_q8_cpu.py rebuilds the same checkpoint from the seed
+its data bytes (Q8: f32 scales then int8 rows, quantize.py:121; F32: the values), the two
+crafted rows in full, and the sha256 / length of the whole output file (the unaligned
+quantize.py layout, :152-186).  tests/test_q8_cpu.py rebuilds the same checkpoint from the seed
 and checks vox_weights.quantize_q8 against every hash.
 
 Run here (needs /root/reference):  python3 tests/golden/gen_q8.py
@@ -57,9 +58,12 @@ def main():
         os.makedirs(src)
         vw.write_safetensors(w, os.path.join(src, "consolidated.safetensors"))
         subprocess.run([sys.executable, REF, src, dst], check=True, stdout=subprocess.DEVNULL)
-        q = vw.load_safetensors(os.path.join(dst, "consolidated.safetensors"), vw.TINY)
+        qpath = os.path.join(dst, "consolidated.safetensors")
+        q = vw.load_safetensors(qpath, vw.TINY)
+        raw = open(qpath, "rb").read()
         out = {"seed": SEED, "edge_tensor": EDGE_TENSOR, "zero_row": ZERO_ROW, "tie_row": TIE_ROW,
-               "tensors": {}}
+               "tensors": {}, "file_sha256": hashlib.sha256(raw).hexdigest(), "file_bytes": len(raw),
+               "header_bytes": int.from_bytes(raw[:8], "little")}
         for name, (sc, qq) in q.q8.items():
             out["tensors"][name] = {"dtype": "Q8", "shape": list(qq.shape),
                                     "sha256": tensor_digest("Q8", [sc, qq])}

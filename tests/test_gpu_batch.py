@@ -81,36 +81,63 @@ def test_batch_mixed_positions_and_continuation(models, tiny_cfg):
     b.close()
 
 
-@pytest.mark.slow
-def test_batch_full_size_matches_single():
-    """Full Voxtral-4B shapes: 3 jfk-shaped streams decoded as one batch give the tokens of
-    decoding each stream alone (and stream 0 those of the CPU oracle)."""
+def _oracle_tokens_parallel(om, mels, chunks):
+    """The oracle's tokens for several streams: each stream's encoder and prefill + first
+    token in turn (the oracle's M > 1 linears share one scratch buffer, as the reference's
+    bf16_scratch does), then the single-threaded greedy decodes side by side in threads
+    (ctypes releases the GIL; the M = 1 path touches no shared state)."""
+    from concurrent.futures import ThreadPoolExecutor
     import os
+    import vox_oracle
+    vox_oracle.set_threads(min(16, os.cpu_count() or 1))
+    sts, first = [], []
+    for mel in mels:
+        st = vox_oracle.OracleStream(om)
+        off = 0
+        for n in chunks:
+            st.encode_mel(mel[off:off + n])
+            off += n
+        first.append(st.decode(max_steps=1, stop_at_eos=False).tolist())
+        sts.append(st)
+    vox_oracle.set_threads(1)
+    with ThreadPoolExecutor(len(sts)) as ex:
+        rest = list(ex.map(lambda st: st.decode(stop_at_eos=False).tolist(), sts))
+    for st in sts:
+        st.close()
+    return [f + r for f, r in zip(first, rest)]
+
+
+@pytest.mark.slow
+def test_batch_full_size_8_streams_each_vs_oracle():
+    """Full Voxtral-4B shapes, config 4's per-GPU load: 8 jfk-shaped streams (1355 / 140 / 1
+    mel-frame chunks, 149 tokens each, different audio) decoded as one batch; EVERY stream's
+    ids equal the CPU oracle's for that stream."""
     import vox_hip
     import vox_oracle
     from vox_weights import VOXTRAL_4B, synth_weights
+    chunks = [1355, 140, 1]
     w = synth_weights(VOXTRAL_4B, seed=0)
     hm = vox_hip.Model(VOXTRAL_4B, w)
-    mels = _mels(VOXTRAL_4B, [1496, 1496, 1200], 42)
+    mels = _mels(VOXTRAL_4B, [sum(chunks)] * 8, 42)
     ss = [vox_hip.Stream(hm) for _ in mels]
     for s, mel in zip(ss, mels):
-        s.encode_mel(mel)
-    b = vox_hip.Batch(hm, 4)
-    got = b.decode(ss, max_steps=1000, stop_at_eos=False)
-    for i, mel in enumerate(mels):
-        one = vox_hip.Stream(hm)
-        one.encode_mel(mel)
-        ref = one.decode(stop_at_eos=False).tolist()
-        assert got[i].tolist() == ref, i
-        one.close()
-    om = vox_oracle.OracleModel(VOXTRAL_4B, w)
-    vox_oracle.set_threads(min(16, os.cpu_count() or 1))
-    assert got[0].tolist() == _reference_tokens(om, mels[0])
-    om.close()
+        off = 0
+        for n in chunks:
+            s.encode_mel(mel[off:off + n])
+            off += n
+    b = vox_hip.Batch(hm, 8)
+    got = [g.tolist() for g in b.decode(ss, max_steps=1000, stop_at_eos=False)]
     for s in ss:
         s.close()
     b.close()
     hm.close()
+    om = vox_oracle.OracleModel(VOXTRAL_4B, w)
+    refs = _oracle_tokens_parallel(om, mels, chunks)
+    om.close()
+    for i in range(8):
+        assert len(refs[i]) == 149
+        assert got[i] == refs[i], (i, next(k for k in range(149) if got[i][k] != refs[i][k]))
+    assert len({tuple(r) for r in refs}) > 1   # the streams really differ
 
 
 def test_batch_long_context_multiblock(tiny_weights):
@@ -140,3 +167,32 @@ def test_batch_long_context_multiblock(tiny_weights):
     b.close()
     hm.close()
     om.close()
+
+
+def test_batch_graph_not_reused_after_stream_churn(models, tiny_cfg):
+    """C4 serving churns streams: decode a batch, free one stream, create another (its
+    handle may land at the freed address) and decode again with the same Batch.  The
+    captured step graph holds per-stream device pointers, so it must be keyed by stream
+    identity (uid), not by handle address: every stream still gets the oracle's ids."""
+    import vox_hip
+    hm, om = models
+    mels = _mels(tiny_cfg, [520, 560, 600, 640], 23)
+    refs = [_reference_tokens(om, m) for m in mels]
+    ss = [vox_hip.Stream(hm) for _ in mels[:3]]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 4)
+    out = [t.tolist() for t in b.decode(ss, max_steps=6, stop_at_eos=False)]
+    assert out[1] == refs[1][:6]
+    old = ss[1].h
+    ss[1].close()
+    ss[1] = vox_hip.Stream(hm)
+    reused = ss[1].h == old
+    ss[1].encode_mel(mels[3])
+    got = [t.tolist() for t in b.decode(ss, max_steps=1000, stop_at_eos=False)]
+    assert out[0] + got[0] == refs[0]
+    assert got[1] == refs[3], reused
+    assert out[2] + got[2] == refs[2]
+    for s in ss:
+        s.close()
+    b.close()

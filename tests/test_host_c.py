@@ -92,3 +92,30 @@ def test_cli_transcribes_like_python_and_oracle(ckpt, tiny_weights, jfk_samples,
     assert ids == sess.tokens == osess.tokens
     sess.close()
     hs.close(); hm.close(); os_.close(); om.close()
+
+
+@pytest.mark.gpu
+def test_cli_q8_checkpoint_in_quantize_py_layout(tmp_path, tiny_weights, jfk_samples):
+    """Config 5 from a file: the TINY_LONG weights quantised and written exactly as the
+    reference's quantize.py writes them (unpadded header, unaligned f32 scales and int8 rows;
+    the layout is pinned byte for byte in test_q8_cpu), loaded by the C loader (vh_load:
+    scales copied aligned, int8 handed over as is, voxtral_safetensors.c:457-468) and
+    transcribed by the CLI on the GPU: ids equal the CPU oracle's q8 path."""
+    import vox_oracle
+    from vox_weights import TINY_LONG, quantize_q8, write_quantize_py_layout
+    q8 = quantize_q8(tiny_weights)
+    path = str(tmp_path / "consolidated.safetensors")
+    write_quantize_py_layout(q8, path)
+    assert (8 + int.from_bytes(open(path, "rb").read(8), "little")) % 4 != 0
+    r = subprocess.run([CLI, "-d", path, "-i", os.path.join(GOLDEN, "jfk.wav"), "-I", "0.5"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    ids = [int(t) for t in r.stdout.split()]
+    om = vox_oracle.OracleModel(TINY_LONG, q8)
+    os_ = vox_oracle.OracleStream(om)
+    osess = vox_oracle.OracleSession(os_, interval_s=0.5)
+    for kind, mel in vox_oracle.transcribe_mel_schedule(jfk_samples, feed_size=8000):
+        getattr(osess, kind)(mel)
+    assert len(ids) > 0
+    assert ids == osess.tokens
+    os_.close(); om.close()

@@ -126,3 +126,57 @@ def test_pipeline_matches_python_reference(pyref):
     assert rel(logits, pyref["pipe_logits"]) < 1e-4, rel(logits, pyref["pipe_logits"])
     assert toks.tolist() == pyref["pipe_tokens"].tolist()
     st.close(); st2.close(); om.close()
+
+
+def _oracle_run(cfg, w, events, interval=None):
+    """tokens, per-step logits and adapter rows of one oracle stream over mel events"""
+    import vox_oracle
+    om = vox_oracle.OracleModel(cfg, w)
+    st = vox_oracle.OracleStream(om)
+    sess = vox_oracle.OracleSession(st, interval_s=interval or 2.0)
+    logits = []
+    for kind, mel in events:
+        if kind == "finish":
+            sess.finished = True
+        sess._enc(mel, 1 if kind == "flush" else sess.min_new)
+        t, lg = st.decode(stop_at_eos=False, want_logits=True)
+        sess.tokens += t.tolist()
+        logits.append(lg)
+    out = (sess.tokens, np.concatenate(logits), st.read_adapter(), sess.chunks)
+    st.close()
+    om.close()
+    return out
+
+
+def test_invariance_compaction_vs_none(tiny_cfg, tiny_weights, jfk_samples):
+    """the window semantics do not depend on the physical KV
+    compaction (voxtral_encoder.c:431-449, voxtral_decoder.c:354-384).  TINY's windows
+    (24 / 48) compact the encoder and decoder caches many times over jfk; a run that only
+    grows the caches gives bit-identical adapter rows, logits and ids."""
+    import vox_oracle
+    events = vox_oracle.transcribe_mel_schedule(jfk_samples)
+    a = _oracle_run(tiny_cfg, tiny_weights, events)
+    vox_oracle.set_no_compaction(True)
+    try:
+        b = _oracle_run(tiny_cfg, tiny_weights, events)
+    finally:
+        vox_oracle.set_no_compaction(False)
+    assert len(a[0]) == 149
+    assert a[0] == b[0]
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_invariance_chunked_vs_one_shot(tiny_cfg, tiny_weights, jfk_samples):
+    """the causal encoder with its conv-stem tails and 4-row carry
+    (voxtral.c:581-759, 868-934) gives the same adapter rows whether the audio arrives in one
+    chunk (vox_transcribe_audio) or in -I 0.5 chunks (main.c file mode), up to f32
+    summation order; greedy ids equal (the reference's own -I 2 / -I 0.5 runs on jfk gave
+    identical ids)."""
+    import vox_oracle
+    one = _oracle_run(tiny_cfg, tiny_weights, vox_oracle.transcribe_mel_schedule(jfk_samples))
+    chk = _oracle_run(tiny_cfg, tiny_weights, vox_oracle.transcribe_mel_schedule(jfk_samples, feed_size=8000), 0.5)
+    assert len(one[3]) == 3 and len(chk[3]) > 10
+    assert one[2].shape == chk[2].shape
+    assert rel(one[2], chk[2]) < 1e-5, rel(one[2], chk[2])
+    assert one[0] == chk[0]

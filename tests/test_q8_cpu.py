@@ -104,3 +104,18 @@ def test_oracle_q8_pipeline_matches_python_reference():
     assert rel(logits, pr["pipeq8_logits"]) < 1e-4, rel(logits, pr["pipeq8_logits"])
     assert toks.tolist() == pr["pipeq8_tokens"].tolist()
     st.close(); st2.close(); om.close()
+
+
+def test_quantize_py_file_layout_byte_identical(ref, q8w, tmp_path):
+    """vox_weights.write_quantize_py_layout writes the reference quantizer's output file
+    byte for byte (unpadded compact header, tensors back to back: unaligned scales/rows),
+    so the GPU test that loads it through the C loader (vh_load) reads exactly what
+    quantize.py produces."""
+    import vox_weights as vw
+    path = tmp_path / "consolidated.safetensors"
+    vw.write_quantize_py_layout(q8w, str(path))
+    raw = path.read_bytes()
+    assert len(raw) == ref["file_bytes"]
+    assert int.from_bytes(raw[:8], "little") == ref["header_bytes"]
+    assert (8 + ref["header_bytes"]) % 4 != 0       # the data section starts unaligned
+    assert hashlib.sha256(raw).hexdigest() == ref["file_sha256"]

@@ -321,6 +321,34 @@ def write_safetensors(w: Weights, path: str):
                 f.write(p.tobytes())
 
 
+def write_quantize_py_layout(w: Weights, path: str):
+    """A Q8 checkpoint byte for byte as quantize.py:152-186 writes it: tensors in the input
+    file's data order (tensor_specs), 2-D ones as Q8 (f32 row scales then int8 rows), the
+    rest F32; compact JSON header (separators ',' ':'), no padding, data back to back -- so
+    scales and rows land at arbitrary (unaligned) offsets.  tests/test_q8_cpu.py pins the
+    whole file against the reference quantizer's output (q8_ref.json file_sha256)."""
+    assert w.is_q8
+    entries = []
+    for name, _, _ in tensor_specs(w.cfg):
+        if name in w.q8:
+            sc, q = w.q8[name]
+            entries.append((name, "Q8", list(q.shape), np.ascontiguousarray(sc).tobytes()
+                            + np.ascontiguousarray(q).tobytes()))
+        else:
+            a = np.ascontiguousarray(w._stored_f32[name], np.float32)
+            entries.append((name, "F32", list(a.shape), a.tobytes()))
+    hdr, off = {}, 0
+    for name, dt, shape, data in entries:
+        hdr[name] = {"dtype": dt, "shape": shape, "data_offsets": [off, off + len(data)]}
+        off += len(data)
+    hj = json.dumps(hdr, separators=(",", ":")).encode("utf-8")
+    with open(path, "wb") as f:
+        f.write(len(hj).to_bytes(8, "little"))
+        f.write(hj)
+        for _, _, _, data in entries:
+            f.write(data)
+
+
 # ---------------------------------------------------------------------------
 # ctypes weight table (same field order in vox_hip_weights_t and vo_weights_t)
 # ---------------------------------------------------------------------------

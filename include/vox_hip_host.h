@@ -11,8 +11,10 @@
  *     tokenizer (voxtral_tokenizer.c) stays out of scope;
  *   - WAV input must be 16 kHz mono 16-bit PCM (the reference's loader also converts
  *     other formats, voxtral_audio.c:49-165);
- *   - continuous (live) mode restarts and alternatives are not wired here (the C ABI has
- *     vox_hip_stream_reset_decoder and vox_hip_stream_set_alt for them).
+ *   - the text / control / invalid classification the live-mode restarts use
+ *     (stream_classify_token, voxtral.c:532-539) works on ids (vh_token_class): the
+ *     reference asks its tokenizer whether a text id decodes to an empty string, which for
+ *     the Tekken vocabulary is id 1000 (raw byte 0x00).
  */
 #ifndef VOX_HIP_HOST_H
 #define VOX_HIP_HOST_H
@@ -54,10 +56,30 @@ int vh_stream_flush(vh_stream_t *s);
 int vh_stream_finish(vh_stream_t *s);
 /* vox_stream_get (voxtral.c:1319-1327), ids instead of strings: up to max queued ids */
 int vh_stream_get(vh_stream_t *s, int *ids, int max);
+
+/* vox_stream_set_continuous (voxtral.c:1677-1679): live mode (main.c enables it for --stdin
+ * and the microphone).  After each decoder drain the decoder restarts on EOS, on more than
+ * 2000 KV positions, on 64 non-text tokens in a row, or after 20 s of fed audio without a
+ * decoded token; restarts other than EOS, and two EOS restarts in a row without text,
+ * reset the whole stream (mel, conv stem, encoder, decoder; voxtral.c:410-420, 1189-1239). */
+void vh_stream_set_continuous(vh_stream_t *s, int on);
+
+/* vox_stream_set_alt (voxtral.c:1329-1337): n_alt clamped to 1..VH_MAX_ALT, cutoff to
+ * [0, 1]; candidates are kept on the device per step (stream_fill_alts, voxtral.c:955-1010) */
+#define VH_MAX_ALT 4
+int vh_stream_set_alt(vh_stream_t *s, int n_alt, float cutoff);
+/* vox_stream_get_alt (voxtral.c:1339-1353), ids: up to max records of VH_MAX_ALT ints --
+ * the chosen id, then its accepted alternatives (text tokens only), -1 for none */
+int vh_stream_get_alt(vh_stream_t *s, int *records, int max);
+
+/* stream_classify_token (voxtral.c:532-539) on ids */
+enum { VH_TOK_TEXT = 0, VH_TOK_CONTROL = 1, VH_TOK_INVALID = 2, VH_TOK_EOS = 3 };
+int vh_token_class(int id);
 /* the stats vox_stream_free prints (voxtral.c:1358-1370) */
 typedef struct {
     int mel_frames, adapter_tokens, generated, chunks;
     double encoder_ms, decoder_ms, prefill_ms;
+    int restarts, full_resets;   /* continuous mode */
 } vh_stats_t;
 void vh_stream_stats(const vh_stream_t *s, vh_stats_t *out);
 

@@ -397,6 +397,33 @@ void vo_stream_free(vo_stream_t *s) {
     free(s);
 }
 
+/* stream_reset_decoder_state (voxtral.c:766-783): KV length 0, adapter backlog dropped */
+void vo_stream_reset_decoder(vo_stream_t *s) {
+    s->d_len = 0;
+    s->d_off = 0;
+    s->total_adapter = 0;
+    s->gen_pos = 0;
+    s->started = 0;
+    s->prev_token = TOKEN_BOS;
+    s->eos_seen = 0;
+    s->n_generated = 0;
+}
+
+/* stream_reset_full_state (voxtral.c:786-814) minus the mel context (the caller's) */
+void vo_stream_reset_full(vo_stream_t *s) {
+    const vo_config_t *c = &s->m->c;
+    s->conv_init = 0;
+    s->conv0_res_count = 0;
+    s->enc_res_count = 0;
+    memset(s->mel_tail, 0, sizeof(float) * (size_t)c->mel_bins * 2);
+    memset(s->conv0_tail, 0, sizeof(float) * (size_t)c->enc_dim * 2);
+    memset(s->conv0_res, 0, sizeof(float) * (size_t)c->enc_dim);
+    memset(s->enc_res, 0, sizeof(float) * (size_t)c->enc_dim * (c->downsample - 1));
+    s->e_len = 0;
+    s->e_off = 0;
+    vo_stream_reset_decoder(s);
+}
+
 void vo_stream_state(const vo_stream_t *s, int *o) {
     o[0] = s->e_len; o[1] = s->e_off; o[2] = s->d_len; o[3] = s->d_off;
     o[4] = s->total_adapter; o[5] = s->gen_pos; o[6] = s->enc_res_count; o[7] = s->conv0_res_count;

@@ -107,6 +107,10 @@ int vo_decoder_forward(vo_stream_t *s, const float *embed, float *logits);
 int vo_stream_decode(vo_stream_t *s, int max_steps, int stop_at_eos, int *tokens_out,
                      float *logits_out);
 void vo_stream_state(const vo_stream_t *s, int *out8);
+/* stream_reset_decoder_state (voxtral.c:766-783) / stream_reset_full_state (:786-814, the
+ * mel context excluded: it belongs to the caller) */
+void vo_stream_reset_decoder(vo_stream_t *s);
+void vo_stream_reset_full(vo_stream_t *s);
 
 /* ---- incremental mel (voxtral_audio.c:405-662) ---- */
 typedef struct vo_mel vo_mel_t;

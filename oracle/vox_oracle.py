@@ -61,6 +61,7 @@ def lib():
             "vo_decoder_forward": (I, [P, fp, fp]),
             "vo_stream_decode": (I, [P, I, I, ip, fp]),
             "vo_stream_state": (None, [P, ip]),
+            "vo_stream_reset_decoder": (None, [P]), "vo_stream_reset_full": (None, [P]),
             "vo_mel_create": (P, [I]), "vo_mel_feed": (I, [P, fp, I]),
             "vo_mel_finish": (I, [P, I]), "vo_mel_data": (fp, [P, ip]), "vo_mel_free": (None, [P]),
         }
@@ -242,6 +243,12 @@ class OracleStream:
                                    f(logits) if want_logits else None)
         return (toks[:n], logits[:n]) if want_logits else toks[:n]
 
+    def reset_decoder(self):
+        lib().vo_stream_reset_decoder(self.h)
+
+    def reset_full(self):
+        lib().vo_stream_reset_full(self.h)
+
     def state(self):
         o = np.zeros(8, np.int32)
         lib().vo_stream_state(self.h, o.ctypes.data_as(ip))
@@ -396,3 +403,123 @@ def transcribe_mel_schedule(samples, delay_tokens=6, feed_size=None):
     events.append(("finish", m.data()))
     m.close()
     return events
+
+
+class OracleAudioSession:
+    """vox_stream_feed / flush / finish over raw 16 kHz samples (voxtral.c:1288-1316,
+    1640-1667) with stream_run_encoder's gating (voxtral.c:827-851), stream_run_decoder's
+    drain (voxtral.c:1013-1145) and, with continuous=True, its live-mode restarts
+    (voxtral.c:1189-1239, limits :410-420).  Token classes as vh_token_class: EOS, control
+    (< 1000), invalid (1000: Tekken's empty raw byte), text.  Records every generated id and
+    the restarts (kind 1 EOS, 2 KV, 3 non-text streak, 4 no-decode watchdog; full reset)."""
+
+    def __init__(self, stream: OracleStream, interval_s=2.0, continuous=False, delay_tokens=6):
+        self.s = stream
+        self.interval = interval_s
+        self.min_new = max(1, int(interval_s * 100.0))
+        self.continuous = continuous
+        self.delay_tokens = delay_tokens
+        self.mel = OracleMel(32 * 1280)
+        self.cursor = 0
+        self.started = False
+        self.finished = False
+        self.real = 0
+        self.last_decode = 0
+        self.streak = 0
+        self.text_since = False
+        self.empty_restarts = 0
+        self.tokens = []
+        self.restarts = []
+
+    def _enc(self, min_new):
+        mel = self.mel.data()
+        new = mel.shape[0] - self.cursor
+        need = 312 if not self.started else min_new
+        if (new < need and not self.finished) or new <= 0:
+            return
+        self.s.encode_mel(mel[self.cursor:])
+        self.started = True
+        self.cursor = mel.shape[0]
+
+    def _dec(self):
+        st = self.s.state()
+        prompt = 1 + 32 + self.delay_tokens
+        started = lib_started(self.s)
+        if not started and self.s.adapter_tokens < prompt:
+            return
+        toks = self.s.decode(stop_at_eos=True).tolist()
+        eos = False
+        for t in toks:
+            if t == 2:
+                eos = True
+            elif t < 1000 or t == 1000:
+                self.streak += 1
+            else:
+                self.streak = 0
+                self.text_since = True
+                self.empty_restarts = 0
+        if toks:
+            self.last_decode = self.real
+        self.tokens += toks
+        if not self.continuous:
+            return
+        st = self.s.state()
+        started = lib_started(self.s)
+        need = 0
+        if eos:
+            need = 1
+        elif started and st["dec_len"] + st["dec_off"] > 2000:
+            need = 2
+        elif started and self.streak >= 64:
+            need = 3
+        elif not self.finished and self.real - self.last_decode >= 16000 * 20:
+            need = 4
+        if not need:
+            return
+        if self.text_since:
+            self.empty_restarts = 0
+        else:
+            self.empty_restarts += 1
+        full = need >= 2 or self.empty_restarts >= 2
+        self.restarts.append((need, full, len(self.tokens)))
+        if full:
+            self.mel.close()
+            self.mel = OracleMel(32 * 1280)
+            self.cursor = 0
+            self.started = False
+            self.s.reset_full()
+            self.empty_restarts = 0
+        else:
+            self.s.reset_decoder()
+        self.streak = 0
+        self.text_since = False
+        self.last_decode = self.real
+
+    def feed(self, samples):
+        self.mel.feed(samples)
+        self.real += len(samples)
+        self._enc(self.min_new)
+        self._dec()
+
+    def flush(self):
+        align = (1280 - (self.real % 1280)) % 1280
+        pad = align + ((self.delay_tokens + 1) + 10) * 1280
+        self.mel.feed(np.zeros(pad, np.float32))
+        self._enc(1)
+        self._dec()
+
+    def finish(self):
+        self.flush()
+        self.finished = True
+        self.mel.finish(0)
+        self._enc(self.min_new)
+        self._dec()
+
+    def close(self):
+        self.mel.close()
+
+
+def lib_started(stream: OracleStream) -> bool:
+    """the oracle stream's decoder has run its prefill (vo_stream_state has no flag for it:
+    a started decoder has generated at least one token since its last reset)"""
+    return stream.state()["gen_pos"] > 0

@@ -119,3 +119,102 @@ def test_cli_q8_checkpoint_in_quantize_py_layout(tmp_path, tiny_weights, jfk_sam
     assert len(ids) > 0
     assert ids == osess.tokens
     os_.close(); om.close()
+
+
+def _write_wav(path, samples):
+    import wave
+    pcm = np.clip(np.round(samples * 32767.0), -32768, 32767).astype("<i2")
+    with wave.open(str(path), "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(16000)
+        w.writeframes(pcm.tobytes())
+
+
+def _text_biased(w):
+    """TINY weights whose control-range embedding rows (ids <= 1000, tied LM head) are
+    scaled down: greedy decoding then emits text ids, so a live stream runs into the KV
+    limit instead of the non-text streak limit."""
+    import copy
+    from vox_weights import EMB, bf16_to_f32, f32_to_bf16
+    w2 = copy.copy(w)
+    w2.t = dict(w.t)
+    name = EMB + ".tok_embeddings.weight"
+    e = bf16_to_f32(w.t[name]).copy()
+    e[:1001] *= 0.05
+    w2.t[name] = f32_to_bf16(e)
+    w2._f32 = {}
+    return w2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bias", ["streak", "kv"])
+def test_cli_continuous_mode_restarts_like_the_reference(tiny_weights, jfk_samples, tmp_path, bias):
+    """Live mode (vox_stream_set_continuous; voxtral.c:1189-1239) on 200 s of audio (jfk
+    repeated) through the C host with --continuous.  "streak": the random TINY model emits
+    runs of control ids, so the decoder restarts on the 64-token non-text streak; "kv":
+    control ids suppressed, so it passes 2000 KV positions.  Both are full resets (new mel
+    context, conv stem, encoder KV).  The ids and the restart count equal the oracle's
+    audio session run with the reference's restart rules."""
+    import vox_oracle
+    from vox_weights import TINY_LONG, write_safetensors
+    w = tiny_weights if bias == "streak" else _text_biased(tiny_weights)
+    ck = tmp_path / "consolidated.safetensors"
+    write_safetensors(w, str(ck))
+    audio = np.concatenate([jfk_samples] * 19)
+    wav = tmp_path / "long.wav"
+    _write_wav(wav, audio)
+    audio = vox_oracle.read_wav(str(wav))
+    r = subprocess.run([CLI, "-d", str(ck), "-i", str(wav), "--continuous"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    ids = [int(t) for t in r.stdout.split()]
+    line = next(l for l in r.stderr.splitlines() if l.startswith("Restarts:"))
+    restarts = int(line.split()[1])
+    om = vox_oracle.OracleModel(TINY_LONG, w)
+    os_ = vox_oracle.OracleStream(om)
+    sess = vox_oracle.OracleAudioSession(os_, interval_s=2.0, continuous=True)
+    for i in range(0, len(audio), 16000):
+        sess.feed(audio[i:i + 16000])
+    sess.finish()
+    print(bias, "oracle restarts", sess.restarts)
+    assert ids == sess.tokens
+    assert restarts == len(sess.restarts) > 0
+    assert any(k == (3 if bias == "streak" else 2) for k, _, _ in sess.restarts)
+    sess.close(); os_.close(); om.close()
+
+
+@pytest.mark.gpu
+def test_cli_alternatives_like_stream_fill_alts(ckpt, tiny_weights, jfk_samples):
+    """--alt 0.5 (main.c:149-154 / vox_stream_set_alt(s, 3, cutoff)): each printed record is
+    the chosen id and the alternatives stream_fill_alts accepts (voxtral.c:955-1010), for
+    text tokens only; checked against the reference rule applied to the oracle's logits."""
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    r = subprocess.run([CLI, "-d", ckpt, "-i", os.path.join(GOLDEN, "jfk.wav"), "--alt", "0.5"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    recs = [[int(x) for x in t.split("|")] for t in r.stdout.split()]
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    os_ = vox_oracle.OracleStream(om)
+    toks, logits = [], []
+    sess = vox_oracle.OracleSession(os_, interval_s=2.0)
+    for kind, mel in vox_oracle.transcribe_mel_schedule(jfk_samples, feed_size=16000):
+        if kind == "finish":
+            sess.finished = True
+        sess._enc(mel, 1 if kind == "flush" else sess.min_new)
+        t, lg = os_.decode(stop_at_eos=True, want_logits=True)
+        toks += t.tolist()
+        logits.append(lg)
+    logits = np.concatenate(logits)
+    assert [rr[0] for rr in recs] == toks
+    n_alt = 0
+    for i, t in enumerate(toks):
+        want, _ = vox_oracle.fill_alts(logits[i], t, 3, 0.5)
+        want = [w for w in want[:3] if w >= 0]
+        if t < 1001 or t == 2:
+            want = [t]
+        assert recs[i] == want, (i, recs[i], want)
+        n_alt += len(want) > 1
+    assert n_alt > 0
+    os_.close(); om.close()

@@ -570,16 +570,27 @@ int vh_set_delay(vh_ctx_t *ctx, int delay_ms) {
 /* ------------------------------------------------------------------------
  * Streaming (voxtral.c:827-851, 1013-1145, 1288-1316, 1640-1667)
  * ------------------------------------------------------------------------ */
+/* live-mode limits (voxtral.c:410-420) */
+#define STREAM_MAX_DECODE_KV 2000
+#define STREAM_MAX_NON_TEXT_STREAK 64
+#define STREAM_MAX_NO_DECODE_SAMPLES (16000 * 20)
+#define STREAM_EMPTY_RESTARTS_FOR_FULL_RESET 2
+#define TOKEN_EOS 2
+#define TOKEN_TEXT_MIN 1000
+
 struct vh_stream {
     vh_ctx_t *ctx;
     vox_hip_stream_t *st;
     vox_hip_mel_t *mel;
     int mel_cursor, conv_started, finished, min_new_mel;
-    long long real_samples;
-    int *queue;
+    long long real_samples, last_decode_sample;
+    int *queue;                 /* records of VH_MAX_ALT ids: chosen id, accepted alternatives, -1 */
     int q_head, q_tail, q_cap;
-    int *dec_buf;
+    int *dec_buf, *alt_buf;
     int generated, chunks, started_decoding;
+    int continuous, n_alt;
+    float alt_cutoff;
+    int nontext_streak, text_since_restart, empty_restarts, restarts, full_resets;
     double enc_ms, dec_ms, prefill_ms;
 };
 
@@ -602,8 +613,10 @@ vh_stream_t *vh_stream_init(vh_ctx_t *ctx) {
     }
     s->min_new_mel = (int)(STREAM_DEFAULT_INTERVAL * 100.0f);
     s->q_cap = 4096;
-    s->queue = malloc(sizeof(int) * s->q_cap);
+    s->queue = malloc(sizeof(int) * VH_MAX_ALT * s->q_cap);
     s->dec_buf = malloc(sizeof(int) * 4096);
+    s->alt_buf = malloc(sizeof(int) * VH_MAX_ALT * 4096);
+    s->n_alt = 1;
     return s;
 }
 
@@ -613,7 +626,31 @@ void vh_stream_free(vh_stream_t *s) {
     vox_hip_stream_free(s->st);
     free(s->queue);
     free(s->dec_buf);
+    free(s->alt_buf);
     free(s);
+}
+
+void vh_stream_set_continuous(vh_stream_t *s, int on) { s->continuous = on ? 1 : 0; }
+
+int vh_stream_set_alt(vh_stream_t *s, int n_alt, float cutoff) {
+    if (n_alt < 1) n_alt = 1;
+    if (n_alt > VH_MAX_ALT) n_alt = VH_MAX_ALT;
+    if (cutoff < 0) cutoff = 0;
+    if (cutoff > 1) cutoff = 1;
+    s->n_alt = n_alt;
+    s->alt_cutoff = cutoff;
+    return vox_hip_stream_set_alt(s->st, n_alt, cutoff);
+}
+
+int vh_token_class(int id) {
+    /* stream_classify_token (voxtral.c:532-539) without the tokenizer: ids below
+     * TOKEN_TEXT_MIN are control tokens; Tekken's id 1000 is the raw byte 0x00, the one text
+     * id whose decode is an empty C string (INVALID); every other text id decodes to a
+     * non-empty piece */
+    if (id == TOKEN_EOS) return VH_TOK_EOS;
+    if (id < TOKEN_TEXT_MIN) return VH_TOK_CONTROL;
+    if (id == TOKEN_TEXT_MIN) return VH_TOK_INVALID;
+    return VH_TOK_TEXT;
 }
 
 void vh_set_processing_interval(vh_stream_t *s, float seconds) {
@@ -622,20 +659,22 @@ void vh_set_processing_interval(vh_stream_t *s, float seconds) {
     if (s->min_new_mel < 1) s->min_new_mel = 1;
 }
 
-static void queue_push(vh_stream_t *s, const int *ids, int n) {
+/* stream_enqueue_token (voxtral.c:542-567): one record per generated id */
+static void queue_push(vh_stream_t *s, const int *recs, int n) {
     for (int i = 0; i < n; i++) {
         const int next = (s->q_tail + 1) % s->q_cap;
         if (next == s->q_head) {  /* full: grow (keeps order) */
-            int *nq = malloc(sizeof(int) * s->q_cap * 2);
+            int *nq = malloc(sizeof(int) * VH_MAX_ALT * s->q_cap * 2);
             int k = 0;
-            for (int j = s->q_head; j != s->q_tail; j = (j + 1) % s->q_cap) nq[k++] = s->queue[j];
+            for (int j = s->q_head; j != s->q_tail; j = (j + 1) % s->q_cap, k++)
+                memcpy(nq + k * VH_MAX_ALT, s->queue + j * VH_MAX_ALT, sizeof(int) * VH_MAX_ALT);
             free(s->queue);
             s->queue = nq;
             s->q_head = 0;
             s->q_tail = k;
             s->q_cap *= 2;
         }
-        s->queue[s->q_tail] = ids[i];
+        memcpy(s->queue + s->q_tail * VH_MAX_ALT, recs + i * VH_MAX_ALT, sizeof(int) * VH_MAX_ALT);
         s->q_tail = (s->q_tail + 1) % s->q_cap;
     }
 }
@@ -662,26 +701,101 @@ static int run_encoder(vh_stream_t *s) {
     return vox_hip_mel_discard_before(s->mel, s->mel_cursor);
 }
 
-/* stream_run_decoder (voxtral.c:1013-1145), non-continuous: drain every adapter row;
- * greedy decoding stops after EOS (token 2) */
+/* stream_reset_full_state (voxtral.c:786-814): new mel context, conv stem, encoder and
+ * decoder state */
+static int reset_full(vh_stream_t *s) {
+    vox_hip_mel_t *m = vox_hip_mel_create(s->st, 32 * RAW_AUDIO_LENGTH_PER_TOK);
+    if (!m) return fail("vox_hip_mel_create: %s", vox_hip_last_error());
+    vox_hip_mel_free(s->mel);
+    s->mel = m;
+    s->mel_cursor = 0;
+    s->conv_started = 0;
+    if (vox_hip_stream_reset(s->st)) return fail("reset: %s", vox_hip_last_error());
+    return 0;
+}
+
+/* stream_run_decoder (voxtral.c:1013-1240): prefill once the prompt's adapter rows exist,
+ * then every available row; greedy decoding stops after EOS (token 2).  In continuous
+ * (live) mode the decoder restarts afterwards on EOS, KV > 2000, a 64-token non-text
+ * streak or 20 s of audio without a decoded token, escalating to a full reset
+ * (voxtral.c:1189-1239). */
 static int run_decoder(vh_stream_t *s) {
+    const int prompt_len = 1 + 32 + s->ctx->delay_tokens;
+    int st6[6];
+    vox_hip_stream_state(s->st, st6);
+    if (!st6[3] && vox_hip_stream_adapter_tokens(s->st) < prompt_len) return 0;  /* waiting for the prompt */
+    int eos = 0;
     for (;;) {
         const double t0 = now_ms();
         const int first = !s->started_decoding;
+        vox_hip_stream_state(s->st, st6);
+        const int gen0 = st6[5];
         /* the first call runs the prefill + first token alone, so its time is the
          * reference's prefill_ms */
         const int n = vox_hip_stream_decode(s->st, first ? 1 : 4096, 1, s->dec_buf, NULL);
         if (n < 0) return fail("decoder: %s", vox_hip_last_error());
         const double dt = now_ms() - t0;
-        if (n == 0) return 0;
+        if (n == 0) break;
         if (first) {
             s->prefill_ms += dt;
             s->started_decoding = 1;
         }
         s->dec_ms += dt;
         s->generated += n;
-        queue_push(s, s->dec_buf, n);
+        s->last_decode_sample = s->real_samples;
+        if (s->n_alt > 1) {
+            if (vox_hip_stream_read_alts(s->st, gen0, n, s->alt_buf, NULL))
+                return fail("alternatives: %s", vox_hip_last_error());
+        } else {
+            for (int i = 0; i < n; i++) {
+                s->alt_buf[i * VH_MAX_ALT] = s->dec_buf[i];
+                for (int a = 1; a < VH_MAX_ALT; a++) s->alt_buf[i * VH_MAX_ALT + a] = -1;
+            }
+        }
+        for (int i = 0; i < n; i++) {
+            const int cls = vh_token_class(s->dec_buf[i]);
+            if (cls == VH_TOK_TEXT) {
+                s->text_since_restart = 1;
+                s->empty_restarts = 0;
+                s->nontext_streak = 0;
+            } else if (cls != VH_TOK_EOS) {
+                s->nontext_streak++;
+                /* alternatives belong to text tokens only (stream_fill_alts is called for
+                 * STREAM_TOK_TEXT) */
+                for (int a = 1; a < VH_MAX_ALT; a++) s->alt_buf[i * VH_MAX_ALT + a] = -1;
+            } else {
+                eos = 1;
+            }
+        }
+        queue_push(s, s->alt_buf, n);
+        if (eos) break;
     }
+    if (!s->continuous) return 0;
+    vox_hip_stream_state(s->st, st6);
+    const int started = st6[3];
+    int need = 0;
+    if (eos) need = 1;
+    else if (started && st6[0] > STREAM_MAX_DECODE_KV) need = 2;
+    else if (started && s->nontext_streak >= STREAM_MAX_NON_TEXT_STREAK) need = 3;
+    else if (!s->finished && s->real_samples - s->last_decode_sample >= STREAM_MAX_NO_DECODE_SAMPLES) need = 4;
+    if (!need) return 0;
+    if (s->text_since_restart) s->empty_restarts = 0;
+    else s->empty_restarts++;
+    const int full = need >= 2 || s->empty_restarts >= STREAM_EMPTY_RESTARTS_FOR_FULL_RESET;
+    s->restarts++;
+    if (full) {
+        s->full_resets++;
+        if (reset_full(s) && vox_hip_stream_reset_decoder(s->st)) return fail("reset: %s", vox_hip_last_error());
+        s->empty_restarts = 0;
+    } else if (vox_hip_stream_reset_decoder(s->st)) {
+        return fail("reset: %s", vox_hip_last_error());
+    }
+    /* stream_reset_decoder_state (voxtral.c:766-783) */
+    s->started_decoding = 0;
+    s->nontext_streak = 0;
+    s->text_since_restart = 0;
+    s->last_decode_sample = s->real_samples;
+    return 0;
 }
 
 int vh_stream_feed(vh_stream_t *s, const float *samples, int n) {
@@ -721,7 +835,17 @@ int vh_stream_finish(vh_stream_t *s) {
 int vh_stream_get(vh_stream_t *s, int *ids, int max) {
     int n = 0;
     while (n < max && s->q_head != s->q_tail) {
-        ids[n++] = s->queue[s->q_head];
+        ids[n++] = s->queue[s->q_head * VH_MAX_ALT];
+        s->q_head = (s->q_head + 1) % s->q_cap;
+    }
+    return n;
+}
+
+int vh_stream_get_alt(vh_stream_t *s, int *recs, int max) {
+    int n = 0;
+    while (n < max && s->q_head != s->q_tail) {
+        memcpy(recs + n * VH_MAX_ALT, s->queue + s->q_head * VH_MAX_ALT, sizeof(int) * VH_MAX_ALT);
+        n++;
         s->q_head = (s->q_head + 1) % s->q_cap;
     }
     return n;
@@ -736,6 +860,8 @@ void vh_stream_stats(const vh_stream_t *s, vh_stats_t *o) {
     o->encoder_ms = s->enc_ms;
     o->decoder_ms = s->dec_ms;
     o->prefill_ms = s->prefill_ms;
+    o->restarts = s->restarts;
+    o->full_resets = s->full_resets;
 }
 
 /* ------------------------------------------------------------------------

@@ -123,6 +123,13 @@ int main(int argc, char** argv) {
     g_gemv_rb = 2;
     add("q8 gemv wo RB2", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ);
     add("q8 gemv w2 RB2", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH);
+    g_gemv_rb = 8;
+    add("q8 gemv qkv RB8", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D);
+    add("q8 gemv w13 RB8", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D);
+    add("q8 gemv lm RB8", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D);
+    g_gemv_rb = 4;
+    add("q8 gemv wo RB4", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ);
+    add("q8 gemv w2 RB4", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH);
     qs = nullptr;
     g_gemv_rb = 0;
     add("gemv w13 same buffer (MALL-hot)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[0], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
@@ -162,9 +169,9 @@ int main(int argc, char** argv) {
     {
         // batched decode GEMMs (16 streams, fragment-major weights and planes); weights are
         // constant-filled, so the packed layout does not matter for timing
-        uint16_t* xp = (uint16_t*)dmalloc((size_t)3 * 16 * 9216 * 2, 1);
+        uint16_t* xp = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * 9216 * 2, 1);
         float* Cs = (float*)dmalloc((size_t)16 * 131072 * 4, 0);
-        float* part = (float*)dmalloc((size_t)16 * 18 * 18432 * 4, 0);
+        float* part = (float*)dmalloc((size_t)2 * 16 * 18 * 18432 * 4, 0);
         for (int nw : {0, 4, 8}) {
             g_skl_nw = nw;
             printf("-- skl NW %d (0 = auto)\n", nw);
@@ -176,6 +183,15 @@ int main(int argc, char** argv) {
                 add(g.n, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
         }
         g_skl_nw = 0;
+        {
+            // streaming encoder chunk (-I 0.5, 25 rows = 2 row blocks of 16)
+            struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
+            for (S g : {S{"skl enc qkv 6144x1280 nb25", 6144, 1280, wqkv.data(), 6144.0 * 1280 * 2},
+                        S{"skl enc wo  1280x2048 nb25", 1280, 2048, wo.data(), 1280.0 * 2048 * 2},
+                        S{"skl enc w13 10240x1280 nb25", 10240, 1280, w13.data(), 10240.0 * 1280 * 2},
+                        S{"skl enc w2  1280x5120 nb25", 1280, 5120, w2.data(), 1280.0 * 5120 * 2}})
+                add(g.n, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 25, part, st)); }, iters, st), g.bytes);
+        }
         const int Rs[] = {0, 2, 2, 4, 4}, NWs[] = {0, 4, 4, 4, 8}, Ds[] = {0, 2, 3, 2, 2};
         for (int cfg = 0; cfg < (int)(sizeof Rs / sizeof Rs[0]); cfg++) {
             g_skf_r = Rs[cfg];

@@ -272,7 +272,9 @@ class Stream:
     def profile(self):
         o = (ctypes.c_double * 8)()
         lib().vox_hip_stream_profile(self.h, o)
-        return {"ms": o[0], "bytes": o[1], "launches": int(o[2]), "avg_ms": o[3]}
+        # kind 0: the W1|W3 GEMV of every layer; 1: the persistent step (all layers)
+        return {"ms": o[0], "bytes": o[1], "launches": int(o[2]), "avg_ms": o[3], "kind": int(o[4]),
+                "bytes_per_launch": o[5]}
 
     def sync(self):
         lib().vox_hip_stream_sync(self.h)

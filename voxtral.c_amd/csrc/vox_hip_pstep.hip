@@ -29,6 +29,15 @@
 // waves of the first H workgroups each take one query head, 32 keys per wave, merged in LDS
 // (voxtral_kernels.c:541-611 semantics: online softmax over the last min(pos+1, W) logical
 // positions).
+//
+// Status (opt-in, VOX_HIP_PSTEP=1): bit-compatible with the oracle
+// bars, and the weight stream alone runs at 35.7 us per Voxtral-4B layer (6.5 TB/s, flags=1
+// in tools/pstep_dbg), but each of the five hand-offs per layer costs ~5 us (attention ~10)
+// and the ring does not hide them: a streamer that issues its refill as it consumes runs at
+// the issue rate of a full memory queue after a boundary, so a landed prefetch is not drained
+// faster than new loads go out.  59 us per layer against 53 for the per-operation graph.  An
+// LDS-DMA loader / consumer split (loaders issue, consumers only read LDS) streamed at only
+// 3.7-4.1 TB/s here.
 #include "vox_hip_internal.h"
 #include "vox_hip_dev.h"
 
@@ -609,9 +618,6 @@ int g_pstep_d = 0;  // tools/pstep_dbg knob: ring depth (0 = default)
 
 static const void* pstep_fn() {
     switch (g_pstep_d) {
-        case 3: return reinterpret_cast<const void*>(&k_pstep<3>);
-        case 4: return reinterpret_cast<const void*>(&k_pstep<4>);
-        case 6: return reinterpret_cast<const void*>(&k_pstep<6>);
         case 8: return reinterpret_cast<const void*>(&k_pstep<8>);
         default: return reinterpret_cast<const void*>(&k_pstep<16>);
     }

@@ -101,6 +101,26 @@ __device__ __forceinline__ float psum(const float* __restrict__ part, int S, int
     for (int s = 1; s < S; s++) v += part[((size_t)s * SK_ROWS + j) * N + n];
     return v;
 }
+// the pair (n, n + 1) of psum (n even), every slab load of a chunk of 8 in flight before
+// its adds (same order of additions: slab 0, 1, 2, ...)
+__device__ __forceinline__ float2 psum2(const float* __restrict__ part, int S, int N, int j, int n) {
+    part += (size_t)(j >> 4) * S * SK_ROWS * N + (size_t)(j & 15) * N + n;
+    const size_t stride = (size_t)SK_ROWS * N;
+    float2 v = *reinterpret_cast<const float2*>(part);
+    for (int s0 = 1; s0 < S; s0 += 8) {
+        float2 t[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            t[c] = s0 + c < S ? *reinterpret_cast<const float2*>(part + (s0 + c) * stride) : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            if (s0 + c < S) {
+                v.x += t[c].x;
+                v.y += t[c].y;
+            }
+    }
+    return v;
+}
 // element (row j, col k) of the fragment-major planes of a row set: plane p of row block j / 16
 __device__ __forceinline__ size_t frag_at(int j, int K, int p, int k) {
     return ((size_t)(j >> 4) * 3 + p) * SK_ROWS * K + frag_off(j & 15, k);

@@ -790,14 +790,36 @@ __global__ __launch_bounds__(HD) void k_attn_tiled_combine(const float* __restri
     __shared__ __attribute__((aligned(16))) float sv[HD];
     const int h = blockIdx.x, q = blockIdx.y, d = threadIdx.x;
     const float* pp = part + (size_t)(h * M + q) * ns * (HD + 2);
-    float mx = -1e30f;
-    for (int z = 0; z < ns; z++) mx = fmaxf(mx, pp[(size_t)z * (HD + 2) + HD]);
-    float num = 0.f, den = 0.f;
-    for (int z = 0; z < ns; z++) {
-        const float* pz = pp + (size_t)z * (HD + 2);
-        const float f = expf(pz[HD] - mx);
-        den = fmaf(f, pz[HD + 1], den);
-        num = fmaf(f, pz[d], num);
+    // every split's (max, sum, value) loads in flight together (chunks of 8 splits); the
+    // merge runs in split order as before
+    float mx = -1e30f, num = 0.f, den = 0.f;
+    for (int z0 = 0; z0 < ns; z0 += 8) {
+        float zm[8], zl[8], zv[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            const float* pz = pp + (size_t)min(z0 + c, ns - 1) * (HD + 2);
+            zm[c] = pz[HD];
+            zl[c] = pz[HD + 1];
+            zv[c] = pz[d];
+        }
+        // rescale the running sums when a later chunk raises the max
+        float cm = mx;
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            if (z0 + c < ns) cm = fmaxf(cm, zm[c]);
+        if (cm > mx) {
+            const float r = expf(mx - cm);
+            num *= r;
+            den *= r;
+            mx = cm;
+        }
+#pragma unroll
+        for (int c = 0; c < 8; c++)
+            if (z0 + c < ns) {
+                const float f = expf(zm[c] - mx);
+                den = fmaf(f, zl[c], den);
+                num = fmaf(f, zv[c], num);
+            }
     }
     const float v = den > 0.f ? num * (1.0f / den) : 0.f;
     if (!xs) {
@@ -1263,13 +1285,15 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             if (j < nq) {
                 const int h = j / (HD / 2), d = j % (HD / 2);
                 const int col = (h0 + h) * HD + 2 * d;
-                const float x0 = psum(F.qkv, F.S, F.N, zb, col), x1 = psum(F.qkv, F.S, F.N, zb, col + 1);
+                const float2 xx = psum2(F.qkv, F.S, F.N, zb, col);
+                const float x0 = xx.x, x1 = xx.y;
                 const float c = rp[2 * d], sn = rp[2 * d + 1];
                 sQ[h][2 * d] = x0 * c - x1 * sn;
                 sQ[h][2 * d + 1] = x0 * sn + x1 * c;
             } else if (j < nq + HD / 2) {
                 const int d = j - nq, col = qd + kvh * HD + 2 * d;
-                const float x0 = psum(F.qkv, F.S, F.N, zb, col), x1 = psum(F.qkv, F.S, F.N, zb, col + 1);
+                const float2 xx = psum2(F.qkv, F.S, F.N, zb, col);
+                const float x0 = xx.x, x1 = xx.y;
                 const float c = rp[2 * d], sn = rp[2 * d + 1];
                 const float k0v = x0 * c - x1 * sn, k1v = x0 * sn + x1 * c;
                 sKn[2 * d] = k0v;
@@ -1765,18 +1789,24 @@ __global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__
     for (int p = t0; p < qd / 2; p += tn) {
         const int d = (2 * p) % hd / 2;
         const float c = rp[2 * d], sn = rp[2 * d + 1];
-        const float x0 = psum(part, S, ld, i, 2 * p), x1 = psum(part, S, ld, i, 2 * p + 1);
+        const float2 xx = psum2(part, S, ld, i, 2 * p);
+        const float x0 = xx.x, x1 = xx.y;
         q[(size_t)i * qd + 2 * p] = x0 * c - x1 * sn;
         q[(size_t)i * qd + 2 * p + 1] = x0 * sn + x1 * c;
     }
     for (int p = t0; p < kvd / 2; p += tn) {
         const int d = (2 * p) % hd / 2;
         const float c = rp[2 * d], sn = rp[2 * d + 1];
-        const float x0 = psum(part, S, ld, i, qd + 2 * p), x1 = psum(part, S, ld, i, qd + 2 * p + 1);
+        const float2 xx = psum2(part, S, ld, i, qd + 2 * p);
+        const float x0 = xx.x, x1 = xx.y;
         kr[2 * p] = x0 * c - x1 * sn;
         kr[2 * p + 1] = x0 * sn + x1 * c;
     }
-    for (int p = t0; p < kvd; p += tn) vr[p] = psum(part, S, ld, i, qd + kvd + p);
+    for (int p = t0; p < kvd / 2; p += tn) {
+        const float2 xx = psum2(part, S, ld, i, qd + kvd + 2 * p);
+        vr[2 * p] = xx.x;
+        vr[2 * p + 1] = xx.y;
+    }
 }
 
 // argmax over row i's logits, first max wins (voxtral_decoder.c:771-779): ARGB slices
@@ -1909,10 +1939,15 @@ __global__ __launch_bounds__(256) void k_slabs_rope_kv(const float* __restrict__
     const int p = blockIdx.x * 256 + threadIdx.x, n = 2 * p;
     if (n >= N) return;
     const int slot = (pos0 + i) % cap;
-    float x0 = psum(part, S, N, i, n), x1 = psum(part, S, N, i, n + 1);
+    // bias and rope first: independent of the slabs, in flight with them
+    const float2 bb = bias ? *reinterpret_cast<const float2*>(bias + n) : make_float2(0.f, 0.f);
+    const float2 cs = n < qd + kvd ? *reinterpret_cast<const float2*>(rope + (size_t)i * hd + 2 * (n % hd / 2))
+                                   : make_float2(1.f, 0.f);
+    const float2 xx = psum2(part, S, N, i, n);
+    float x0 = xx.x, x1 = xx.y;
     if (bias) {
-        x0 += bias[n];
-        x1 += bias[n + 1];
+        x0 += bb.x;
+        x1 += bb.y;
     }
     if (n >= qd + kvd) {
         float* vr = Vc + (size_t)slot * kvd + (n - qd - kvd);
@@ -1920,9 +1955,7 @@ __global__ __launch_bounds__(256) void k_slabs_rope_kv(const float* __restrict__
         vr[1] = x1;
         return;
     }
-    const float* rp = rope + (size_t)i * hd;
-    const int d = n % hd / 2;  // qd is a multiple of hd: the pair's rope index
-    const float c = rp[2 * d], s = rp[2 * d + 1];
+    const float c = cs.x, s = cs.y;  // qd is a multiple of hd: the pair's rope index n % hd / 2
     float* dst = n < qd ? q + (size_t)i * qd + n : Kc + (size_t)slot * kvd + (n - qd);
     dst[0] = x0 * c - x1 * s;
     dst[1] = x0 * s + x1 * c;
@@ -1980,44 +2013,69 @@ __global__ __launch_bounds__(64) void k_rmsnorm_fplanes(const float* __restrict_
 // projection (k_skl, summed in split order as k_resid_slabs), the updated row written back,
 // its sum of squares reduced in the block, the normalised row stored as fragment-major
 // planes.  A thread owns 8 consecutive columns (D <= 8 * 512).
+// EPT consecutive elements per thread (4: D <= 2048, 8: D <= 4096); every load of a thread
+// (row, slabs in chunks, bias, norm weight, ada) goes out before the first wait
+template <int EPT>
 __global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict__ x, int D,
                                                                const float* __restrict__ part, int S,
                                                                const float* __restrict__ bias,
                                                                const float* __restrict__ w,
                                                                const float* __restrict__ ada, float eps,
                                                                uint16_t* __restrict__ xs) {
+    constexpr int NV = EPT / 4;               // float4 per thread
+    constexpr int CH = EPT == 4 ? 16 : 8;     // slabs per load round
     __shared__ float sred[8];
     const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int k = tid * 8;
+    const int k = tid * EPT;
     const bool own = k < D;
-    float v[8];
+    float v[EPT], wv[EPT], av[EPT], bv[EPT];
     float ss = 0.f;
     if (own) {
         float* xr = x + (size_t)j * D + k;
-        const float4 a = *reinterpret_cast<const float4*>(xr), b = *reinterpret_cast<const float4*>(xr + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        if (S > 0) {
-            float r[8];
-            const float* pb = part + (size_t)(j >> 4) * S * SK_ROWS * D;
-#pragma unroll 4
-            for (int s = 0; s < S; s++) {
-                const float* pp = pb + ((size_t)s * SK_ROWS + (j & 15)) * D + k;
-                const float4 c = *reinterpret_cast<const float4*>(pp), d = *reinterpret_cast<const float4*>(pp + 4);
-                const float t[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
 #pragma unroll
-                for (int e = 0; e < 8; e++) r[e] = s ? r[e] + t[e] : t[e];
+        for (int u = 0; u < NV; u++) {
+            const float4 a = *reinterpret_cast<const float4*>(xr + 4 * u);
+            const float4 ww = *reinterpret_cast<const float4*>(w + k + 4 * u);
+            const float4 aa = ada ? *reinterpret_cast<const float4*>(ada + k + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + k + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[4 * u] = a.x; v[4 * u + 1] = a.y; v[4 * u + 2] = a.z; v[4 * u + 3] = a.w;
+            wv[4 * u] = ww.x; wv[4 * u + 1] = ww.y; wv[4 * u + 2] = ww.z; wv[4 * u + 3] = ww.w;
+            av[4 * u] = aa.x; av[4 * u + 1] = aa.y; av[4 * u + 2] = aa.z; av[4 * u + 3] = aa.w;
+            bv[4 * u] = bb.x; bv[4 * u + 1] = bb.y; bv[4 * u + 2] = bb.z; bv[4 * u + 3] = bb.w;
+        }
+        if (S > 0) {
+            float r[EPT];
+            const float* pb = part + (size_t)(j >> 4) * S * SK_ROWS * D + (size_t)(j & 15) * D + k;
+            for (int s0 = 0; s0 < S; s0 += CH) {
+                float4 t[CH][NV];
+#pragma unroll
+                for (int c = 0; c < CH; c++)
+#pragma unroll
+                    for (int u = 0; u < NV; u++)
+                        t[c][u] = s0 + c < S ? *reinterpret_cast<const float4*>(pb + (size_t)(s0 + c) * SK_ROWS * D + 4 * u)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int c = 0; c < CH; c++)
+                    if (s0 + c < S)
+#pragma unroll
+                        for (int u = 0; u < NV; u++) {
+                            const float tt[4] = {t[c][u].x, t[c][u].y, t[c][u].z, t[c][u].w};
+#pragma unroll
+                            for (int e = 0; e < 4; e++) r[4 * u + e] = (s0 + c) ? r[4 * u + e] + tt[e] : tt[e];
+                        }
             }
             if (bias) {
 #pragma unroll
-                for (int e = 0; e < 8; e++) r[e] += bias[k + e];
+                for (int e = 0; e < EPT; e++) r[e] += bv[e];
             }
 #pragma unroll
-            for (int e = 0; e < 8; e++) v[e] += r[e];
-            *reinterpret_cast<float4*>(xr) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<float4*>(xr + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            for (int e = 0; e < EPT; e++) v[e] += r[e];
+#pragma unroll
+            for (int u = 0; u < NV; u++)
+                *reinterpret_cast<float4*>(xr + 4 * u) = make_float4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
         }
 #pragma unroll
-        for (int e = 0; e < 8; e++) ss = fmaf(v[e], v[e], ss);
+        for (int e = 0; e < EPT; e++) ss = fmaf(v[e], v[e], ss);
     }
     ss = wave_sum(ss);
     if (lane == 0) sred[wave] = ss;
@@ -2027,13 +2085,13 @@ __global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict
     for (int i = 0; i < 8; i++) tot += sred[i];
     if (!own) return;
     const float inv = 1.0f / sqrtf(tot / (float)D + eps);
-    uint32_t hp[4], mp[4], lq[4];
+    uint32_t hp[EPT / 2], mp[EPT / 2], lq[EPT / 2];
 #pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-        float v0 = v[e] * inv * w[k + e], v1 = v[e + 1] * inv * w[k + e + 1];
+    for (int e = 0; e < EPT; e += 2) {
+        float v0 = v[e] * inv * wv[e], v1 = v[e + 1] * inv * wv[e + 1];
         if (ada) {
-            v0 *= (1.0f + ada[k + e]);
-            v1 *= (1.0f + ada[k + e + 1]);
+            v0 *= (1.0f + av[e]);
+            v1 *= (1.0f + av[e + 1]);
         }
         uint16_t h0, m0, l0, h1, m1, l1;
         split3(v0, h0, m0, l0);
@@ -2042,9 +2100,16 @@ __global__ __launch_bounds__(512) void k_resid_rmsnorm_fplanes(float* __restrict
         mp[e / 2] = m0 | ((uint32_t)m1 << 16);
         lq[e / 2] = l0 | ((uint32_t)l1 << 16);
     }
-    *reinterpret_cast<uint4*>(xs + frag_at(j, D, 0, k)) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
-    *reinterpret_cast<uint4*>(xs + frag_at(j, D, 1, k)) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
-    *reinterpret_cast<uint4*>(xs + frag_at(j, D, 2, k)) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+    if (EPT == 8) {
+        *reinterpret_cast<uint4*>(xs + frag_at(j, D, 0, k)) = make_uint4(hp[0], hp[1], hp[2 % (EPT / 2)], hp[3 % (EPT / 2)]);
+        *reinterpret_cast<uint4*>(xs + frag_at(j, D, 1, k)) = make_uint4(mp[0], mp[1], mp[2 % (EPT / 2)], mp[3 % (EPT / 2)]);
+        *reinterpret_cast<uint4*>(xs + frag_at(j, D, 2, k)) = make_uint4(lq[0], lq[1], lq[2 % (EPT / 2)], lq[3 % (EPT / 2)]);
+    } else {
+        // 4 consecutive elements share one 8-B run of the fragment layout (frag_off)
+        *reinterpret_cast<uint2*>(xs + frag_at(j, D, 0, k)) = make_uint2(hp[0], hp[1]);
+        *reinterpret_cast<uint2*>(xs + frag_at(j, D, 1, k)) = make_uint2(mp[0], mp[1]);
+        *reinterpret_cast<uint2*>(xs + frag_at(j, D, 2, k)) = make_uint2(lq[0], lq[1]);
+    }
 }
 
 // rows of x (f32) into fragment-major planes
@@ -2278,11 +2343,9 @@ __global__ __launch_bounds__(256) void k_swiglu_fplanes(const float* __restrict_
     const int h0 = c * 2, N = 2 * H;
     const int rg = (h0 >> 4) * 32 + (h0 & 15);  // W1 row of unit h0; its W3 row is rg + 16
     uint16_t hh[2], mm[2], ll[2];
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const float gv = psum(part, S, N, j, rg + q), uv = psum(part, S, N, j, rg + 16 + q);
-        split3(silu(gv) * uv, hh[q], mm[q], ll[q]);
-    }
+    const float2 g2 = psum2(part, S, N, j, rg), u2 = psum2(part, S, N, j, rg + 16);
+    split3(silu(g2.x) * u2.x, hh[0], mm[0], ll[0]);
+    split3(silu(g2.y) * u2.y, hh[1], mm[1], ll[1]);
     // h0 even: one 4-B piece per plane
     *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 0, h0)) = hh[0] | ((uint32_t)hh[1] << 16);
     *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 1, h0)) = mm[0] | ((uint32_t)mm[1] << 16);
@@ -2834,8 +2897,13 @@ hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hi
 hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
                                   uint16_t* xs, const float* part, int S, hipStream_t st, const float* bias) {
     if (nb < 1 || nb > SK_MAX_ROWS || D % 64) return hipErrorInvalidValue;
+    if (D <= 4 * 512 && D % 4 == 0) {
+        hipLaunchKernelGGL(k_resid_rmsnorm_fplanes<4>, dim3(nb), dim3(512), 0, st, x, D, part, S, bias, w, ada, eps, xs);
+        LAUNCH_CHECK();
+        return hipSuccess;
+    }
     if (D <= 8 * 512) {
-        hipLaunchKernelGGL(k_resid_rmsnorm_fplanes, dim3(nb), dim3(512), 0, st, x, D, part, S, bias, w, ada, eps, xs);
+        hipLaunchKernelGGL(k_resid_rmsnorm_fplanes<8>, dim3(nb), dim3(512), 0, st, x, D, part, S, bias, w, ada, eps, xs);
         LAUNCH_CHECK();
         return hipSuccess;
     }

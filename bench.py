@@ -59,6 +59,9 @@ def parse():
                     help="config 3: raw audio fed in -I-sized pieces through the device mel + chunked encoder")
     ap.add_argument("--audio-seconds", type=float, default=180.0, help="config 3 audio length")
     ap.add_argument("--interval", type=float, default=0.5, help="config 3 -I interval (s)")
+    ap.add_argument("--clip-seconds", type=float, default=0.0,
+                    help="config 2's long clips (e.g. 59.75): one vox_transcribe_audio pass over synthetic audio "
+                         "of this length (one-shot feed through the device mel, flush, finish)")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: placeholder host step, same launcher and JSON")
     return ap.parse_args()
@@ -260,7 +263,7 @@ def main():
     mel_dev = vox_hip.DeviceArray(mel)
     if args.streams > 1:
         return bench_streams(args, d, cfg, model, st, mel, mel_dev, rng)
-    if args.streaming:
+    if args.streaming or args.clip_seconds > 0:
         return bench_streaming(args, d, cfg, model, st)
 
     for _ in range(args.warmup):
@@ -299,8 +302,9 @@ def main():
     avg_ms = prof["avg_ms"] if prof["launches"] else float("nan")
     achieved = w13_bytes / (avg_ms * 1e-3) / 1e9 if prof["launches"] else None
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_w13_traffic.json")  # bf16 W1|W3 (tools/pmc.sh)
-    if os.path.exists(pmc) and not args.q8:
+    # W1|W3 HBM bytes per launch from the PMC passes (tools/pmc.sh, tools/pmc_q8.sh)
+    pmc = os.path.join(ROOT, "profiles", "pmc_w13_q8_traffic.json" if args.q8 else "pmc_w13_traffic.json")
+    if os.path.exists(pmc):
         traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
 
     out = {
@@ -404,8 +408,13 @@ def bench_streaming(args, d, cfg, model, st):
     rolling 750-row KV, adapter) with the decoder drained after every piece, then
     vox_stream_finish.  Decoding ignores EOS so the work is fixed."""
     import vox_hip
+    oneshot = args.clip_seconds > 0
+    if oneshot:
+        # vox_transcribe_audio (voxtral.c:1388-1401): every sample in one vox_stream_feed
+        args.audio_seconds = args.clip_seconds
+        args.interval = args.clip_seconds
     audio = synth_audio(args.audio_seconds, 99 + d.rank)
-    piece = max(160, min(int(args.interval * 16000), 16000 * 60))
+    piece = len(audio) if oneshot else max(160, min(int(args.interval * 16000), 16000 * 60))
     secs = len(audio) / 16000.0
 
     class Timed:
@@ -448,7 +457,7 @@ def bench_streaming(args, d, cfg, model, st):
         wall = time.perf_counter() - t0
         sess.close()
         return {"wall": wall, "enc": ts.t_enc + t_mel, "dec": ts.t_dec, "steps": ts.steps,
-                "chunks": len(sess.chunks), "tokens": len(sess.tokens)}
+                "chunks": len(sess.chunks), "chunk_frames": list(sess.chunks), "tokens": len(sess.tokens)}
 
     for _ in range(args.warmup):
         run()
@@ -467,17 +476,25 @@ def bench_streaming(args, d, cfg, model, st):
     enc_w = cfg.enc_layers * (eq + 2 * ekv + eq + 2 * cfg.enc_hidden + cfg.enc_hidden) * cfg.enc_dim * wb
     enc_w += (4 * cfg.enc_dim + cfg.dec_dim) * cfg.dec_dim * wb
     ms_chunk = enc_s * 1000.0 / max(1, sum(r["chunks"] for r in runs))
+    if oneshot:
+        mode = f"{args.clip_seconds} s clip one-shot (config 2 long clip)"
+        workload = (f"{args.clip_seconds} s of 16 kHz audio in one vox_stream_feed + flush + finish "
+                    f"(vox_transcribe_audio): device log-mel, encoder chunks {runs[0]['chunk_frames']} mel frames "
+                    f"(<= 1024-row passes), {runs[0]['steps']} greedy steps")
+    else:
+        mode = f"streaming -I {args.interval} (config 3)"
+        workload = (f"{args.audio_seconds:.0f} s of 16 kHz audio fed in {piece}-sample pieces "
+                    f"(main.c file mode, -I {args.interval}): device log-mel, {runs[0]['chunks']} encoder "
+                    f"chunks, {runs[0]['steps']} greedy steps (KV to ~{runs[0]['steps'] + 40} positions)")
     out = {
         "metric": "decoder tokens/sec + encoder RTF, Voxtral-4B " + ("q8" if args.q8 else "bf16")
-                  + f", streaming -I {args.interval} (config 3), at 1/2/4/8 MI355X",
+                  + f", {mode}, at 1/2/4/8 MI355X",
         "value": round(tok_s, 2), "unit": "tokens/s", "n_gpus": d.world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(wall * 1000.0 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": round(tok_s / d.world / MPS_TOK_S, 2),
         "dtype": "f32", "weights_dtype": "q8" if args.q8 else "bf16",
         "data": "synthetic (seeded random weights of the exact architecture; synthetic speech-band audio)",
-        "config": {"workload": f"{args.audio_seconds:.0f} s of 16 kHz audio fed in {piece}-sample pieces "
-                               f"(main.c file mode, -I {args.interval}): device log-mel, {runs[0]['chunks']} encoder "
-                               f"chunks, {runs[0]['steps']} greedy steps (KV to ~{runs[0]['steps'] + 40} positions)",
+        "config": {"workload": workload,
                    "model": "Voxtral-Mini-4B-Realtime", "global_batch": d.world, "seq_len": runs[0]["steps"],
                    "streams_per_gpu": 1, "parallelism": f"replicas x{d.world} (no collective)"},
         "encoder_rtf": round(enc_s / (secs * args.steps), 5),
@@ -487,6 +504,20 @@ def bench_streaming(args, d, cfg, model, st):
         "encoder_chunk_weight_gbs": round(enc_w / (ms_chunk * 1e-3) / 1e9, 1),
         "decoder_ms_per_token": round(dec_s * 1000.0 / max(1, steps_all / d.world), 4),
     }
+    if oneshot:
+        # long one-shot chunks are MFMA work: useful FLOPs of the schedule (mel + conv + encoder
+        # + adapter time) against the dense bf16 peak (3 bf16 MFMAs per product: issued ~3x)
+        efl = encoder_flops(cfg, runs[0]["chunk_frames"])
+        tf = efl / (enc_s / args.steps) / 1e12
+        out["encoder_roofline"] = {"bound": "mfma", "flops_per_pass": int(efl), "achieved": round(tf, 1),
+                                   "peak": MFMA_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_TFLOPS, 4),
+                                   "mfma_planes": 3, "issued_frac": round(3 * tf / MFMA_BF16_TFLOPS, 4)}
+    else:
+        # ~25-row chunks are far below the MFMA ridge: every chunk streams the encoder +
+        # adapter weights once, so the bound is that byte stream at the HBM peak
+        gbs = enc_w / (ms_chunk * 1e-3) / 1e9
+        out["encoder_roofline"] = {"bound": "hbm", "bytes_per_chunk": enc_w, "achieved": round(gbs, 1),
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     st.close()

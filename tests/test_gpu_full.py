@@ -59,3 +59,83 @@ def test_full_jfk_transcription(full, jfk_samples):
     assert h_tok == o_tok
     hs.close()
     os_.close()
+
+
+def synth_audio(seconds, seed):
+    """Speech-band synthetic audio (no recording offline; the path's work depends only on
+    the length): noise bursts under a slow envelope plus drifting tones."""
+    rng = np.random.default_rng(seed)
+    n = int(seconds * 16000)
+    t = np.arange(n) / 16000.0
+    env = 0.5 + 0.5 * np.sin(2 * np.pi * 0.7 * t) * np.sin(2 * np.pi * 0.13 * t)
+    x = 0.05 * rng.standard_normal(n) * env + 0.1 * env * np.sin(2 * np.pi * (180 + 60 * np.sin(0.5 * t)) * t)
+    return x.astype(np.float32)
+
+
+def test_full_long_clip_one_shot(full):
+    """C2's longest clip (59.75 s, vox_transcribe_audio one-shot, voxtral.c:1388-1401): the
+    first encoder call takes every frame fed so far -- over 3000 encoder rows, run in passes
+    of <= 1024 rows through all 32 layers -- then the flush and finish chunks.  Adapter rows
+    against the oracle, then 8 greedy steps (ids and logits)."""
+    import vox_hip
+    import vox_oracle
+    cfg, hm, om = full
+    events = vox_oracle.transcribe_mel_schedule(synth_audio(59.75, 7))
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    cur = 0
+    for kind, mel in events:
+        assert hs.encode_mel(mel[cur:]) == os_.encode_mel(mel[cur:])
+        cur = mel.shape[0]
+    assert events[0][1].shape[0] // 2 > 3000  # encoder rows of the one-shot chunk (3 passes)
+    assert hs.adapter_tokens == os_.adapter_tokens
+    ra = rel(hs.read_adapter(), os_.read_adapter())
+    assert ra < TOL, ra
+    ht, hl = hs.decode(max_steps=8, stop_at_eos=False, want_logits=True)
+    ot, ol = os_.decode(max_steps=8, stop_at_eos=False, want_logits=True)
+    rl = rel(hl, ol)
+    print(f"59.75 s one-shot: {hs.adapter_tokens} adapter rows rel err {ra:.2e}, 8 steps logits rel err {rl:.2e}")
+    assert np.array_equal(ht, ot) and len(ht) == 8
+    assert rl < TOL, rl
+    hs.close()
+    os_.close()
+
+
+def test_full_streaming_60s_encoder(full):
+    """C3 scale: 60 s of audio fed in -I 0.5 pieces (main.c file mode) through the device
+    log-mel and the chunked encoder (~25-row chunks over the rolling 750-row window, KV ring
+    vs the reference's compaction) against the oracle's session on host mel; the decoder is
+    left out on both sides (the oracle's single-threaded decode would take minutes).  Every
+    chunk size and every adapter row is compared."""
+    import vox_hip
+    import vox_oracle
+    cfg, hm, om = full
+    audio = synth_audio(60.0, 11)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    ha = vox_hip.AudioSession(hs, interval_s=0.5)
+    ha._run_decoder = lambda stop_at_eos=True: None
+    oa = vox_oracle.OracleAudioSession(os_, interval_s=0.5)
+    oa._dec = lambda: None
+    ochunks = []
+    enc = oa._enc
+
+    def counted(min_new):
+        before = oa.cursor
+        enc(min_new)
+        if oa.cursor != before:
+            ochunks.append(oa.cursor - before)
+    oa._enc = counted
+    for i in range(0, len(audio), 8000):
+        ha.feed_samples(audio[i:i + 8000])
+        oa.feed(audio[i:i + 8000])
+    ha.finish_samples()
+    oa.finish()
+    assert len(ha.chunks) > 100
+    assert ha.chunks == ochunks, (ha.chunks[:8], ochunks[:8])
+    assert hs.adapter_tokens == os_.adapter_tokens
+    ra = rel(hs.read_adapter(), os_.read_adapter())
+    print(f"60 s -I 0.5: {len(ha.chunks)} chunks, {hs.adapter_tokens} adapter rows rel err {ra:.2e}")
+    assert ra < TOL, ra
+    ha.close()
+    oa.close()
+    hs.close()
+    os_.close()

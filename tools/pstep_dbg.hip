@@ -211,6 +211,30 @@ int main(int argc, char** argv) {
             tm += sum_med[k] / NL;
         }
         printf("  sum of medians %.2f us per layer; layer 0 QKV start -> last W2 stream end %.2f us\n", tm, (t1 - t0) * 0.01);
+        // each hand-off: the producers' spread (last block's stream end - median block's) and the
+        // latency after the LAST producer (median block's operand-ready time - last stream end)
+        {
+            const int pe[4] = {1, 5, 7, 9}, pr[4] = {4, 6, 8, 0};
+            const char* en[4] = {"QKV -> wo (attention)", "wo -> W13", "W13 -> W2", "W2 -> next QKV"};
+            for (int e = 0; e < 4; e++) {
+                double sk = 0, la = 0;
+                int n = 0;
+                for (int l = 0; l < NL; l++) {
+                    if (e == 3 && l + 1 == NL) continue;
+                    std::vector<double> te, tr;
+                    for (int bb = 0; bb < cus; bb++) {
+                        te.push_back((double)h[((size_t)l * cus + bb) * 16 + pe[e]]);
+                        tr.push_back((double)h[((size_t)(e == 3 ? l + 1 : l) * cus + bb) * 16 + pr[e]]);
+                    }
+                    std::sort(te.begin(), te.end());
+                    std::sort(tr.begin(), tr.end());
+                    sk += (te.back() - te[te.size() / 2]) * 0.01;
+                    la += (tr[tr.size() / 2] - te.back()) * 0.01;
+                    n++;
+                }
+                printf("  edge %-22s producer spread %5.2f us, after last producer %5.2f us\n", en[e], sk / n, la / n);
+            }
+        }
         // streamer wave 0 in the W1|W3 phase: 13 = released after the wo boundary, 10 = first slot
         // consumed, 11 = first slot of local row 3, 12 = last slot consumed (W1|W3 end)
         double dA = 0, dB = 0, dC = 0;
@@ -243,6 +267,26 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&fm, f0, f1));
         const double lb = 2.0 * ((double)NQKV * D + (double)D * DQ + 2.0 * DH * D + (double)D * DH);
         printf("stream only (no hand-offs): %.2f us per layer, %.0f GB/s\n", fm * 100 / NL, lb * NL / (fm * 1e-4) / 1e9);
+        pb.flags = 2;  // consume the first ring contents over and over: no weight traffic
+        CK(launch_pstep(pb, cus, st));
+        CK(hipEventRecord(f0, st));
+        for (int i = 0; i < 10; i++) CK(launch_pstep(pb, cus, st));
+        CK(hipEventRecord(f1, st));
+        CK(hipEventSynchronize(f1));
+        CK(hipEventElapsedTime(&fm, f0, f1));
+        printf("consume only (no loads, no hand-offs): %.2f us per layer (%.0f GB/s equivalent)\n", fm * 100 / NL,
+               lb * NL / (fm * 1e-4) / 1e9);
+        for (int T : {100, 300, 500, 800}) {  // every hand-off replaced by a fixed wait of T x 10 ns
+            pb.flags = 4 | (T << 8);
+            CK(launch_pstep(pb, cus, st));
+            CK(hipEventRecord(f0, st));
+            for (int i = 0; i < 10; i++) CK(launch_pstep(pb, cus, st));
+            CK(hipEventRecord(f1, st));
+            CK(hipEventSynchronize(f1));
+            CK(hipEventElapsedTime(&fm, f0, f1));
+            printf("stream + 4 fixed %.1f us waits per layer: %.2f us per layer (stream + waits = %.2f)\n", T * 0.01,
+                   fm * 100 / NL, 0.0);
+        }
     }
     // timing (repeat launches; the inputs drift, values do not matter here)
     hipEvent_t e0, e1;

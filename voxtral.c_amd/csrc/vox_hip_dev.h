@@ -57,6 +57,14 @@ __device__ __forceinline__ float wave_sum(float v) {
     v += __shfl_xor(v, 32, 64);
     return v;
 }
+// All-DPP wave64 sum (no LDS round trip): the total lands in lane 63 only.
+// row_bcast:15 adds row r-1's lane 15 into rows 1 and 3, row_bcast:31 adds lane 31 into rows 2 and 3.
+__device__ __forceinline__ float wave_sum63(float v) {
+    v = row_sum16(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
+    return v;
+}
 __device__ __forceinline__ float wave_max(float v) {
     v = row_max16(v);
     v = fmaxf(v, __shfl_xor(v, 16, 64));

@@ -47,6 +47,13 @@
 
 namespace vox {
 
+// PS_DIAG (tools/pstep_dbg builds only): 1 = no streamer timeline stamps, 2 = also no operand
+// reads in the streamer's dot products, 3 = a one-add stand-in for the dot product
+#ifndef PS_DIAG
+#define PS_DIAG 0
+#endif
+#define PS_STREAMER_STAMPS (PS_DIAG == 0)
+
 constexpr int PS_SW = 8;                 // streamer waves
 constexpr int PS_AW = 8;                 // aux waves
 constexpr int PS_NT = (PS_SW + PS_AW) * 64;
@@ -262,27 +269,36 @@ __global__ __launch_bounds__(PS_NT, 1) void k_pstep(const PStepArgs a) {
         const float4* xo4 = reinterpret_cast<const float4*>(s_xo);
         int xb = 2 * (kw * cg.CH + lane);
         float acc = 0.f;
+        // the operand chunk of the next slot is read from LDS one slot ahead, so its latency
+        // hides behind this slot's FMAs and refill
+        float4 xa = xo4[xb], xc = xo4[xb + 1];
         for (;;) {
 #pragma unroll
             for (int i = 0; i < PS_D; i++) {
-                acc = dot8(make_uint4(r[i].x, r[i].y, r[i].z, r[i].w), xo4[xb + 128 * cj], xo4[xb + 128 * cj + 1], acc);
-                if (a.stamps && wave == 0 && lane == 0 && cp == 2 && cj == 0 && (ck == 0 || ck == 3))
+#if PS_DIAG == 3
+                acc += __uint_as_float(r[i].x);
+#elif PS_DIAG == 2
+                acc = dot8(make_uint4(r[i].x, r[i].y, r[i].z, r[i].w), make_float4(1.f, 2.f, 3.f, 4.f), make_float4(acc, 2.f, 3.f, 4.f), acc);
+#else
+                acc = dot8(make_uint4(r[i].x, r[i].y, r[i].z, r[i].w), xa, xc, acc);
+#endif
+                if (PS_STREAMER_STAMPS && a.stamps && wave == 0 && lane == 0 && cp == 2 && cj == 0 && (ck == 0 || ck == 3))
                     a.stamps[((size_t)cl * gridDim.x + blockIdx.x) * 16 + 10 + (ck ? 1 : 0)] = __builtin_amdgcn_s_memrealtime();
-                r[i] = issue();
+                if (!(a.flags & 2)) r[i] = issue();  // flags & 2 (diagnostics): consume only, no refills
                 if (++cj == cg.L) {
                     cj = 0;
-                    acc = wave_sum(acc);
-                    if (lane == 0) s_part[(rw + 4 * ck) * 2 + kw] = acc;
+                    acc = wave_sum63(acc);
+                    if (lane == 63) s_part[(rw + 4 * ck) * 2 + kw] = acc;
                     acc = 0.f;
                     if (++ck == cg.nk) {
                         ck = 0;
                         // the aux waves' barriers of this boundary (see their sequence below)
                         const int nb = cp == 0 ? 4 : cp == 1 ? 3 : cp == 2 ? 2 : (cl == nl - 1 ? 1 : 3);
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        if (a.stamps && wave == 0 && lane == 0 && cp == 2)
+                        if (PS_STREAMER_STAMPS && a.stamps && wave == 0 && lane == 0 && cp == 2)
                             a.stamps[((size_t)cl * gridDim.x + blockIdx.x) * 16 + 12] = __builtin_amdgcn_s_memrealtime();
                         for (int q = 0; q < nb; q++) __builtin_amdgcn_s_barrier();
-                        if (a.stamps && wave == 0 && lane == 0 && cp == 1)
+                        if (PS_STREAMER_STAMPS && a.stamps && wave == 0 && lane == 0 && cp == 1)
                             a.stamps[((size_t)cl * gridDim.x + blockIdx.x) * 16 + 13] = __builtin_amdgcn_s_memrealtime();
                         if (++cp == 4) {
                             cp = 0;
@@ -292,6 +308,8 @@ __global__ __launch_bounds__(PS_NT, 1) void k_pstep(const PStepArgs a) {
                         xb = 2 * (kw * cg.CH + lane);
                     }
                 }
+                xa = xo4[xb + 128 * cj];
+                xc = xo4[xb + 128 * cj + 1];
             }
         }
     streamed:
@@ -337,7 +355,7 @@ __global__ __launch_bounds__(PS_NT, 1) void k_pstep(const PStepArgs a) {
         }
     };
     const int Rq = s_geo[0].R, Ro = s_geo[1].R, R2 = s_geo[3].R;
-    const bool skip = (a.flags & 1) != 0;  // diagnostics: barriers only (timing of the weight stream alone)
+    const bool skip = (a.flags & 7) != 0;  // diagnostics: barriers only (timing of the weight stream alone)
 
     // layer 0's QKV operand: the step input x (plain: written by the previous launch)
     {
@@ -362,29 +380,18 @@ __global__ __launch_bounds__(PS_NT, 1) void k_pstep(const PStepArgs a) {
         const int lcap = a.cap;
         PS_STAMP(l, 0);
         if (skip) {
-            ps_barrier();
-            PS_STAMP(l, 1);
-            ps_barrier();
-            PS_STAMP(l, 2);
-            ps_barrier();
-            PS_STAMP(l, 3);
-            ps_barrier();
-            PS_STAMP(l, 4);
-            ps_barrier();
-            PS_STAMP(l, 5);
-            ps_barrier();
-            ps_barrier();
-            PS_STAMP(l, 6);
-            ps_barrier();
-            PS_STAMP(l, 7);
-            ps_barrier();
-            PS_STAMP(l, 8);
-            ps_barrier();
-            PS_STAMP(l, 9);
-            if (l != nl - 1) {
+            // flags & 4 (diagnostics): every hand-off replaced by a wait of flags >> 8 ticks (10 ns)
+            const uint64_t T = (uint64_t)(a.flags >> 8);
+            auto edge = [&](int nb) {
                 ps_barrier();
-                ps_barrier();
-            }
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (__builtin_amdgcn_s_memrealtime() - t0 < T) __builtin_amdgcn_s_sleep(1);
+                for (int q = 1; q < nb; q++) ps_barrier();
+            };
+            edge(4);
+            edge(3);
+            edge(2);
+            edge(l != nl - 1 ? 3 : 1);
             continue;
         }
         // attention: wave aw takes keys [first + 32 aw, +32) in 4 blocks of 8; lane = (key kk,

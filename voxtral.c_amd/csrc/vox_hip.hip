@@ -477,6 +477,9 @@ struct vox_hip_stream {
     size_t gws_n;
     uint16_t* exp_;          // skinny encoder: row planes [4][3][16][max K] (fragment order)
     float* eslab;            // skinny encoder: split-K slabs [4][S][16][N]
+    uint16_t* exp2;          // k_sklx: the second planes buffer (wo / w2 inputs)
+    int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
+    float* essq;             // k_sklx row sums of squares per column slice [2][slices][16]
     int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
     float alt_cutoff;
     int graph_alt;           // alt mode the step graphs were captured with
@@ -684,7 +687,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
-    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab);
+    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2);
     dfree(s->ptab); dfree(s->pgran); dfree(s->pctl);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
@@ -980,6 +983,15 @@ static bool enc_skinny_ok(const vox_hip_config_t& c) {
            (2 * EH) % 64 == 0 && ED <= 8 * 512;
 }
 
+static int enc_fused_env() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VOX_HIP_ENC_FUSED");
+        v = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return v;
+}
+
 static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long long pos0, const float* rope) {
     vox_hip_model_t* m = s->m;
     const vox_hip_config_t& c = m->c;
@@ -994,9 +1006,74 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
                                      std::max((size_t)skl_splits(ED) * 2 * EH, (size_t)skl_splits(EH) * ED));
         CK(dalloc(&s->exp_, (size_t)2 * 3 * SK_ROWS * kmax));
         CK(dalloc(&s->eslab, (size_t)2 * SK_ROWS * slab));
+        CK(dalloc(&s->eticket, (size_t)SKX_TICKETS));
+        CK(dalloc(&s->essq, (size_t)2 * SK_ROWS * (ED / 64)));
     }
     uint16_t* xp = s->exp_;
     float* sl = s->eslab;
+    if (enc_fused_env() && !m->enc[0].sqkv) {
+        // bf16: the row kernels folded into the projections (k_sklx): 5 launches per layer.
+        // Planes alternate between two buffers so that no launch overwrites its own input:
+        // xa = the QKV / W1|W3 inputs (x * norm weight), xq = the wo / w2 inputs.
+        if (!s->exp2) CK(dalloc(&s->exp2, (size_t)2 * 3 * SK_ROWS * std::max(ED, std::max(EQ, EH))));
+        uint16_t *xa = xp, *xq = s->exp2;
+        SklFused f;
+        f.part = sl;
+        f.ticket = s->eticket;
+        f.eps = c.enc_eps;
+        const int nsl_wo = sklx_slices(ED, EQ), nsl_w2 = sklx_slices(ED, EH);
+        CK(launch_rmsnorm_fplanes(x, n, ED, m->enc[0].attn_norm, nullptr, c.enc_eps, xa, nullptr, 0, st));
+        for (int l = 0; l < c.enc_layers; l++) {
+            const EncLayerD& L = m->enc[l];
+            const DecFragD& F = m->efrag[l];
+            float* Kc = s->ek + (size_t)l * s->ecap * EKV;
+            float* Vc = s->ev + (size_t)l * s->ecap * EKV;
+            // QKV (attention RMSNorm: layer 0 normalised planes, then x * w planes scaled by
+            // the inverse RMS), bias + RoPE + K/V append epilogue (encoder.c:562-607)
+            SklFused q = f;
+            q.ssq_in = s->essq;
+            q.nsl = nsl_w2;
+            q.bias = L.bqkv;
+            q.rope = rope;
+            q.qd = EQ;
+            q.kvd = EKV;
+            q.hd = hd;
+            q.pos0 = (int)pos0;
+            q.cap = s->ecap;
+            q.q = s->q;
+            q.Kc = Kc;
+            q.Vc = Vc;
+            CK(launch_gemm_sklx(l ? SKX_PRO_SCALE : SKX_PRO_PLANES, SKX_EPI_QKV, xa, ED, F.wqkv, NQKV, n, q, st));
+            CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale,
+                                 st, s->gws, s->gws_n, xq));
+            // wo + bias residual (encoder.c:640-644); the FFN norm's planes and row sums of squares
+            SklFused o = f;
+            o.x = x;
+            o.bias = L.bo;
+            o.ssq_out = s->essq;
+            o.planes = xa;
+            o.nw = L.ffn_norm;
+            CK(launch_gemm_sklx(SKX_PRO_PLANES, SKX_EPI_RESID, xq, EQ, F.wo, ED, n, o, st));
+            // W1|W3 (FFN RMSNorm), SwiGLU epilogue into the w2 planes (encoder.c:646-676)
+            SklFused u = f;
+            u.ssq_in = s->essq;
+            u.nsl = nsl_wo;
+            u.planes = xq;
+            CK(launch_gemm_sklx(SKX_PRO_SCALE, SKX_EPI_SWIGLU, xa, ED, F.w13, 2 * EH, n, u, st));
+            // w2 + bias residual (encoder.c:678-684); the next layer's attention-norm planes
+            SklFused d = f;
+            d.x = x;
+            d.bias = L.b2;
+            d.ssq_out = s->essq;
+            if (l + 1 < c.enc_layers) {
+                d.planes = xa;
+                d.nw = m->enc[l + 1].attn_norm;
+            }
+            CK(launch_gemm_sklx(SKX_PRO_PLANES, SKX_EPI_RESID, xq, EH, F.w2, ED, n, d, st));
+        }
+        CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, n, ED, c.enc_eps, st));
+        return 0;
+    }
     for (int l = 0; l < c.enc_layers; l++) {
         const EncLayerD& L = m->enc[l];
         const DecFragD& F = m->efrag[l];

@@ -150,6 +150,41 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
 int skl_splits(int K);
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
                            float* part, hipStream_t st);
+// k_sklx: k_skl with the neighbouring row kernels folded in (bf16 weights).  Inputs are
+// always planes; SKX_PRO_SCALE planes hold x * w (* (1 + ada)) of an RMSNorm whose inverse RMS
+// is applied to the MFMA results, computed from the row sums of squares that the producer left
+// per column slice (ssq_in[rb][nsl][16], summed in slice order).  Epilogue: the slabs go out
+// write-through and one ticket per (row block, column slice) counts them; the block that
+// completes a slice sums its S slabs in split order (as psum) and finishes it: SKX_EPI_QKV =
+// bias + RoPE + K/V ring append (k_slabs_rope_kv), SKX_EPI_RESID = x += slabs + bias, the
+// slice's row sums of squares to ssq_out[rb][X][16] and (planes != null) the next
+// projection's planes x * nw (* (1 + ada)), SKX_EPI_SWIGLU = silu(W1) * W3 into the next
+// projection's planes (k_swiglu_fplanes).
+enum { SKX_PRO_PLANES = 0, SKX_PRO_SCALE = 1 };
+enum { SKX_EPI_QKV = 1, SKX_EPI_RESID = 2, SKX_EPI_SWIGLU = 3 };
+struct SklFused {
+    const float* ssq_in = nullptr;
+    int nsl = 0;
+    float eps = 0.f;
+    float* part = nullptr;
+    int* ticket = nullptr;  // zeroed once; every finishing block resets its own
+    const float* bias = nullptr;
+    float* x = nullptr;
+    float* ssq_out = nullptr;
+    uint16_t* planes = nullptr;
+    const float* nw = nullptr;   // SKX_EPI_RESID planes: the next RMSNorm's weight (and ada)
+    const float* ada = nullptr;
+    const float* rope = nullptr;  // row of position pos0
+    int qd = 0, kvd = 0, hd = 0, pos0 = 0, cap = 0;
+    float* q = nullptr;
+    float* Kc = nullptr;
+    float* Vc = nullptr;
+};
+// column slices of a k_sklx launch (the ssq_out slices its consumer sums)
+int sklx_slices(int N, int K);
+constexpr int SKX_TICKETS = 4 * 1024;
+hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const void* Wf, int N, int nb,
+                            const SklFused& f, hipStream_t st);
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

@@ -2278,13 +2278,26 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
     constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
     constexpr int NF = KS * 6 / NW;  // 16-B plane pieces per thread
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int KB = K >> 6, s = blockIdx.y, kb0 = s * KS;
-    const int g = blockIdx.x * NW + wave;
+    const int KB = K >> 6, S = KB / KS, X = N / (16 * NW);
+    // 1-D grid.  Z > 1 row blocks (more than 16 rows): the Z blocks that stream the same weight
+    // slice u = 8q + r for row blocks z = 0..Z-1 are ids (qZ + z) * 8 + r, i.e. the same XCD
+    // under round-robin placement and dispatched together, so the repeat reads of each weight
+    // byte hit that XCD's L2 instead of HBM (placement is a speed matter only, never correctness)
+    int u = blockIdx.x, z = 0;
+    const int Z = (nb + SK_ROWS - 1) / SK_ROWS;
+    if (Z > 1) {
+        const int t = u >> 3;
+        z = t % Z;
+        u = (t / Z) * 8 + (u & 7);
+        if (u >= X * S) return;
+    }
+    const int s = u / X, kb0 = s * KS;
+    const int g = (u % X) * NW + wave;
     const size_t P = (size_t)SK_ROWS * K;
-    // row block blockIdx.z: its planes and slabs ([rb][3][16][K], [rb][S][16][N])
-    xs += (size_t)blockIdx.z * 3 * P;
-    part += (size_t)blockIdx.z * gridDim.y * SK_ROWS * N;
-    nb -= blockIdx.z * SK_ROWS;
+    // row block z: its planes and slabs ([rb][3][16][K], [rb][S][16][N])
+    xs += (size_t)z * 3 * P;
+    part += (size_t)z * S * SK_ROWS * N;
+    nb -= z * SK_ROWS;
     // planes first: vmcnt retires in issue order, so the weights issued after them stay in
     // flight while the plane pieces are written to LDS
     uint4 f[NF];
@@ -2350,6 +2363,219 @@ __global__ __launch_bounds__(256) void k_swiglu_fplanes(const float* __restrict_
     *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 0, h0)) = hh[0] | ((uint32_t)hh[1] << 16);
     *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 1, h0)) = mm[0] | ((uint32_t)mm[1] << 16);
     *reinterpret_cast<uint32_t*>(xs + frag_at(j, H, 2, h0)) = ll[0] | ((uint32_t)ll[1] << 16);
+}
+
+// ============================================================================
+// k_sklx: k_skl (above) with its neighbouring row kernels folded in, for the streaming
+// encoder's ~25-row chunks where those kernels (5 us each, latency only) cost as much as the
+// projections.  Same grid, planes and MFMA loop as k_skl (bf16 weights); see SklFused.
+// ============================================================================
+template <int NW, int KS, int PRO, int EPI>
+__global__ __launch_bounds__(NW * 64) void k_sklx(const uint16_t* __restrict__ xs, int K,
+                                                  const uint8_t* __restrict__ W, int N, int nb, const SklFused f) {
+    __shared__ uint4 xb[KS * 6 * 64];  // [block][plane][half][lane]
+    __shared__ float s_ss[PRO == SKX_PRO_SCALE ? 2 * NW * 64 : 1];
+    __shared__ int s_fin;
+    constexpr int FB = 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int KB = K >> 6, S = KB / KS, X = N / (16 * NW);
+    // 1-D grid, row blocks of one weight slice on one XCD (k_skl)
+    int u = blockIdx.x, z = 0;
+    const int Z = (nb + SK_ROWS - 1) / SK_ROWS;
+    if (Z > 1) {
+        const int t = u >> 3;
+        z = t % Z;
+        u = (t / Z) * 8 + (u & 7);
+        if (u >= X * S) return;
+    }
+    const int s = u / X, xi = u % X, kb0 = s * KS;
+    const int g = xi * NW + wave;
+    const int nbz = min(nb - z * SK_ROWS, SK_ROWS);  // rows of this row block
+    const __amdgpu_buffer_rsrc_t Wd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g * KB * FB, 0, KB * FB, 0x00020000);
+    u32x4 a[KS][2];
+    constexpr int NF = KS * 6 / NW;
+    const size_t P = (size_t)SK_ROWS * K;
+    const uint16_t* xz = xs + (size_t)z * 3 * P;
+    uint4 fp[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        const int idx = tid + i * NW * 64;
+        const int blk = idx / 384, rem = idx % 384;
+        const int p = rem >> 7, t = (rem >> 6) & 1, l = rem & 63;
+        fp[i] = *reinterpret_cast<const uint4*>(xz + p * P + (size_t)((kb0 + blk) * 2 + t) * 512 + l * 8);
+    }
+    // SKX_PRO_SCALE: the producer's per-slice row sums of squares, all in flight at once
+    const int nss = PRO == SKX_PRO_SCALE ? f.nsl * SK_ROWS : 0;
+    const float* sp = f.ssq_in + (size_t)z * nss;
+    float ss0 = 0.f, ss1 = 0.f;
+    if (PRO == SKX_PRO_SCALE) {
+        if (tid < nss) ss0 = sp[tid];
+        if (tid + NW * 64 < nss) ss1 = sp[tid + NW * 64];
+    }
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+            a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(Wd, lane * 16 + t * 1024, (kb0 + kb) * FB, 2);
+#pragma unroll
+    for (int i = 0; i < NF; i++) xb[tid + i * NW * 64] = fp[i];
+    if (PRO == SKX_PRO_SCALE) {
+        if (tid < nss) s_ss[tid] = ss0;
+        if (tid + NW * 64 < nss) s_ss[tid + NW * 64] = ss1;
+    }
+    __syncthreads();
+    // the inverse RMS of this lane's row j = lane & 15 (slices summed in order, every thread alike)
+    float inv = 1.f;
+    if (PRO == SKX_PRO_SCALE) {
+        float ss = 0.f;
+        for (int q = 0; q < f.nsl; q++) ss += s_ss[q * SK_ROWS + (lane & 15)];
+        inv = 1.0f / sqrtf(ss / (float)K + f.eps);
+    }
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const u32x4 q = a[kb][t];
+            const bf16x8 af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, xb[((kb * 3 + p) * 2 + t) * 64 + lane]),
+                                                             acc, 0, 0, 0);
+        }
+    if (PRO == SKX_PRO_SCALE) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[i] *= inv;
+    }
+    // slab [z][s][16][N] out write-through (sc1), then the slice's ticket
+    const size_t zbase = (size_t)z * S * SK_ROWS * N;
+    const __amdgpu_buffer_rsrc_t Pd = __builtin_amdgcn_make_buffer_rsrc(f.part + zbase, 0, S * SK_ROWS * N * 4, 0x00020000);
+    {
+        const int j = lane & 15;
+        if (j < nbz)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]), __float_as_uint(acc[3])}, Pd,
+                (((s * SK_ROWS + j) * N) + g * 16 + (lane >> 4) * 4) * 4, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* tk = f.ticket + z * X + xi;
+    if (tid == 0) s_fin = S == 1 || atomicAdd(tk, 1) == S - 1;
+    __syncthreads();
+    if (!s_fin) return;
+    if (tid == 0 && S > 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- this block completes slice xi: columns [c0, c0 + 16 NW) of rows z * 16 + j ----
+    const int c0 = xi * NW * 16;
+    auto slab2 = [&](int j, int n) -> float2 {  // psum2 over write-through slabs (sc1 loads)
+        float2 v = make_float2(0.f, 0.f);
+        for (int s0 = 0; s0 < S; s0 += 8) {
+            u32x2 t[8];
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+                if (s0 + c < S)
+                    t[c] = __builtin_amdgcn_raw_buffer_load_b64(Pd, (((s0 + c) * SK_ROWS + j) * N + n) * 4, 0, 16);
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+                if (s0 + c < S) {
+                    v.x = (s0 + c) ? v.x + __uint_as_float(t[c].x) : __uint_as_float(t[c].x);
+                    v.y = (s0 + c) ? v.y + __uint_as_float(t[c].y) : __uint_as_float(t[c].y);
+                }
+        }
+        return v;
+    };
+    if (EPI == SKX_EPI_RESID) {
+        // thread: row j, 4 consecutive columns; x += (slabs + bias); row sums of squares
+        constexpr int TPR = NW * 4;  // threads per row (16 or 32, inside one wave)
+        const int j = tid / TPR, n = c0 + 4 * (tid % TPR);
+        float ss = 0.f;
+        if (j < nbz) {
+            float* xr = f.x + (size_t)(z * SK_ROWS + j) * N + n;
+            const float4 xo = *reinterpret_cast<const float4*>(xr);
+            const float4 bb = f.bias ? *reinterpret_cast<const float4*>(f.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float2 r0 = slab2(j, n), r1 = slab2(j, n + 2);
+            float r[4] = {r0.x, r0.y, r1.x, r1.y};
+            if (f.bias) {
+                r[0] += bb.x;
+                r[1] += bb.y;
+                r[2] += bb.z;
+                r[3] += bb.w;
+            }
+            const float4 v = make_float4(xo.x + r[0], xo.y + r[1], xo.z + r[2], xo.w + r[3]);
+            *reinterpret_cast<float4*>(xr) = v;
+            ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+            if (f.planes) {
+                // the next projection's planes: x * w (* (1 + ada)); its inverse RMS is applied
+                // to its MFMA results (SKX_PRO_SCALE)
+                const float4 ww = *reinterpret_cast<const float4*>(f.nw + n);
+                const float4 aa = f.ada ? *reinterpret_cast<const float4*>(f.ada + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float ve[4] = {v.x, v.y, v.z, v.w}, we[4] = {ww.x, ww.y, ww.z, ww.w}, ae[4] = {aa.x, aa.y, aa.z, aa.w};
+                uint16_t hh[4], mm[4], ll[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    float y = ve[e] * we[e];
+                    if (f.ada) y *= (1.0f + ae[e]);
+                    split3(y, hh[e], mm[e], ll[e]);
+                }
+                const int jj = z * SK_ROWS + j;
+                *reinterpret_cast<uint2*>(f.planes + frag_at(jj, N, 0, n)) =
+                    make_uint2(hh[0] | ((uint32_t)hh[1] << 16), hh[2] | ((uint32_t)hh[3] << 16));
+                *reinterpret_cast<uint2*>(f.planes + frag_at(jj, N, 1, n)) =
+                    make_uint2(mm[0] | ((uint32_t)mm[1] << 16), mm[2] | ((uint32_t)mm[3] << 16));
+                *reinterpret_cast<uint2*>(f.planes + frag_at(jj, N, 2, n)) =
+                    make_uint2(ll[0] | ((uint32_t)ll[1] << 16), ll[2] | ((uint32_t)ll[3] << 16));
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < TPR; o <<= 1) ss += __shfl_xor(ss, o, 64);
+        if (tid % TPR == 0) f.ssq_out[((size_t)z * X + xi) * SK_ROWS + j] = ss;
+    } else if (EPI == SKX_EPI_SWIGLU) {
+        // thread: row j, hidden units h0, h0 + 1 (W1 row rg, W3 row rg + 16: upload_w13)
+        constexpr int TPR = NW * 4;
+        const int j = tid / TPR, pp = tid % TPR;
+        if (j < nbz) {
+            const int H = N / 2, h0 = xi * NW * 8 + 2 * pp;
+            const int rg = (h0 >> 4) * 32 + (h0 & 15);
+            const float2 g2 = slab2(j, rg), u2 = slab2(j, rg + 16);
+            uint16_t hh[2], mm[2], ll[2];
+            split3(silu(g2.x) * u2.x, hh[0], mm[0], ll[0]);
+            split3(silu(g2.y) * u2.y, hh[1], mm[1], ll[1]);
+            const int jj = z * SK_ROWS + j;
+            *reinterpret_cast<uint32_t*>(f.planes + frag_at(jj, H, 0, h0)) = hh[0] | ((uint32_t)hh[1] << 16);
+            *reinterpret_cast<uint32_t*>(f.planes + frag_at(jj, H, 1, h0)) = mm[0] | ((uint32_t)mm[1] << 16);
+            *reinterpret_cast<uint32_t*>(f.planes + frag_at(jj, H, 2, h0)) = ll[0] | ((uint32_t)ll[1] << 16);
+        }
+    } else {
+        // SKX_EPI_QKV: column pairs (n, n + 1), two per thread (k_slabs_rope_kv)
+        constexpr int PPR = NW * 8;  // pairs per row
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+            const int item = tid + it * NW * 64;
+            const int j = item / PPR, n = c0 + 2 * (item % PPR);
+            if (j >= nbz) continue;
+            const int i = z * SK_ROWS + j;
+            const int slot = (f.pos0 + i) % f.cap;
+            const float2 bb = f.bias ? *reinterpret_cast<const float2*>(f.bias + n) : make_float2(0.f, 0.f);
+            const float2 cs = n < f.qd + f.kvd
+                                  ? *reinterpret_cast<const float2*>(f.rope + (size_t)i * f.hd + 2 * (n % f.hd / 2))
+                                  : make_float2(1.f, 0.f);
+            const float2 xx = slab2(j, n);
+            float x0 = xx.x, x1 = xx.y;
+            if (f.bias) {
+                x0 += bb.x;
+                x1 += bb.y;
+            }
+            if (n >= f.qd + f.kvd) {
+                float* vr = f.Vc + (size_t)slot * f.kvd + (n - f.qd - f.kvd);
+                vr[0] = x0;
+                vr[1] = x1;
+                continue;
+            }
+            float* dst = n < f.qd ? f.q + (size_t)i * f.qd + n : f.Kc + (size_t)slot * f.kvd + (n - f.qd);
+            dst[0] = x0 * cs.x - x1 * cs.y;
+            dst[1] = x0 * cs.y + x1 * cs.x;
+        }
+    }
 }
 
 // im2col for the causal conv stem (voxtral_kernels.c:430-447):
@@ -2985,8 +3211,11 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
 template <int Q, int NW, int KS>
 static hipError_t skl_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
                              float* part, hipStream_t st) {
-    hipLaunchKernelGGL((k_skl<Q, NW, KS>), dim3(N / (16 * NW), K / (64 * KS), (nb + SK_ROWS - 1) / SK_ROWS),
-                       dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W), wscale, N, nb, part);
+    const int units = (N / (16 * NW)) * (K / (64 * KS));
+    const int Z = (nb + SK_ROWS - 1) / SK_ROWS;
+    const int grid = Z > 1 ? (units + 7) / 8 * 8 * Z : units;
+    hipLaunchKernelGGL((k_skl<Q, NW, KS>), dim3(grid), dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W),
+                       wscale, N, nb, part);
     return hipGetLastError();
 }
 
@@ -3013,6 +3242,54 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
     SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4)
     SKL_X(1, 4, 8) SKL_X(1, 8, 8) SKL_X(1, 4, 4) SKL_X(1, 8, 4)
 #undef SKL_X
+    return hipErrorInvalidValue;
+}
+
+static int sklx_nw(int N, int K) {
+    // waves per block as launch_gemm_skl picks them
+    const int S = skl_splits(K);
+    const int nb8 = (N / 128) * S;
+    int nw = g_skl_nw ? g_skl_nw : (N % 128 == 0 && nb8 >= (N <= 4096 ? 128 : 384) ? 8 : 4);
+    if (N % (16 * nw)) nw = 4;
+    return nw;
+}
+
+int sklx_slices(int N, int K) { return N / (16 * sklx_nw(N, K)); }
+
+template <int NW, int KS, int PRO, int EPI>
+static hipError_t sklx_launch(const uint16_t* xs, int K, const void* W, int N, int nb, const SklFused& f,
+                              hipStream_t st) {
+    const int units = (N / (16 * NW)) * (K / (64 * KS));
+    const int Z = (nb + SK_ROWS - 1) / SK_ROWS;
+    const int grid = Z > 1 ? (units + 7) / 8 * 8 * Z : units;
+    hipLaunchKernelGGL((k_sklx<NW, KS, PRO, EPI>), dim3(grid), dim3(NW * 64), 0, st, xs, K,
+                       static_cast<const uint8_t*>(W), N, nb, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const void* Wf, int N, int nb,
+                            const SklFused& f, hipStream_t st) {
+    const int S = skl_splits(K);
+    if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S || !f.part || !f.ticket) return hipErrorInvalidValue;
+    const int ks = K / 64 / S, nw = sklx_nw(N, K);
+    if (N % (16 * nw) || (N / (16 * nw)) * ((nb + SK_ROWS - 1) / SK_ROWS) > SKX_TICKETS) return hipErrorInvalidValue;
+    if (!xs || (pro == SKX_PRO_SCALE && (!f.ssq_in || f.nsl < 1 || f.nsl * SK_ROWS > 2 * nw * 64)))
+        return hipErrorInvalidValue;
+    if (epi == SKX_EPI_RESID && f.planes && !f.nw) return hipErrorInvalidValue;
+    if (epi == SKX_EPI_RESID && (!f.x || !f.ssq_out)) return hipErrorInvalidValue;
+    if (epi == SKX_EPI_SWIGLU && (!f.planes || N % 64)) return hipErrorInvalidValue;
+    if (epi == SKX_EPI_QKV && (!f.q || !f.Kc || !f.Vc || !f.rope || f.hd % 2 || f.qd % f.hd || f.cap < 1 ||
+                               N != f.qd + 2 * f.kvd))
+        return hipErrorInvalidValue;
+#define SKX_X(NWW, KSS, PP, EE) \
+    if (nw == NWW && ks == KSS && pro == PP && epi == EE) return sklx_launch<NWW, KSS, PP, EE>(xs, K, Wf, N, nb, f, st);
+#define SKX_CFG(PP, EE) SKX_X(4, 4, PP, EE) SKX_X(4, 8, PP, EE) SKX_X(8, 4, PP, EE) SKX_X(8, 8, PP, EE)
+    SKX_CFG(SKX_PRO_PLANES, SKX_EPI_QKV)
+    SKX_CFG(SKX_PRO_SCALE, SKX_EPI_QKV)
+    SKX_CFG(SKX_PRO_PLANES, SKX_EPI_RESID)
+    SKX_CFG(SKX_PRO_SCALE, SKX_EPI_SWIGLU)
+#undef SKX_CFG
+#undef SKX_X
     return hipErrorInvalidValue;
 }
 

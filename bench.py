@@ -212,6 +212,12 @@ def cpu_model():
     return "unknown"
 
 
+def gemm_planes():
+    """bf16 activation planes k_gemm2 issues per useful MFMA (csrc/vox_hip_kernels.hip
+    gemm_planes: 2 unless VOX_HIP_GEMM_PLANES=3)"""
+    return 3 if os.environ.get("VOX_HIP_GEMM_PLANES", "") == "3" else 2
+
+
 def encoder_flops(cfg, mel_chunks):
     """Useful FLOPs of one stream_run_encoder pass over the given mel chunks (conv stem,
     encoder layers incl. windowed attention, adapter), following the
@@ -354,8 +360,8 @@ def main():
     enc_tf = efl / (enc_s / args.steps) / 1e12
     out["encoder_roofline"] = {"bound": "mfma", "flops_per_pass": int(efl), "achieved": round(enc_tf, 1),
                                "peak": MFMA_BF16_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(enc_tf / MFMA_BF16_TFLOPS, 4), "mfma_planes": 3,
-                               "issued_frac": round(3 * enc_tf / MFMA_BF16_TFLOPS, 4)}
+                               "frac": round(enc_tf / MFMA_BF16_TFLOPS, 4), "mfma_planes": gemm_planes(),
+                               "issued_frac": round(gemm_planes() * enc_tf / MFMA_BF16_TFLOPS, 4)}
     if keep_host:
         out["cpu_baseline"] = cpu_baseline(cfg, w, mel, args.cpu_steps, q8=args.q8)
     if d.rank == 0:
@@ -511,7 +517,8 @@ def bench_streaming(args, d, cfg, model, st):
         tf = efl / (enc_s / args.steps) / 1e12
         out["encoder_roofline"] = {"bound": "mfma", "flops_per_pass": int(efl), "achieved": round(tf, 1),
                                    "peak": MFMA_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_TFLOPS, 4),
-                                   "mfma_planes": 3, "issued_frac": round(3 * tf / MFMA_BF16_TFLOPS, 4)}
+                                   "mfma_planes": gemm_planes(),
+                                   "issued_frac": round(gemm_planes() * tf / MFMA_BF16_TFLOPS, 4)}
     else:
         # ~25-row chunks are far below the MFMA ridge: every chunk streams the encoder +
         # adapter weights once, so the bound is that byte stream at the HBM peak

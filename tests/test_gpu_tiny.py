@@ -128,7 +128,7 @@ def test_long_stream_multiblock_attention(tiny_weights):
 def test_alternatives_match_stream_fill_alts(models, jfk_samples):
     """--alt (voxtral.c:955-1010): candidates kept on the device per step agree with the
     reference's softmax + repeated scan applied to the oracle's logits (ids exact, probs
-    1e-5 relative), for several n_alt / cutoff settings."""
+    within what the logit bar allows), for several n_alt / cutoff settings."""
     import vox_hip
     import vox_oracle
     hm, om = models
@@ -151,7 +151,9 @@ def test_alternatives_match_stream_fill_alts(models, jfk_samples):
         for i, tok in enumerate(ht):
             rid, rpr = vox_oracle.fill_alts(ol[i], tok, n_alt, cutoff)
             assert ids[i].tolist() == rid, (i, ids[i], rid)
-            np.testing.assert_allclose(pr[i], rpr, rtol=1e-5, atol=1e-9)
+            # a logit error e moves p by a factor exp(e) (numerator) and the normaliser alike:
+            # the logit bar (LOGIT_TOL of the largest logit) bounds the probability's relative error
+            np.testing.assert_allclose(pr[i], rpr, rtol=2 * LOGIT_TOL * float(np.max(np.abs(ol[i]))), atol=1e-9)
             n_with_alts += ids[i][1] >= 0
         if n_alt > 1 and cutoff >= 0.5:
             assert n_with_alts > 0

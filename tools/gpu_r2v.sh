@@ -1,0 +1,4 @@
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/r2v_gputest.log 2>&1
+echo rc=$?

@@ -237,7 +237,7 @@ __device__ __forceinline__ void g2_load(G2Regs& r, const float* __restrict__ Ap,
 }
 
 // split A into the hi/mid/lo bf16 planes (exact), W to bf16 (Q8: exact), into one LDS buffer
-template <int WQ8>
+template <int WQ8, int NP>
 __device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int srow, int sk, float amask) {
     constexpr int PLANE = 128 * (64 + 8);
     const float4 ra[8] = {r.a0, r.a1, r.a2, r.a3, r.a4, r.a5, r.a6, r.a7};
@@ -245,19 +245,19 @@ __device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int sr
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {
         float v[8] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w, ra[i + 1].x, ra[i + 1].y, ra[i + 1].z, ra[i + 1].w};
-        uint32_t t[3][8];
+        uint32_t t[NP][8];
 #pragma unroll
         for (int e = 0; e < 8; e++) {
             float r = v[e] * amask;
 #pragma unroll
-            for (int p = 0; p < 3; p++) {
+            for (int p = 0; p < NP; p++) {
                 const uint32_t bb = f2bf(r);
                 t[p][e] = bb;
                 r = r - __uint_as_float(bb << 16);
             }
         }
 #pragma unroll
-        for (int p = 0; p < 3; p++) {
+        for (int p = 0; p < NP; p++) {
             uint4 pk;
             pk.x = t[p][0] | (t[p][1] << 16);
             pk.y = t[p][2] | (t[p][3] << 16);
@@ -266,7 +266,7 @@ __device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int sr
             *reinterpret_cast<uint4*>(base + p * PLANE + srow * 72 + sk + 4 * i) = pk;
         }
     }
-    uint16_t* wb = base + 3 * PLANE + srow * 72 + sk;
+    uint16_t* wb = base + NP * PLANE + srow * 72 + sk;
     if (WQ8) {
         const uint32_t d[8] = {rw[0].x, rw[0].y, rw[0].z, rw[0].w, rw[1].x, rw[1].y, rw[1].z, rw[1].w};
 #pragma unroll
@@ -290,7 +290,9 @@ __device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int sr
     }
 }
 
-template <int EPI, int WQ8>
+// NP = activation planes: 3 (hi + mid + lo = the exact f32 value) or 2 (hi + lo: the value
+// to ~2^-18 relative; the default, see gemm_planes and DESIGN.md section 5)
+template <int EPI, int WQ8, int NP = 3>
 __global__ __launch_bounds__(256, 2) void k_gemm2(const float* __restrict__ A, int lda,
                                                   const void* __restrict__ W, int K, int M, int N,
                                                   const float* __restrict__ wscale,
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(const float* __restrict__ A, i
     for (int st = 0; st < nst; st++) {
         if (st) __syncthreads();  // the previous stage's fragments have been read
 #if VOX_G2_DIAG != 2
-        g2_store<WQ8>(rg, g2_lds, srow, sk, amask);
+        g2_store<WQ8, NP>(rg, g2_lds, srow, sk, amask);
         if (st + 1 < nst) g2_load<WQ8>(rg, Ap, Wp, Wq, (st + 1) * G2_K);  // in flight during this stage's MFMAs
 #endif
         __syncthreads();
@@ -337,9 +339,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(const float* __restrict__ A, i
             bf16x8 bfrag[4];
 #pragma unroll
             for (int ni = 0; ni < 4; ni++)
-                bfrag[ni] = *reinterpret_cast<const bf16x8*>(base + 3 * PLANE + (wc * 64 + ni * 16 + fr) * G2_LDS + kk + fk);
+                bfrag[ni] = *reinterpret_cast<const bf16x8*>(base + NP * PLANE + (wc * 64 + ni * 16 + fr) * G2_LDS + kk + fk);
 #pragma unroll
-            for (int p = 0; p < 3; p++)
+            for (int p = 0; p < NP; p++)
 #pragma unroll
                 for (int mi = 0; mi < 4; mi++) {
                     const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(base + p * PLANE + (wr * 64 + mi * 16 + fr) * G2_LDS + kk + fk);
@@ -392,6 +394,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(const float* __restrict__ A, i
     }
 }
 constexpr size_t G2_LDS_BYTES = (size_t)4 * G2_M * G2_LDS * 2;  // 73,728 B: two blocks per CU
+// Activation planes of k_gemm2: 2 by default (hi + lo, ~2^-18 relative per activation:
+// full-size jfk logits 1.5e-5 / adapter rows 1.4e-5 of the largest magnitude against the
+// 5e-5 bar, ids identical; 20 % less GEMM time), VOX_HIP_GEMM_PLANES=3 for the exact split.
+int g_gemm_planes = 0;
+static int gemm_planes() {
+    if (!g_gemm_planes) {
+        const char* e = getenv("VOX_HIP_GEMM_PLANES");
+        g_gemm_planes = (e && atoi(e) == 3) ? 3 : 2;
+    }
+    return g_gemm_planes;
+}
 
 // ============================================================================
 // Split-K finish: sum the S partial tiles in slice order (deterministic), then the GEMM
@@ -2705,18 +2718,26 @@ static int gemm2_ksplit(int M, int N, int K, size_t ws_elems) {
     return best;
 }
 
-template <int E, int Q>
-static hipError_t gemm2_launch(dim3 grid, hipStream_t st, const float* A, int lda, const void* W, int K,
-                               int M, int N, const float* wscale, const float* bias, float* C, int ldc) {
+template <int E, int Q, int NP>
+static hipError_t gemm2_launch_np(dim3 grid, hipStream_t st, const float* A, int lda, const void* W, int K,
+                                  int M, int N, const float* wscale, const float* bias, float* C, int ldc) {
     static bool attr = false;  // opt in to > 64 KB of dynamic LDS once per instance
+    const size_t lds = (size_t)(NP + 1) * G2_M * G2_LDS * 2;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm2<E, Q>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)G2_LDS_BYTES);
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm2<E, Q, NP>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_gemm2<E, Q>), grid, dim3(256), G2_LDS_BYTES, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
+    hipLaunchKernelGGL((k_gemm2<E, Q, NP>), grid, dim3(256), lds, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
     return hipGetLastError();
+}
+
+template <int E, int Q>
+static hipError_t gemm2_launch(dim3 grid, hipStream_t st, const float* A, int lda, const void* W, int K,
+                               int M, int N, const float* wscale, const float* bias, float* C, int ldc) {
+    return gemm_planes() == 2 ? gemm2_launch_np<E, Q, 2>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc)
+                              : gemm2_launch_np<E, Q, 3>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
 }
 
 template <int EPI, int NS>

@@ -954,7 +954,19 @@ extern "C" int vox_hip_mel_read(vox_hip_mel_t* m, int global_first, int n, float
 // batched decoder's kernel: rows = up to 2 B fragments of 16, every weight byte streamed
 // once per row block) with the consumers fused (residual + bias + RMSNorm into planes,
 // SwiGLU into planes, bias into the QKV rows).  Longer chunks keep k_gemm2.
-static const int ENC_SKINNY_ROWS = 32;
+static const int ENC_SKINNY_MAX = SK_MAX_ROWS;  // buffers: up to SK_MAX_ROWS / 16 row blocks
+static int enc_skinny_rows() {
+    // chunks of up to this many rows take the skinny path (VOX_HIP_ENC_SKINNY_ROWS, <= 96).
+    // 80: the ~70-row flush chunk of a one-shot clip too (jfk encoder RTF 0.00129 -> 0.00118:
+    // five 16-row blocks re-reading each weight slice from the XCD's L2 beat a mostly empty
+    // 128-row k_gemm2 tile)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VOX_HIP_ENC_SKINNY_ROWS");
+        v = e ? std::max(0, std::min(ENC_SKINNY_MAX, atoi(e))) : 80;
+    }
+    return v;
+}
 
 static int model_enc_frag(vox_hip_model_t* m) {
     if (!m->efrag.empty()) return 0;
@@ -1004,10 +1016,11 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
         const int kmax = std::max(ED, std::max(EQ, EH));
         const size_t slab = std::max(std::max((size_t)skl_splits(ED) * NQKV, (size_t)skl_splits(EQ) * ED),
                                      std::max((size_t)skl_splits(ED) * 2 * EH, (size_t)skl_splits(EH) * ED));
-        CK(dalloc(&s->exp_, (size_t)2 * 3 * SK_ROWS * kmax));
-        CK(dalloc(&s->eslab, (size_t)2 * SK_ROWS * slab));
+        const int RB = ENC_SKINNY_MAX / SK_ROWS;
+        CK(dalloc(&s->exp_, (size_t)RB * 3 * SK_ROWS * kmax));
+        CK(dalloc(&s->eslab, (size_t)RB * SK_ROWS * slab));
         CK(dalloc(&s->eticket, (size_t)SKX_TICKETS));
-        CK(dalloc(&s->essq, (size_t)2 * SK_ROWS * (ED / 64)));
+        CK(dalloc(&s->essq, (size_t)RB * SK_ROWS * (ED / 64)));
     }
     uint16_t* xp = s->exp_;
     float* sl = s->eslab;
@@ -1015,7 +1028,8 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
         // bf16: the row kernels folded into the projections (k_sklx): 5 launches per layer.
         // Planes alternate between two buffers so that no launch overwrites its own input:
         // xa = the QKV / W1|W3 inputs (x * norm weight), xq = the wo / w2 inputs.
-        if (!s->exp2) CK(dalloc(&s->exp2, (size_t)2 * 3 * SK_ROWS * std::max(ED, std::max(EQ, EH))));
+        if (!s->exp2)
+            CK(dalloc(&s->exp2, (size_t)(ENC_SKINNY_MAX / SK_ROWS) * 3 * SK_ROWS * std::max(ED, std::max(EQ, EH))));
         uint16_t *xa = xp, *xq = s->exp2;
         SklFused f;
         f.part = sl;
@@ -1117,7 +1131,7 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
     const float scale = 1.0f / sqrtf((float)hd);
     hipStream_t st = s->st;
     if (n > ENC_SUB) return set_err("encoder pass of %d rows > %d", n, ENC_SUB);
-    if (n <= ENC_SKINNY_ROWS && enc_skinny_env() && enc_skinny_ok(c)) return run_encoder_rows_skinny(s, x, n, pos0, rope);
+    if (n <= enc_skinny_rows() && enc_skinny_env() && enc_skinny_ok(c)) return run_encoder_rows_skinny(s, x, n, pos0, rope);
     for (int l = 0; l < c.enc_layers; l++) {
         const EncLayerD& L = m->enc[l];
         float* Kc = s->ek + (size_t)l * s->ecap * EKV;

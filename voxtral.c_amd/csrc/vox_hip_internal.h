@@ -130,7 +130,7 @@ hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, 
 // Batched decode GEMMs for M <= 16 rows held as three bf16 planes xs[3][16][K] (hi/mid/lo =
 // the exact f32 rows) in MFMA fragment order; weights packed by launch_frag_pack.
 constexpr int SK_ROWS = 16;
-constexpr int SK_MAX_ROWS = 64;  // rows of one skinny launch: up to 4 row blocks of 16
+constexpr int SK_MAX_ROWS = 96;  // rows of one skinny launch: up to 6 row blocks of 16
                                  // (planes [rb][3][16][K], slabs [rb][S][16][N])
 hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hipStream_t st);
 // RMSNorm (+ ada) of nb rows into planes; S > 0: x += the S split slabs of part first

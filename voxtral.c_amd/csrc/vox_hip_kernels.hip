@@ -1736,50 +1736,59 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
                                                       float* __restrict__ x,
                                                       const float* __restrict__ part_alt,
                                                       float* __restrict__ alts) {
-    __shared__ float sv[256];
-    __shared__ int si[256];
-    __shared__ int stok, srow, sstep;
+    constexpr int XPT = 16;  // next-input elements per thread (D <= 4096)
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the step state and this thread's adapter elements of the next input do not depend on
+    // the argmax: their loads go out with the partials' (one round trip, not three)
+    const int st0 = state[0], st1 = state[1], step = state[3];
+    const int srow = st1 + 1;
+    const bool mk = adapter && srow < adapter_rows;
+    float av[XPT];
+    const float* a = adapter + (size_t)(mk ? srow : 0) * D;
+#pragma unroll
+    for (int j = 0; j < XPT; j++) av[j] = (mk && tid + 256 * j < D) ? a[tid + 256 * j] : 0.f;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        float v = pv[i];
-        int id = pi[i];
+    for (int i = tid; i < n; i += 256) {
+        const float v = pv[i];
+        const int id = pi[i];
         if (v > bv || (v == bv && id < bi)) { bv = v; bi = id; }
     }
-    sv[threadIdx.x] = bv;
-    si[threadIdx.x] = bi;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            float v = sv[threadIdx.x + s];
-            int id = si[threadIdx.x + s];
-            if (v > sv[threadIdx.x] || (v == sv[threadIdx.x] && id < si[threadIdx.x])) {
-                sv[threadIdx.x] = v;
-                si[threadIdx.x] = id;
-            }
-        }
-        __syncthreads();
+    // max value, lowest id among ties (voxtral.c argmax: strict >), by shuffles in the wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float v = __shfl_xor(bv, o, 64);
+        const int id = __shfl_xor(bi, o, 64);
+        if (v > bv || (v == bv && id < bi)) { bv = v; bi = id; }
     }
-    if (threadIdx.x == 0) {
-        int tok = si[0];
-        if (tok == 0x7fffffff) tok = 0;
-        int step = state[3];
+    if (lane == 0) {
+        sv[wave] = bv;
+        si[wave] = bi;
+    }
+    __syncthreads();
+    float best = sv[0];
+    int besti = si[0];
+#pragma unroll
+    for (int w = 1; w < 4; w++)
+        if (sv[w] > best || (sv[w] == best && si[w] < besti)) { best = sv[w]; besti = si[w]; }
+    const int tok = besti == 0x7fffffff ? 0 : besti;
+    if (tid == 0) {
         // the token log is a ring of tokens_cap entries (the host drains it every <= 16 steps)
         if (tokens) tokens[step % tokens_cap] = tok;
-        state[0] += 1;
-        state[1] += 1;
+        state[0] = st0 + 1;
+        state[1] = srow;
         state[2] = tok;
         state[3] = step + 1;
-        stok = tok;
-        sstep = step;
-        srow = state[1];
     }
-    __syncthreads();
-    if (adapter && srow < adapter_rows) {
-        const float* a = adapter + (size_t)srow * D;
-        for (int i = threadIdx.x; i < D; i += 256) x[i] = a[i] + emb_at(emb, esc, stok, D, i);
+    if (mk) {
+        // next step's input x = adapter[row] + tok_emb[token] (voxtral.c:1106-1113)
+#pragma unroll
+        for (int j = 0; j < XPT; j++)
+            if (tid + 256 * j < D) x[tid + 256 * j] = av[j] + emb_at(emb, esc, tok, D, tid + 256 * j);
     }
-    if (alts) alt_merge(part_alt, n, stok, sv[0], sstep % tokens_cap, alts);
+    if (alts) alt_merge(part_alt, n, tok, best, step % tokens_cap, alts);
 }
 
 // ============================================================================
@@ -3102,6 +3111,7 @@ hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state
                                int cap, const float* adapter, int adapter_rows,
                                const void* emb, const float* esc, int D, float* x,
                                const float* part_alt, float* alts, hipStream_t st) {
+    if (adapter && D > 16 * 256) return hipErrorInvalidValue;  // k_argmax_final: 16 next-input elements per thread
     hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, pv, pi, n, state, tokens, cap,
                        adapter, adapter_rows, emb, esc, D, x, part_alt, alts);
     LAUNCH_CHECK();

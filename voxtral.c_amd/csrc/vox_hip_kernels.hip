@@ -215,35 +215,40 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int l
 #endif
 
 // k_gemm2 staging: 32 A floats and 32 W elements per thread (row t/2, k half (t&1)*32)
-struct G2Regs {  // one stage's staging registers (named members: kept in VGPRs)
-    float4 a0, a1, a2, a3, a4, a5, a6, a7;
-    uint4 w0, w1, w2, w3;
+// AV = A float4 per thread: 8 (256 threads, 128-column tiles) or 4 (512 threads, 256-column
+// tiles); W: 32 elements per thread either way
+template <int AV>
+struct G2Regs {  // one stage's staging registers (constant-indexed arrays: kept in VGPRs)
+    float4 a[AV];
+    uint4 w[4];
 };
 
-template <int WQ8>
-__device__ __forceinline__ void g2_load(G2Regs& r, const float* __restrict__ Ap, const uint16_t* __restrict__ Wp,
+template <int WQ8, int AV>
+__device__ __forceinline__ void g2_load(G2Regs<AV>& r, const float* __restrict__ Ap, const uint16_t* __restrict__ Wp,
                                         const int8_t* __restrict__ Wq, int ko) {
     const float4* a = reinterpret_cast<const float4*>(Ap + ko);
-    r.a0 = a[0]; r.a1 = a[1]; r.a2 = a[2]; r.a3 = a[3];
-    r.a4 = a[4]; r.a5 = a[5]; r.a6 = a[6]; r.a7 = a[7];
+#pragma unroll
+    for (int i = 0; i < AV; i++) r.a[i] = a[i];
     if (WQ8) {
         const uint4* q = reinterpret_cast<const uint4*>(Wq + ko);
-        r.w0 = q[0];
-        r.w1 = q[1];
+        r.w[0] = q[0];
+        r.w[1] = q[1];
     } else {
         const uint4* w = reinterpret_cast<const uint4*>(Wp + ko);
-        r.w0 = w[0]; r.w1 = w[1]; r.w2 = w[2]; r.w3 = w[3];
+#pragma unroll
+        for (int i = 0; i < 4; i++) r.w[i] = w[i];
     }
 }
 
 // split A into the hi/mid/lo bf16 planes (exact), W to bf16 (Q8: exact), into one LDS buffer
-template <int WQ8, int NP>
-__device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int srow, int sk, float amask) {
+template <int WQ8, int NP, int AV>
+__device__ __forceinline__ void g2_store(const G2Regs<AV>& r, uint16_t* base, int srow, int sk, int wrow, int wk,
+                                         float amask) {
     constexpr int PLANE = 128 * (64 + 8);
-    const float4 ra[8] = {r.a0, r.a1, r.a2, r.a3, r.a4, r.a5, r.a6, r.a7};
-    const uint4 rw[4] = {r.w0, r.w1, r.w2, r.w3};
+    const float4* ra = r.a;
+    const uint4* rw = r.w;
 #pragma unroll
-    for (int i = 0; i < 8; i += 2) {
+    for (int i = 0; i < AV; i += 2) {
         float v[8] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w, ra[i + 1].x, ra[i + 1].y, ra[i + 1].z, ra[i + 1].w};
         uint32_t t[NP][8];
 #pragma unroll
@@ -266,7 +271,7 @@ __device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int sr
             *reinterpret_cast<uint4*>(base + p * PLANE + srow * 72 + sk + 4 * i) = pk;
         }
     }
-    uint16_t* wb = base + NP * PLANE + srow * 72 + sk;
+    uint16_t* wb = base + NP * PLANE + wrow * 72 + wk;
     if (WQ8) {
         const uint32_t d[8] = {rw[0].x, rw[0].y, rw[0].z, rw[0].w, rw[1].x, rw[1].y, rw[1].z, rw[1].w};
 #pragma unroll
@@ -292,42 +297,48 @@ __device__ __forceinline__ void g2_store(const G2Regs& r, uint16_t* base, int sr
 
 // NP = activation planes: 3 (hi + mid + lo = the exact f32 value) or 2 (hi + lo: the value
 // to ~2^-18 relative; the default, see gemm_planes and DESIGN.md section 5)
-template <int EPI, int WQ8, int NP = 3>
-__global__ __launch_bounds__(256, 2) void k_gemm2(const float* __restrict__ A, int lda,
-                                                  const void* __restrict__ W, int K, int M, int N,
-                                                  const float* __restrict__ wscale,
-                                                  const float* __restrict__ bias,
-                                                  float* __restrict__ C, int ldc) {
+// WN = waves along N: 2 (128 x 128 tile, 256 threads) or 4 (128 x 256 tile, 512 threads: each
+// A stage feeds twice the columns, so the activations are re-read from L2 half as often;
+// bf16 weights with two planes, so the stage buffer stays 73.7 KB and two blocks share a CU)
+template <int EPI, int WQ8, int NP = 3, int WN = 2>
+__global__ __launch_bounds__(128 * WN, 2) void k_gemm2(const float* __restrict__ A, int lda,
+                                                       const void* __restrict__ W, int K, int M, int N,
+                                                       const float* __restrict__ wscale,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ C, int ldc) {
     extern __shared__ __attribute__((aligned(16))) uint16_t g2_lds[];
-    // [buf][plane 0..2 = A hi/mid/lo, 3 = W][128][G2_LDS]
+    // [plane 0..NP-1 = A hi/(mid)/lo][128][G2_LDS], then W [64 WN][G2_LDS]
     constexpr int PLANE = G2_M * G2_LDS;
+    constexpr int AV = WN == 2 ? 8 : 4;   // A float4 per thread
+    constexpr int TPR = 16 / AV;          // threads per A row
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
-    const int m0 = blockIdx.y * G2_M, n0 = blockIdx.x * G2_N;
+    const int wr = wave / WN, wc = wave % WN;
+    const int m0 = blockIdx.y * G2_M, n0 = blockIdx.x * (64 * WN);
     const int Ks = K / gridDim.z, kb = blockIdx.z * Ks;
     const int nst = Ks / G2_K;
-    // staging: thread -> (row t/2, 32 consecutive k at (t&1)*32)
-    const int srow = tid >> 1, sk = (tid & 1) * 32;
+    // staging: A row t / TPR, 4 AV consecutive k; W row t / 2, 32 consecutive k at (t & 1) * 32
+    const int srow = tid / TPR, sk = (tid % TPR) * 4 * AV;
+    const int wrow = tid >> 1, wk = (tid & 1) * 32;
     const int arow = min(m0 + srow, M - 1);
     const float amask = (m0 + srow) < M ? 1.0f : 0.0f;
     const float* Ap = A + (size_t)arow * lda + kb + sk;
-    const uint16_t* Wp = static_cast<const uint16_t*>(W) + (size_t)(n0 + srow) * K + kb + sk;
-    const int8_t* Wq = static_cast<const int8_t*>(W) + (size_t)(n0 + srow) * K + kb + sk;
+    const uint16_t* Wp = static_cast<const uint16_t*>(W) + (size_t)(n0 + wrow) * K + kb + wk;
+    const int8_t* Wq = static_cast<const int8_t*>(W) + (size_t)(n0 + wrow) * K + kb + wk;
 
-    G2Regs rg;
+    G2Regs<AV> rg;
     f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    g2_load<WQ8>(rg, Ap, Wp, Wq, 0);
+    g2_load<WQ8, AV>(rg, Ap, Wp, Wq, 0);
     const int fr = lane & 15, fk = (lane >> 4) * 8;
     for (int st = 0; st < nst; st++) {
         if (st) __syncthreads();  // the previous stage's fragments have been read
 #if VOX_G2_DIAG != 2
-        g2_store<WQ8, NP>(rg, g2_lds, srow, sk, amask);
-        if (st + 1 < nst) g2_load<WQ8>(rg, Ap, Wp, Wq, (st + 1) * G2_K);  // in flight during this stage's MFMAs
+        g2_store<WQ8, NP, AV>(rg, g2_lds, srow, sk, wrow, wk, amask);
+        if (st + 1 < nst) g2_load<WQ8, AV>(rg, Ap, Wp, Wq, (st + 1) * G2_K);  // in flight during this stage's MFMAs
 #endif
         __syncthreads();
 #if VOX_G2_DIAG == 1
@@ -2713,40 +2724,61 @@ int gemm_ksplit(int M, int N, int K, size_t ws_elems) {
 // k_gemm2 split count: two 128x128 blocks per CU (LDS), so a launch of T tiles x S slices
 // runs ceil(T S / 512) rounds of K/(64 S) stages (~1.3 us each, two blocks sharing a CU);
 // a split adds the partial tiles' round trip (2 S M N 4 B at ~5 TB/s) and the reduce.
-static int gemm2_ksplit(int M, int N, int K, size_t ws_elems) {
-    const int tiles = (N / G2_N) * ((M + G2_M - 1) / G2_M);
+static int gemm2_ksplit(int M, int N, int K, size_t ws_elems, int tn = G2_N) {
+    // tn = 256 (WN = 4): half the tiles, each with twice the MFMA work per stage
+    const int tiles = (N / tn) * ((M + G2_M - 1) / G2_M);
+    const double tstage = tn == G2_N ? 1.3 : 2.6;
     int best = 1;
     double best_t = 1e30;
     for (int s = 1; s <= 32; s *= 2) {
         if (K % (s * G2_K) || (s > 1 && ((size_t)s * M * N > ws_elems || K / s < 2 * G2_K))) break;
         const double rounds = (double)((tiles * s + 511) / 512);
-        double t = rounds * (K / s / G2_K) * 1.3;
+        double t = rounds * (K / s / G2_K) * tstage;
         if (s > 1) t += 4.0 + 2.0 * s * (double)M * N * 4 / 5e6;
         if (t < best_t) { best_t = t; best = s; }
     }
     return best;
 }
 
-template <int E, int Q, int NP>
+template <int E, int Q, int NP, int WN>
 static hipError_t gemm2_launch_np(dim3 grid, hipStream_t st, const float* A, int lda, const void* W, int K,
                                   int M, int N, const float* wscale, const float* bias, float* C, int ldc) {
     static bool attr = false;  // opt in to > 64 KB of dynamic LDS once per instance
-    const size_t lds = (size_t)(NP + 1) * G2_M * G2_LDS * 2;
+    const size_t lds = ((size_t)NP * G2_M + 64 * WN) * G2_LDS * 2;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm2<E, Q, NP>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm2<E, Q, NP, WN>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_gemm2<E, Q, NP>), grid, dim3(256), lds, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
+    hipLaunchKernelGGL((k_gemm2<E, Q, NP, WN>), grid, dim3(128 * WN), lds, st, A, lda, W, K, M, N, wscale, bias, C,
+                       ldc);
     return hipGetLastError();
+}
+
+int g_gemm_wide = -1;  // tools/kbench knob: 128 x 256 tiles where they apply (-1: VOX_HIP_GEMM_WIDE, default on)
+static bool gemm_wide(int M, int N, const float* wscale) {
+    if (g_gemm_wide < 0) {
+        const char* e = getenv("VOX_HIP_GEMM_WIDE");
+        g_gemm_wide = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    if (!g_gemm_wide || wscale || gemm_planes() != 2 || N % 256) return false;
+    // wide tiles where they still fill the GPU, or where both widths need split-K anyway
+    // (tools/kbench at M = 677: W1|W3 61.9 -> 53.3, wo 27.8 -> 25.9, w2 45.6 -> 40.2 us; the
+    // QKV's 288 narrow tiles would drop to 144 wide ones: 51.4 -> 62.5, kept narrow)
+    const int mt = (M + G2_M - 1) / G2_M;
+    return (N / 256) * mt >= 192 || (N / G2_N) * mt < 128;
 }
 
 template <int E, int Q>
 static hipError_t gemm2_launch(dim3 grid, hipStream_t st, const float* A, int lda, const void* W, int K,
                                int M, int N, const float* wscale, const float* bias, float* C, int ldc) {
-    return gemm_planes() == 2 ? gemm2_launch_np<E, Q, 2>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc)
-                              : gemm2_launch_np<E, Q, 3>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
+    if (!Q && gemm_wide(M, N, wscale)) {
+        grid.x = N / 256;
+        return gemm2_launch_np<E, 0, 2, 4>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
+    }
+    return gemm_planes() == 2 ? gemm2_launch_np<E, Q, 2, 2>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc)
+                              : gemm2_launch_np<E, Q, 3, 2>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
 }
 
 template <int EPI, int NS>
@@ -2754,7 +2786,7 @@ static hipError_t gemm_t(const float* A, int lda, const void* W, const float* ws
                          int N, const float* bias, float* C, int ldc, hipStream_t st, float* ws,
                          size_t ws_elems) {
     if (NS == 3 && N % G2_N == 0 && K % G2_K == 0 && lda % 4 == 0) {
-        const int S = ws ? gemm2_ksplit(M, N, K, ws_elems) : 1;
+        const int S = ws ? gemm2_ksplit(M, N, K, ws_elems, gemm_wide(M, N, wscale) ? 256 : G2_N) : 1;
         if (S > 1) {
             dim3 grid(N / G2_N, (M + G2_M - 1) / G2_M, S);
             hipError_t e = wscale ? gemm2_launch<EPI_PARTIAL, 1>(grid, st, A, lda, W, K, M, N, wscale, nullptr, ws, N)

@@ -143,69 +143,6 @@ int main(int argc, char** argv) {
     add("q8 gemv lm   (131072x3072)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D);
     qs = nullptr;
     {
-        // A decode step's GEMV chain, 26 x (qkv, wo, w13, w2): one stream (kernel-boundary
-        // barriers) against two streams whose neighbouring launches overlap, each block
-        // issuing its first weight loads before it waits for its predecessor's arrivals
-        // (GemvArgs::chain).  Per layer.
-        unsigned* chain;
-        CK(hipMalloc(&chain, 64));
-        CK(hipMemset(chain, 0, 64));
-        hipStream_t st2;
-        CK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
-        hipEvent_t join;
-        CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-        unsigned total = 0;
-        auto pass = [&](int mode, int q8) {
-            // mode 0: one stream; 1: one stream, chain protocol; 2: two streams chained
-            const float* qsv = q8 ? wsc : nullptr;
-            int k = 0;
-            for (int l = 0; l < NL; l++) {
-                struct Op { int pro, epi, K, rows; const uint16_t* W; };
-                const Op ops[4] = {{PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, wqkv[l]}, {PRO_NONE, EPI_RESID, DQ, D, wo[l]},
-                                   {PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, w13[l]}, {PRO_NONE, EPI_RESID, DH, D, w2[l]}};
-                for (const Op& o : ops) {
-                    GemvArgs a;
-                    memset(&a, 0, sizeof a);
-                    a.x = x; a.K = o.K; a.W = o.W; a.wscale = qsv; a.rows = o.rows; a.norm_w = normw; a.ada = ada;
-                    a.eps = 1e-5f; a.y = y; a.qd = DQ; a.kvd = DKV; a.hd = HD; a.rope = rope; a.state = state;
-                    a.Kc = Kc; a.Vc = Vc; a.cap = cap;
-                    if (mode) {
-                        a.chain = chain;
-                        a.chain_wait = total;
-                        a.chain_flags = CHAIN_WAIT | CHAIN_SIGNAL;
-                        total += gemv_grid(o.rows);
-                    }
-                    CK(launch_gemv(o.pro, o.epi, a, (mode == 2 && (k & 1)) ? st2 : st));
-                    k++;
-                }
-            }
-            if (mode == 2) {
-                CK(hipEventRecord(join, st2));
-                CK(hipStreamWaitEvent(st, join, 0));
-            }
-        };
-        for (int q8 : {0, 1}) {
-            for (int mb : {1024, 512}) {
-                g_gemv_max_blocks = mb;
-                for (int mode : {0, 1, 2}) {
-                    if (mode == 2 && mb > 512) continue;  // co-residency of two neighbours needs <= 2 blocks per CU
-                    const double us = timeit([&] { pass(mode, q8); }, iters / 10 + 1, st) / NL;
-                    char nm[96];
-                    snprintf(nm, sizeof nm, "chain %s grid<=%d %s", q8 ? "q8" : "bf16", mb,
-                             mode == 0 ? "one stream" : mode == 1 ? "one stream + protocol" : "two streams chained");
-                    const double lb = (DQ + 2.0 * DKV) * D + (double)D * DQ + 2.0 * DH * D + (double)D * DH;
-                    add(nm, us, lb * (q8 ? 1 : 2));
-                }
-            }
-        }
-        g_gemv_max_blocks = GEMV_MAX_BLOCKS;
-        unsigned hc[CHAIN_SHARDS + 1];
-        CK(hipMemcpy(hc, chain, sizeof hc, hipMemcpyDeviceToHost));
-        unsigned sum = 0;
-        for (int i = 0; i < CHAIN_SHARDS; i++) sum += hc[i];
-        printf("chain arrivals %u (expected %u), timeout flag %u\n", sum, total, hc[CHAIN_SHARDS]);
-    }
-    {
         // M>1 GEMMs of the encoder / prefill (useful TFLOP/s = 2 M N K / t)
         float* ws = (float*)dmalloc((size_t)8 << 22, 0);
         float* Am = (float*)dmalloc((size_t)1024 * 9216 * 4, 1);

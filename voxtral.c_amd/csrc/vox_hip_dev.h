@@ -163,36 +163,4 @@ __device__ __forceinline__ float dot16q(uint4 w, const float4 (&x)[4], float acc
     return acc;
 }
 
-// Chained launches (GemvArgs::chain): a consumer block waits for the producers' arrivals and
-// acquires their outputs (agent scope: L1 and this XCD's L2 invalidated, so the plain loads
-// that follow see the other XCDs' stores); a producer block drains its stores, releases them
-// (its XCD's dirty L2 lines written back) and arrives on its shard.  The wait is bounded: past
-// ~0.1 s it raises the timeout flag (and every later wait of the chain gives up at once) (chain[CHAIN_SHARDS]) and goes on, so a launch-order
-// surprise costs a wrong step that the host reports, never a hung GPU.
-__device__ __forceinline__ void chain_wait(unsigned* c, unsigned target) {
-    if (threadIdx.x == 0) {
-        for (unsigned it = 0;; it++) {
-            unsigned s = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) s += __hip_atomic_load(c + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((int)(s - target) >= 0) break;
-            if (it > (1u << 16) || __hip_atomic_load(c + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                __hip_atomic_fetch_or(c + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-}
-__device__ __forceinline__ void chain_signal(unsigned* c) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(c + (blockIdx.x & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 }  // namespace vox

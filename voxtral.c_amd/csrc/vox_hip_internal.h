@@ -38,17 +38,7 @@ struct GemvArgs {
     float* part_val;
     int* part_idx;
     float* part_alt;       // EPI_LOGITS_ALT: [blocks][ALT_PART]
-    // Chained launch (two HIP streams, no kernel-boundary barrier between neighbours): the
-    // block issues its first weight loads, then waits until the chain's arrival count
-    // (CHAIN_SHARDS counters, summed) reaches chain_wait, and bumps its shard once its
-    // outputs are released.  chain == null: an ordinary launch.
-    unsigned* chain;
-    unsigned chain_wait;
-    int chain_flags;       // CHAIN_WAIT | CHAIN_SIGNAL
 };
-constexpr int CHAIN_SHARDS = 8;        // arrival counters (one per XCD); [CHAIN_SHARDS] = timeout flag
-enum { CHAIN_WAIT = 1, CHAIN_SIGNAL = 2 };
-extern int g_gemv_max_blocks;          // grid cap (chained launches: 2 blocks per CU)
 
 constexpr int VOX_MAX_BATCH = 16;    // streams per batched decode step
 // per-stream operands of one decode-attention launch (blockIdx.z = stream of a batch)

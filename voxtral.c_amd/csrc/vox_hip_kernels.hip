@@ -983,9 +983,6 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 #pragma unroll
         for (int i = 0; i < RB; i++) wsc[i] = a.wscale[rows[i]];
     }
-    // chained launch: x (and the residual, state) come from the previous kernel, which may
-    // still be running; the first group's weight loads are already in flight
-    if (a.chain && (a.chain_flags & CHAIN_WAIT)) chain_wait(a.chain, a.chain_wait);
 
     float4 xr[KQ][XPC];
     float ss = 0.f;
@@ -1187,7 +1184,6 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             }
         }
     }
-    if (a.chain && (a.chain_flags & CHAIN_SIGNAL)) chain_signal(a.chain);
 }
 
 // ============================================================================
@@ -2936,15 +2932,14 @@ static int gemv_rb(int rows) {
     return 2;
 }
 
-int g_gemv_max_blocks = GEMV_MAX_BLOCKS;
 int gemv_grid(int rows) {
-    // the largest divisor of the group count that fits 4 blocks per CU (2 for chained
-    // launches): every block then runs the same number of groups (no tail)
-    const int ng = rows / gemv_rb(rows), mb = g_gemv_max_blocks;
+    // the largest divisor of the group count that fits 4 blocks per CU: every block then
+    // runs the same number of groups (no tail)
+    const int ng = rows / gemv_rb(rows);
     int best = 1;
-    for (int gsz = 1; gsz <= mb && gsz <= ng; gsz++)
+    for (int gsz = 1; gsz <= GEMV_MAX_BLOCKS && gsz <= ng; gsz++)
         if (ng % gsz == 0) best = gsz;
-    if (best < mb / 4 && ng > mb) best = mb;  // no good divisor: accept a tail
+    if (best < 256 && ng > GEMV_MAX_BLOCKS) best = GEMV_MAX_BLOCKS;  // no good divisor: accept a tail
     return best;
 }
 

@@ -1446,11 +1446,20 @@ static int run_steps(vox_hip_stream_t* s, int n, int pos0) {
     const vox_hip_config_t& c = s->m->c;
     const int gi = graph_index(s, std::min(pos0 + n, c.dec_window));
     const int splits = graph_splits(s, gi);
+    if (s->profiling && use_graphs() && n > 1) {
+        // profiled batch: the first n - 1 steps replay the graph, the last one (whose W1|W3
+        // events collect_graph_profile reads) runs eagerly below
+        s->profiling = 0;
+        const int rc = run_steps(s, n - 1, pos0);
+        s->profiling = 1;
+        if (rc) return -1;
+        pos0 += n - 1;
+        n = 1;
+    }
     if (!use_graphs() || s->profiling) {
         // eager launches of the same device-state kernels: profiling (the W1|W3 launches
         // carry dispatch-recorded HIP events, which a graph cannot hold), profilers that
-        // cannot follow graph replays (VOX_HIP_GRAPH=0).  Measured as fast as the graph
-        // replay on MI355X (kernels are long enough for the host to stay ahead).
+        // cannot follow graph replays (VOX_HIP_GRAPH=0).
         if (s->profiling && s->pev.empty()) {
             s->pev.resize(2 * c.dec_layers);
             for (auto& e : s->pev) CK(hipEventCreate(&e));

@@ -64,6 +64,8 @@ def parse():
                          "of this length (one-shot feed through the device mel, flush, finish)")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: placeholder host step, same launcher and JSON")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1,
+                    help="(tests) with --dry-run, this rank exits with an error before the first barrier")
     return ap.parse_args()
 
 
@@ -85,11 +87,37 @@ def launch_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    # poll every rank: the first one that fails takes its siblings down (they would
+    # otherwise wait in a barrier for the dead rank until the process-group timeout)
     rc = 0
-    for p in procs:
-        p.wait()
-        rc = rc or p.returncode
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                print(f"bench.py: rank {procs.index(p)} exited with {r}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 10
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+                break
+        if live:
+            time.sleep(0.05)
     return rc
+
+
+GLOO_TIMEOUT_S = 600   # a rank lost mid-run ends the job within this bound, not torch's default
 
 
 class Dist:
@@ -101,10 +129,12 @@ class Dist:
             raise SystemExit(f"bench.py: WORLD_SIZE={self.world} but --gpus {n}")
         self.torch = None
         if self.world > 1:
+            import datetime
+
             import torch
             import torch.distributed as dist
             self.torch, self.dist = torch, dist
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=GLOO_TIMEOUT_S))
 
     def barrier(self):
         if self.torch is not None:
@@ -375,6 +405,8 @@ def dry_run(args, d):
     """The launcher / reduction path without a GPU: every rank times `steps` placeholder
     host steps (a small numpy matmul standing in for a transcription) between the same
     barriers and reports the same aggregate fields.  Not a measurement of the engine."""
+    if d.rank == args.dry_run_fail_rank:
+        sys.exit(f"bench.py: rank {d.rank} failing on purpose (--dry-run-fail-rank)")
     a = np.random.default_rng(d.rank).standard_normal((256, 256)).astype(np.float32)
     for _ in range(args.warmup):
         a @ a

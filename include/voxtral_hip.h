@@ -176,6 +176,10 @@ vox_hip_batch_t *vox_hip_batch_create(vox_hip_model_t *m, int max_streams);
 void vox_hip_batch_free(vox_hip_batch_t *b);
 int vox_hip_batch_decode(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, int max_steps,
                          int stop_at_eos, int *tokens_out, int *counts_out);
+/* Logits [vocab] of the last batched step, for a stream that step advanced (the logits the
+ * reference's vox_decoder_forward returns, voxtral_decoder.c:762-779; for tests and --alt
+ * style callers).  Returns 0, or <0 if s was not in that step. */
+int vox_hip_batch_read_logits(vox_hip_batch_t *b, vox_hip_stream_t *s, float *out);
 /* Decoder state snapshot: [0]=kv logical length, [1]=next adapter row, [2]=prev token,
  * [3]=started, [4]=eos_seen, [5]=tokens generated. */
 int vox_hip_stream_state(vox_hip_stream_t *s, int *out6);

@@ -66,6 +66,24 @@ def test_bench_launcher_dry_run_world2():
     assert o["value"] == pytest.approx(2 * 4 * 8 / (o["ms_per_step"] * 4 / 1000.0), rel=0.02)
 
 
+def test_bench_launcher_fails_fast_when_a_rank_dies():
+    """A rank that exits with an error takes the job down at once: the launcher polls its
+    children and stops the sibling waiting in the barrier (instead of leaving it there until
+    the process-group timeout), and returns the failing rank's status."""
+    import time
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "2",
+                        "--warmup", "1", "--dry-run", "--dry-run-fail-rank", "1"],
+                       capture_output=True, text=True, timeout=200, env=env)
+    assert r.returncode != 0
+    assert "rank 1 exited" in r.stderr, r.stderr[-2000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert time.time() - t0 < 120
+
+
 def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],

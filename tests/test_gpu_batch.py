@@ -7,6 +7,12 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+LOGIT_TOL = 5e-5   # of the largest logit magnitude, as the single-stream bar
+
+
+def rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1e-6, float(np.max(np.abs(b)))))
+
 
 def _mels(cfg, sizes, seed):
     rng = np.random.default_rng(seed)
@@ -57,6 +63,42 @@ def test_batch_matches_single_and_oracle(models, tiny_cfg, nstreams):
     b.close()
 
 
+def test_batch_logits_per_step_vs_oracle(models, tiny_cfg):
+    """The batched path's logit bar: 3 TINY streams advanced one batched step per call; every
+    step's logits (after the first token, which each stream takes on its own prefill path)
+    within LOGIT_TOL of the oracle's, ids identical."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    mels = _mels(tiny_cfg, [480, 560, 640], 31)
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 3)
+    n = 40
+    got = [[] for _ in ss]
+    lg = [[] for _ in ss]
+    for step in range(n):
+        for i, t in enumerate(b.decode(ss, max_steps=1, stop_at_eos=False)):
+            got[i] += t.tolist()
+            if step:
+                lg[i].append(b.read_logits(ss[i]))
+    worst = 0.0
+    for i, mel in enumerate(mels):
+        o = vox_oracle.OracleStream(om)
+        o.encode_mel(mel)
+        t, ol = o.decode(max_steps=n, stop_at_eos=False, want_logits=True)
+        o.close()
+        assert got[i] == t.tolist(), i
+        r = rel(np.stack(lg[i]), ol[1:])
+        worst = max(worst, r)
+        assert r < LOGIT_TOL, (i, r)
+    print(f"batched logits vs oracle: worst rel err {worst:.2e}")
+    for s in ss:
+        s.close()
+    b.close()
+
+
 def test_batch_mixed_positions_and_continuation(models, tiny_cfg):
     """streams at different decode positions (one advanced alone first), decoding resumed
     in several batch calls and finished on the single-stream path."""
@@ -100,11 +142,16 @@ def _oracle_tokens_parallel(om, mels, chunks):
         first.append(st.decode(max_steps=1, stop_at_eos=False).tolist())
         sts.append(st)
     vox_oracle.set_threads(1)
+
+    def rest_of(st):
+        a = st.decode(max_steps=st.adapter_tokens - 38 - 2, stop_at_eos=False).tolist()
+        b, lg = st.decode(stop_at_eos=False, want_logits=True)
+        return a + b.tolist(), lg[-1]
     with ThreadPoolExecutor(len(sts)) as ex:
-        rest = list(ex.map(lambda st: st.decode(stop_at_eos=False).tolist(), sts))
+        rest = list(ex.map(rest_of, sts))
     for st in sts:
         st.close()
-    return [f + r for f, r in zip(first, rest)]
+    return [f + r[0] for f, r in zip(first, rest)], [r[1] for r in rest]
 
 
 @pytest.mark.slow
@@ -127,16 +174,22 @@ def test_batch_full_size_8_streams_each_vs_oracle():
             off += n
     b = vox_hip.Batch(hm, 8)
     got = [g.tolist() for g in b.decode(ss, max_steps=1000, stop_at_eos=False)]
+    last = [b.read_logits(s) for s in ss]   # the final batched step (all 8 streams in it)
     for s in ss:
         s.close()
     b.close()
     hm.close()
     om = vox_oracle.OracleModel(VOXTRAL_4B, w)
-    refs = _oracle_tokens_parallel(om, mels, chunks)
+    refs, ref_last = _oracle_tokens_parallel(om, mels, chunks)
     om.close()
+    worst = 0.0
     for i in range(8):
         assert len(refs[i]) == 149
         assert got[i] == refs[i], (i, next(k for k in range(149) if got[i][k] != refs[i][k]))
+        r = rel(last[i], ref_last[i])
+        worst = max(worst, r)
+        assert r < LOGIT_TOL, (i, r)
+    print(f"8 full-size streams: ids equal, last-step logits worst rel err {worst:.2e}")
     assert len({tuple(r) for r in refs}) > 1   # the streams really differ
 
 

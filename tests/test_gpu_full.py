@@ -100,6 +100,49 @@ def test_full_long_clip_one_shot(full):
     os_.close()
 
 
+def test_full_streaming_decode_vs_oracle(full):
+    """C3's decode at full size: 24 s of audio fed in -I 0.5 pieces (main.c file mode), the
+    decoder drained after every piece (stream_run_decoder, voxtral.c:1013-1145) on both
+    sides; over 200 greedy steps interleaved with ~50 encoder chunks, every id identical and
+    every step's logits within TOL of the oracle's."""
+    import vox_hip
+    import vox_oracle
+    cfg, hm, om = full
+    audio = synth_audio(24.0, 13)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    ha = vox_hip.AudioSession(hs, interval_s=0.5)
+    oa = vox_oracle.OracleAudioSession(os_, interval_s=0.5)
+    hl, ol, ot = [], [], []
+
+    def hdec(stop_at_eos=True):
+        t, lg = hs.decode(stop_at_eos=False, want_logits=True)
+        ha.tokens += t.tolist()
+        hl.append(lg)
+
+    def odec():
+        t, lg = os_.decode(stop_at_eos=False, want_logits=True)
+        ot.extend(t.tolist())
+        ol.append(lg)
+    ha._run_decoder = hdec
+    oa._dec = odec
+    for i in range(0, len(audio), 8000):
+        ha.feed_samples(audio[i:i + 8000])
+        oa.feed(audio[i:i + 8000])
+    ha.finish_samples()
+    oa.finish()
+    assert len(ha.chunks) > 40
+    assert len(ot) > 200, len(ot)
+    assert ha.tokens == ot
+    hl, ol = np.concatenate(hl), np.concatenate(ol)
+    rl = rel(hl, ol)
+    print(f"24 s -I 0.5 full decode: {len(ha.chunks)} chunks, {len(ot)} ids equal, logits rel err {rl:.2e}")
+    assert rl < TOL, rl
+    ha.close()
+    oa.close()
+    hs.close()
+    os_.close()
+
+
 def test_full_streaming_60s_encoder(full):
     """C3 scale: 60 s of audio fed in -I 0.5 pieces (main.c file mode) through the device
     log-mel and the chunked encoder (~25-row chunks over the rolling 750-row window, KV ring

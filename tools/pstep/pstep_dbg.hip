@@ -9,7 +9,7 @@
 #include <vector>
 #include <algorithm>
 
-#include "../voxtral.c_amd/csrc/vox_hip_internal.h"
+#include "vox_hip_pstep.h"
 
 using namespace vox;
 namespace vox { extern int g_pstep_d; }

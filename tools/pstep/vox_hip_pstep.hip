@@ -38,8 +38,8 @@
 // faster than new loads go out.  59 us per layer against 53 for the per-operation graph.  An
 // LDS-DMA loader / consumer split (loaders issue, consumers only read LDS) streamed at only
 // 3.7-4.1 TB/s here.
-#include "vox_hip_internal.h"
-#include "vox_hip_dev.h"
+#include "vox_hip_pstep.h"
+#include "../../voxtral.c_amd/csrc/vox_hip_dev.h"
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>

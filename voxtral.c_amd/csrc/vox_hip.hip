@@ -486,12 +486,6 @@ struct vox_hip_stream {
     int graph_rope_gen;      // model rope table generation the step graphs were captured with
     int *pidx, *state, *tokens;   // tokens: ring of tokens_cap ids, index = step % tokens_cap
     int* twin_state;              // decoder_full_step's argmax state (the graph state stays untouched)
-    // persistent decode step (vox_hip_pstep.hip): layer table, hand-off granules, control words
-    PLayer* ptab;
-    uint2* pgran;
-    int* pctl;
-    int pgrid;                    // workgroups (= CUs); 0: the per-operation step only
-    int prof_kind;                // what the profiled events bracket: 0 W1|W3 GEMV, 1 persistent step
     int dec_rows_cap, tokens_cap;
     hipGraphExec_t step_exec[STEP_GRAPHS];  // [g]: attention with 2^g key splits (g = 0: no combine)
     int graph_ready;              // bit mask of built graphs
@@ -559,71 +553,6 @@ static int stream_alloc_dec_rows(vox_hip_stream_t* s, int rows) {
 
 extern "C" void vox_hip_stream_free(vox_hip_stream_t* s);
 
-// Persistent step (vox_hip_pstep.hip): opt-in with VOX_HIP_PSTEP=1 while it is slower than
-// the per-operation graph, used when the shapes fit the kernel.  One
-// workgroup per CU (its register use admits one), all co-resident: grid = CU count.
-static int pstep_env() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("VOX_HIP_PSTEP");
-        v = (e && atoi(e) != 0) ? 1 : 0;  // opt-in while it is slower than the per-operation graph
-    }
-    return v;
-}
-
-static int pstep_setup(vox_hip_stream_t* s) {
-    vox_hip_model_t* m = s->m;
-    const vox_hip_config_t& c = m->c;
-    s->pgrid = 0;
-    if (!pstep_env()) return 0;
-    int dev = 0, cus = 0;
-    CK(hipGetDevice(&dev));
-    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
-    if (!pstep_ok(c.dec_dim, c.dec_heads, c.dec_kv_heads, c.dec_head_dim, c.dec_hidden, cus) || c.dec_layers > 64) return 0;
-    for (int l = 0; l < c.dec_layers; l++)
-        if (m->dec[l].sqkv) return 0;  // bf16 weights only (Q8: the per-operation step)
-    std::vector<PLayer> t(c.dec_layers);
-    for (int l = 0; l < c.dec_layers; l++) {
-        const DecLayerD& L = m->dec[l];
-        t[l].w[0] = L.wqkv; t[l].w[1] = L.wo; t[l].w[2] = L.w13; t[l].w[3] = L.w2;
-        t[l].attn_norm = L.attn_norm;
-        t[l].ffn_norm = L.ffn_norm;
-        t[l].ada = m->ada_scale + (size_t)l * c.dec_dim;
-        t[l].Kc = s->dk + (size_t)l * s->dcap * DKV;
-        t[l].Vc = s->dv + (size_t)l * s->dcap * DKV;
-    }
-    CK(dalloc(reinterpret_cast<uint8_t**>(&s->ptab), sizeof(PLayer) * c.dec_layers));
-    CK(h2d(s->ptab, t.data(), sizeof(PLayer) * c.dec_layers));
-    CK(dalloc(&s->pgran, (size_t)(DQ + 2 * DKV) + DQ + c.dec_dim + c.dec_hidden));
-    CK(dalloc(&s->pctl, 4));
-    s->pgrid = cus;
-    return 0;
-}
-
-static PStepArgs pstep_args(vox_hip_stream_t* s) {
-    vox_hip_model_t* m = s->m;
-    const vox_hip_config_t& c = m->c;
-    const int DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
-    PStepArgs a;
-    memset(&a, 0, sizeof a);
-    a.layers = s->ptab;
-    a.nl = c.dec_layers;
-    a.D = c.dec_dim; a.H = c.dec_heads; a.KVH = c.dec_kv_heads; a.DH = c.dec_hidden;
-    a.cap = s->dcap; a.window = c.dec_window;
-    a.eps = c.dec_eps;
-    a.scale = 1.0f / sqrtf((float)c.dec_head_dim);
-    a.state = s->state;
-    a.rope = m->rope_dec;
-    a.x = s->xd;
-    a.gq = s->pgran;
-    a.ga = a.gq + DQ + 2 * DKV;
-    a.gx = a.ga + DQ;
-    a.gg = a.gx + c.dec_dim;
-    a.ctl = s->pctl;
-    return a;
-}
-
 extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     static std::atomic<unsigned long long> next_uid{1};
     vox_hip_stream_t* s = new vox_hip_stream_t();
@@ -668,7 +597,6 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     s->alt_cutoff = 0.f;
     TRYH(hipEventCreate(&s->evt[0]));
     TRYH(hipEventCreate(&s->evt[1]));
-    if (pstep_setup(s)) return fail();
 #undef TRYH
     if (stream_alloc_frames(s, 2048) || stream_alloc_adapter(s, 1024) || stream_alloc_dec_rows(s, 64))
         return fail();
@@ -688,7 +616,6 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
     dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2);
-    dfree(s->ptab); dfree(s->pgran); dfree(s->pctl);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
     for (hipEvent_t e : s->pev) hipEventDestroy(e);
@@ -1289,18 +1216,6 @@ static int enqueue_lm_head(vox_hip_stream_t* s, const int* state);
 static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row,
                                int splits) {
     vox_hip_model_t* m = s->m;
-    if (state && splits == 1 && s->pgrid) {
-        // every layer in one persistent launch (contexts of <= pstep_max_keys() keys)
-        const PStepArgs a = pstep_args(s);
-        const bool gprof = s->profiling && !s->capturing && s->pev.size() >= 2;
-        if (gprof) {
-            CK(launch_pstep_timed(a, s->pgrid, s->pev[0], s->pev[1], s->st));
-            s->prof_kind = 1;
-        } else {
-            CK(launch_pstep(a, s->pgrid, s->st));
-        }
-        return enqueue_lm_head(s, state);
-    }
     const vox_hip_config_t& c = m->c;
     const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
     const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
@@ -1333,7 +1248,6 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
         // profiling: HIP events recorded by the W1|W3 launch's own dispatch (eager steps)
         const bool gprof = s->profiling && state && !s->capturing && (int)s->pev.size() == 2 * c.dec_layers;
-        if (gprof) s->prof_kind = 0;
         if (gprof) CK(launch_gemv_timed(PRO_NORM_ADA, EPI_SWIGLU, a, s->pev[2 * l], s->pev[2 * l + 1], st));
         else CK(launch_gemv(PRO_NORM_ADA, EPI_SWIGLU, a, st));
         // W2 + residual (decoder.c:758-760)
@@ -1409,18 +1323,6 @@ static int build_step_graph(vox_hip_stream_t* s, int gi) {
 static int collect_graph_profile(vox_hip_stream_t* s) {
     if (!s->profiling || !s->graph_prof) return 0;
     const vox_hip_config_t& c = s->m->c;
-    if (s->prof_kind == 1) {
-        // the persistent step: every decoder layer's weights (+ the K/V rows its attention read)
-        float ms = 0.f;
-        CK(hipEventElapsedTime(&ms, s->pev[0], s->pev[1]));
-        const double D = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
-        const double layer = 2.0 * ((DQ + 2 * DKV) * D + D * DQ + 2.0 * c.dec_hidden * D + D * c.dec_hidden);
-        const int keys = std::min(s->h_state[0] + 1, c.dec_window);  // context of the sampled step (approx.)
-        s->prof_ms += ms;
-        s->prof_bytes += c.dec_layers * (layer + 2.0 * DKV * 4 * keys);
-        s->prof_launches++;
-        return 0;
-    }
     for (int l = 0; l < c.dec_layers; l++) {
         float ms = 0.f;
         CK(hipEventElapsedTime(&ms, s->pev[2 * l], s->pev[2 * l + 1]));
@@ -1638,7 +1540,7 @@ extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
     out8[1] = s->prof_bytes;
     out8[2] = (double)s->prof_launches;
     out8[3] = s->prof_launches ? s->prof_ms / s->prof_launches : 0.0;
-    out8[4] = s->prof_kind;
+    out8[4] = 0;  // what the events bracket: the W1|W3 GEMV of every layer
     out8[5] = s->prof_launches ? s->prof_bytes / s->prof_launches : 0.0;
     out8[6] = out8[7] = 0.0;
     return 0;
@@ -1987,6 +1889,9 @@ struct vox_hip_batch {
     const float* gadapter[VOX_MAX_BATCH];
     int gadapter_cap[VOX_MAX_BATCH];
     const float* grope;
+    // rows of the last batched step (b->logits row i = stream luid[i])
+    unsigned long long luid[VOX_MAX_BATCH];
+    int lnb;
 };
 
 // pack one [N, K] matrix (bf16, or int8 when q8) into fragment order (k_frag_pack)
@@ -2237,6 +2142,8 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
                                  b->st));
         if (batch_run(b, act.data(), nb, splits, steps)) return -1;
         CK(hipStreamSynchronize(b->st));
+        b->lnb = nb;
+        for (int i = 0; i < nb; i++) b->luid[i] = act[i]->uid;
         for (int i = 0; i < nb; i++) {
             vox_hip_stream_t* s = act[i];
             tok.resize(steps);
@@ -2254,4 +2161,16 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
         }
     }
     return total;
+}
+
+extern "C" int vox_hip_batch_read_logits(vox_hip_batch_t* b, vox_hip_stream_t* s, float* out) {
+    if (!b || !s || !out) return set_err("batch_read_logits: null argument");
+    const int V = b->m->c.vocab;
+    for (int i = 0; i < b->lnb; i++)
+        if (b->luid[i] == s->uid) {
+            CK(hipMemcpyAsync(out, b->logits + (size_t)i * V, (size_t)V * 4, hipMemcpyDeviceToHost, b->st));
+            CK(hipStreamSynchronize(b->st));
+            return 0;
+        }
+    return set_err("batch_read_logits: the stream was not advanced by the last batched step");
 }

@@ -39,7 +39,7 @@ EXPORTS = [
     "vox_hip_model_ada_scale", "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
-    "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode",
+    "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode", "vox_hip_batch_read_logits",
     "vox_hip_stream_state", "vox_hip_stream_set_alt", "vox_hip_stream_read_alts", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
@@ -79,6 +79,7 @@ def lib():
         "vox_hip_stream_state": (I, [P, ip]),
         "vox_hip_batch_create": (P, [P, I]), "vox_hip_batch_free": (None, [P]),
         "vox_hip_batch_decode": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, I, I, ip, ip]),
+        "vox_hip_batch_read_logits": (I, [P, P, fp]),
         "vox_hip_stream_set_alt": (I, [P, I, F]),
         "vox_hip_stream_read_alts": (I, [P, I, I, ip, fp]),
         "vox_hip_sgemm_bf16": (None, [I, I, I, fp, P, fp]),
@@ -272,7 +273,7 @@ class Stream:
     def profile(self):
         o = (ctypes.c_double * 8)()
         lib().vox_hip_stream_profile(self.h, o)
-        # kind 0: the W1|W3 GEMV of every layer; 1: the persistent step (all layers)
+        # kind 0: the events bracket the W1|W3 GEMV of every layer
         return {"ms": o[0], "bytes": o[1], "launches": int(o[2]), "avg_ms": o[3], "kind": int(o[4]),
                 "bytes_per_launch": o[5]}
 
@@ -473,6 +474,13 @@ class Batch:
         if r < 0:
             _err("vox_hip_batch_decode")
         return [toks[i, :cnt[i]].copy() for i in range(n)]
+
+    def read_logits(self, stream: "Stream") -> np.ndarray:
+        """logits of the last batched step for a stream that step advanced"""
+        out = np.empty(stream.cfg.vocab, np.float32)
+        if lib().vox_hip_batch_read_logits(self.h, stream.h, fptr(out)) != 0:
+            _err("vox_hip_batch_read_logits")
+        return out
 
     def close(self):
         if self.h:

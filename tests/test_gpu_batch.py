@@ -70,7 +70,7 @@ def test_batch_logits_per_step_vs_oracle(models, tiny_cfg):
     import vox_hip
     import vox_oracle
     hm, om = models
-    mels = _mels(tiny_cfg, [480, 560, 640], 31)
+    mels = _mels(tiny_cfg, [800, 900, 1000], 31)   # 62+ steps of adapter rows each
     ss = [vox_hip.Stream(hm) for _ in mels]
     for s, mel in zip(ss, mels):
         s.encode_mel(mel)

@@ -62,6 +62,11 @@ def parse():
     ap.add_argument("--clip-seconds", type=float, default=0.0,
                     help="config 2's long clips (e.g. 59.75): one vox_transcribe_audio pass over synthetic audio "
                          "of this length (one-shot feed through the device mel, flush, finish)")
+    ap.add_argument("--stagger", action="store_true",
+                    help="config 4 as a server: --streams S streams on the C host's per-GPU scheduler "
+                         "(vh_sched_*), fed -I 0.5 pieces of the 7 sample lengths cycled, staggered starts")
+    ap.add_argument("--serve-seconds", type=float, default=120.0,
+                    help="--stagger: audio each stream serves (clips back to back)")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: placeholder host step, same launcher and JSON")
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1,
@@ -297,6 +302,8 @@ def main():
     rng = np.random.default_rng(1234 + d.rank)
     mel = rng.uniform(-0.6, 1.4, size=(sum(JFK_CHUNKS), cfg.mel_bins)).astype(np.float32)
     mel_dev = vox_hip.DeviceArray(mel)
+    if args.stagger:
+        return bench_serve(args, d, cfg, model, st)
     if args.streams > 1:
         return bench_streams(args, d, cfg, model, st, mel, mel_dev, rng)
     if args.streaming or args.clip_seconds > 0:
@@ -560,6 +567,119 @@ def bench_streaming(args, d, cfg, model, st):
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     st.close()
+    model.close()
+
+
+# the reference's 7 WAV samples (samples/jfk.wav, test_speech.wav, benchmark/night1968/*):
+# their lengths in seconds; the served audio is synthetic of these lengths
+SAMPLE_SECONDS = [11.0, 3.64175, 5.0000625, 15.0000625, 45.0000625, 59.7494375, 88.8899375]
+
+
+def bench_serve(args, d, cfg, model, st0):
+    """config 4 as a serving loop (BASELINE.json configs[3]; SURVEY.md 8d: "the 7 WAVs
+    cycled, 8 per GPU, staggered starts"): S concurrent streams on this GPU, owned by the C
+    host's scheduler (vh_sched_*, include/vox_hip_host.h).  Stream i starts 1 s (two ticks)
+    after stream i-1 and transcribes the 7 sample lengths in turn from clip i on, a fresh
+    vh_stream per clip, until it has served --serve-seconds of audio.  One tick = every live
+    stream feeds its next 0.5 s piece (vox_stream_feed: device mel + encoder chunk; -I 0.5),
+    or flush + finish after its clip's last piece, then one vh_sched_run (prefills + batched
+    greedy steps for every stream with adapter rows).  Ticks run back to back (as fast as the
+    GPU goes).  Reported: aggregate ids/s over the whole loop, the tick latency (a piece's
+    wait for its ids) p50 / p99, and audio served per wall second."""
+    import vox_hip
+    st0.close()
+    S, piece = args.streams, 8000
+    ctx = vox_hip.HostCtx(model)
+    q = vox_hip.Scheduler(ctx, S)
+    rng = np.random.default_rng(5 + d.rank)
+    clips = [synth_audio(sec, 500 + k) for k, sec in enumerate(SAMPLE_SECONDS)]
+
+    def run(serve_s):
+        served = [0.0] * S
+        cur = [None] * S        # [HostStream, clip index, next sample, finished]
+        nxt = list(range(S))
+        ids, lat, clips_done, tick = 0, [], 0, 0
+        t_all = time.perf_counter()
+        while True:
+            live = False
+            t0 = time.perf_counter()
+            for k in range(S):
+                if tick < 2 * k:             # staggered start
+                    live = True
+                    continue
+                if cur[k] is None:
+                    if served[k] >= serve_s:
+                        continue
+                    hs = vox_hip.HostStream(ctx, interval_s=0.5)
+                    q.attach(hs)
+                    cur[k] = [hs, nxt[k] % len(clips), 0, False]
+                    nxt[k] += 1
+                live = True
+                hs, c, pos, _ = cur[k]
+                if pos < len(clips[c]):
+                    hs.feed(clips[c][pos:pos + piece])
+                    cur[k][2] = pos + piece
+                else:
+                    hs.finish()
+                    cur[k][3] = True
+            if not live:
+                break
+            q.run()
+            for k in range(S):
+                if cur[k] is None:
+                    continue
+                ids += len(cur[k][0].get())
+                if cur[k][3]:                 # finished this tick: retire the clip
+                    served[k] += len(clips[cur[k][1]]) / 16000.0
+                    q.detach(cur[k][0])
+                    cur[k][0].close()
+                    cur[k] = None
+                    clips_done += 1
+            lat.append(time.perf_counter() - t0)
+            tick += 1
+        return {"wall": time.perf_counter() - t_all, "ids": ids, "lat": lat, "ticks": tick,
+                "clips": clips_done, "audio_s": sum(served)}
+
+    for _ in range(args.warmup):
+        run(min(args.serve_seconds, 20.0))
+    q_stats0 = q.stats()
+    d.barrier()
+    runs = [run(args.serve_seconds) for _ in range(args.steps)]
+    d.barrier()
+    st = q.stats()
+    wall = d.max(sum(r["wall"] for r in runs))
+    ids_all = d.sum(sum(r["ids"] for r in runs))
+    audio_all = d.sum(sum(r["audio_s"] for r in runs))
+    lat = np.array([x for r in runs for x in r["lat"]]) * 1000.0
+    batch_tok = st["tokens"] - q_stats0["tokens"]
+    batch_ms = st["batch_ms"] - q_stats0["batch_ms"]
+    out = {
+        "metric": "decoder tokens/sec + encoder RTF, Voxtral-4B " + ("q8" if args.q8 else "bf16")
+                  + f", {S} streams per MI355X served by the per-GPU scheduler (config 4), at 1/2/4/8 MI355X",
+        "value": round(ids_all / wall, 2), "unit": "tokens/s", "n_gpus": d.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall * 1000.0 / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": round(ids_all / wall / d.world / MPS_TOK_S, 2),
+        "dtype": "f32", "weights_dtype": "q8" if args.q8 else "bf16",
+        "data": "synthetic (seeded random weights of the exact architecture; synthetic speech-band audio "
+                "of the 7 sample lengths)",
+        "config": {"workload": f"{S} streams per GPU, each serving {args.serve_seconds:.0f} s of audio as clips of "
+                               f"the 7 sample lengths {[round(x, 2) for x in SAMPLE_SECONDS]} s cycled (from clip i), "
+                               "fed in 0.5 s pieces (-I 0.5), starts staggered by 1 s; one vh_sched_run per tick",
+                   "model": "Voxtral-Mini-4B-Realtime", "global_batch": S * d.world, "streams_per_gpu": S,
+                   "parallelism": f"replicas x{d.world}, {S} scheduled streams each"},
+        "value_is": "all ids generated / wall time of the serving loop (mel, encoder, prefill and decode included)",
+        "tick_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
+                            "p99": round(float(np.percentile(lat, 99)), 3), "max": round(float(lat.max()), 3)},
+        "audio_seconds_per_wall_second": round(audio_all / wall, 2),
+        "overall_rtf_per_stream": round(wall / (audio_all / d.world / S), 5),
+        "clips": sum(r["clips"] for r in runs),
+        "batched_decode": {"ids": batch_tok, "ms": round(batch_ms, 1),
+                           "ids_per_s": round(batch_tok / max(1e-9, batch_ms * 1e-3), 1)},
+    }
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    q.close()
+    ctx.close()
     model.close()
 
 

@@ -83,6 +83,40 @@ typedef struct {
 } vh_stats_t;
 void vh_stream_stats(const vh_stream_t *s, vh_stats_t *out);
 
+/* Wrap a model the caller created with vox_hip_model_create (Python mirror, servers that
+ * load once and share): vh_free on the result leaves the model alone. */
+vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int delay_tokens);
+
+/* Per-GPU stream scheduler.  The reference decodes each vox_stream_t on its
+ * own: stream_run_decoder's token loop (voxtral.c:1105-1145) streams every decoder weight
+ * once per token per stream.  A scheduler owns up to VH_SCHED_MAX streams of one model on
+ * one GPU; attached streams run their mel front-end and encoder in vh_stream_feed / flush /
+ * finish as audio arrives, and leave the decoder to vh_sched_run, which
+ *   1. runs the prefill + first token of every stream whose prompt rows are complete,
+ *   2. advances every running stream by batched greedy steps (vox_hip_batch_decode: one
+ *      weight read per step for all of them, attention / KV / argmax per stream) until each
+ *      has used its adapter rows or produced EOS,
+ *   3. applies each stream's live-mode restarts (vh_stream_set_continuous) as run after its
+ *      own drain.
+ * Called after every round of feeds, it yields per stream the ids vh_stream_feed would have
+ * queued (vh_stream_get / get_alt read them as before).  Streams with --alt (n_alt > 1) keep
+ * the single-stream decode, whose steps record the candidates; a live-mode stream drains on
+ * its own path inside vh_stream_flush (and so inside vh_stream_finish), where the reference's
+ * restart checks run between the flush and the final chunk. */
+#define VH_SCHED_MAX 16
+typedef struct vh_sched vh_sched_t;
+typedef struct {
+    int runs, prefills, batch_calls;
+    long long tokens;        /* ids from batched steps */
+    double run_ms, batch_ms; /* wall time in vh_sched_run / in vox_hip_batch_decode */
+} vh_sched_stats_t;
+vh_sched_t *vh_sched_create(vh_ctx_t *ctx, int max_streams);
+void vh_sched_free(vh_sched_t *q);          /* detaches its streams */
+int vh_sched_attach(vh_sched_t *q, vh_stream_t *s);
+int vh_sched_detach(vh_sched_t *q, vh_stream_t *s);
+int vh_sched_run(vh_sched_t *q);            /* ids generated, < 0 on error */
+void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out);
+
 /* vox_load_wav (voxtral_audio.c:143-166) for 16 kHz mono 16-bit PCM: malloc'd samples */
 float *vh_load_wav(const char *path, int *n_samples);
 

@@ -1,0 +1,107 @@
+"""The per-GPU stream scheduler of the C host (vh_sched_*, include/vox_hip_host.h; SURVEY.md
+8f#1: the per-stream token loop of voxtral.c:1105-1145 and the feed path of :1288-1316
+turned into a serving loop).  Streams of different lengths start at staggered times and are
+fed in -I 0.5 pieces; after every round of feeds vh_sched_run prefills the streams whose
+prompt is complete and advances all running streams with batched steps.  Every stream's ids
+must equal its own single-stream CPU-oracle run on the same pieces (the reference's
+vox_stream_feed / flush / finish, voxtral.c:1288-1316, 1640-1667)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PIECE = 8000   # 0.5 s of 16 kHz samples per feed
+
+
+def _oracle_ids(om, audio, interval, continuous=False):
+    import vox_oracle
+    os_ = vox_oracle.OracleStream(om)
+    sess = vox_oracle.OracleAudioSession(os_, interval_s=interval, continuous=continuous)
+    for i in range(0, len(audio), PIECE):
+        sess.feed(audio[i:i + PIECE])
+    sess.finish()
+    ids, restarts = sess.tokens, sess.restarts
+    sess.close()
+    os_.close()
+    return ids, restarts
+
+
+def _serve(hm, audios, starts, interval, continuous=False, max_streams=8):
+    """One serving loop on one GPU: at tick t every stream that has started feeds its next
+    piece (flush + finish after its last one), then one vh_sched_run for all of them."""
+    import vox_hip
+    ctx = vox_hip.HostCtx(hm)
+    q = vox_hip.Scheduler(ctx, max_streams)
+    ss = [vox_hip.HostStream(ctx, interval_s=interval, continuous=continuous) for _ in audios]
+    for s in ss:
+        q.attach(s)
+    pos = [0] * len(audios)
+    done = [False] * len(audios)
+    ids = [[] for _ in audios]
+    tick = 0
+    while not all(done):
+        for k, (a, s) in enumerate(zip(audios, ss)):
+            if done[k] or tick < starts[k]:
+                continue
+            if pos[k] < len(a):
+                s.feed(a[pos[k]:pos[k] + PIECE])
+                pos[k] += PIECE
+            else:
+                s.finish()   # vox_stream_finish: flush padding, mel finish, last chunk
+                done[k] = True
+        q.run()
+        for k, s in enumerate(ss):
+            ids[k] += s.get()
+        tick += 1
+    st = q.stats()
+    for s in ss:
+        s.close()
+    q.close()
+    ctx.close()
+    return ids, st
+
+
+def test_scheduler_staggered_streams_match_oracle(tiny_weights, jfk_samples):
+    """6 streams, 6 audio lengths (2.5 .. 33 s, jfk-derived, different offsets), starts
+    staggered by 3 ticks; ids per stream equal the oracle's; the batched steps really ran
+    (more tokens from batched steps than from prefills)."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    long = np.concatenate([jfk_samples] * 3)
+    lens = [2.5, 11.0, 5.0, 33.0, 7.3, 19.0]
+    audios = [np.ascontiguousarray(long[int(k * 24000) % 16000:][:int(s * 16000)]) for k, s in enumerate(lens)]
+    starts = [3 * k for k in range(len(audios))]
+    ids, st = _serve(hm, audios, starts, 0.5)
+    for k, a in enumerate(audios):
+        ref, _ = _oracle_ids(om, a, 0.5)
+        assert len(ref) > 0
+        assert ids[k] == ref, (k, len(ids[k]), len(ref))
+    assert st["tokens"] > st["prefills"] > 0 and st["batch_calls"] > 0
+    print("scheduler stats", st)
+    hm.close()
+    om.close()
+
+
+def test_scheduler_continuous_restarts_per_stream(tiny_weights, jfk_samples):
+    """Live mode (vh_stream_set_continuous) on two scheduled streams of 88 s: each stream's
+    restarts (64-token non-text streaks on the random TINY model, voxtral.c:1189-1239) stay
+    its own, and its ids equal the oracle's live-mode session on the same pieces."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    a = np.concatenate([jfk_samples] * 8)
+    audios = [a, np.ascontiguousarray(-a[5000:])]
+    ids, _ = _serve(hm, audios, [0, 7], 2.0, continuous=True)
+    n_restarts = 0
+    for k, au in enumerate(audios):
+        ref, restarts = _oracle_ids(om, au, 2.0, continuous=True)
+        n_restarts += len(restarts)
+        assert ids[k] == ref, (k, len(ids[k]), len(ref))
+    assert n_restarts > 0
+    hm.close()
+    om.close()

@@ -439,7 +439,20 @@ struct vh_ctx {
     vox_hip_config_t cfg;
     vox_hip_model_t *model;
     int delay_tokens;
+    int owns_model;   /* 0: vh_ctx_wrap of a caller's model */
 };
+
+vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int delay_tokens) {
+    if (!model || !cfg) {
+        fail("vh_ctx_wrap: null model or config");
+        return NULL;
+    }
+    vh_ctx_t *ctx = calloc(1, sizeof *ctx);
+    ctx->cfg = *cfg;
+    ctx->model = model;
+    ctx->delay_tokens = delay_tokens;
+    return ctx;
+}
 
 const vox_hip_config_t *vh_config(const vh_ctx_t *ctx) { return &ctx->cfg; }
 
@@ -543,6 +556,7 @@ vh_ctx_t *vh_load(const char *path) {
     ctx->delay_tokens = 6;  /* default 480 ms (voxtral.c:136) */
     if (!L.bad) {
         ctx->model = vox_hip_model_create(c, &w, ctx->delay_tokens);
+        ctx->owns_model = 1;
         if (!ctx->model) fail("vox_hip_model_create: %s", vox_hip_last_error());
     }
     arena_free(&a);
@@ -556,7 +570,7 @@ vh_ctx_t *vh_load(const char *path) {
 
 void vh_free(vh_ctx_t *ctx) {
     if (!ctx) return;
-    vox_hip_model_free(ctx->model);
+    if (ctx->owns_model) vox_hip_model_free(ctx->model);
     free(ctx);
 }
 
@@ -580,6 +594,7 @@ int vh_set_delay(vh_ctx_t *ctx, int delay_ms) {
 
 struct vh_stream {
     vh_ctx_t *ctx;
+    vh_sched_t *sched;          /* non-NULL: decoding is left to vh_sched_run */
     vox_hip_stream_t *st;
     vox_hip_mel_t *mel;
     int mel_cursor, conv_started, finished, min_new_mel;
@@ -622,6 +637,7 @@ vh_stream_t *vh_stream_init(vh_ctx_t *ctx) {
 
 void vh_stream_free(vh_stream_t *s) {
     if (!s) return;
+    if (s->sched) vh_sched_detach(s->sched, s);
     vox_hip_mel_free(s->mel);
     vox_hip_stream_free(s->st);
     free(s->queue);
@@ -714,63 +730,48 @@ static int reset_full(vh_stream_t *s) {
     return 0;
 }
 
-/* stream_run_decoder (voxtral.c:1013-1240): prefill once the prompt's adapter rows exist,
- * then every available row; greedy decoding stops after EOS (token 2).  In continuous
- * (live) mode the decoder restarts afterwards on EOS, KV > 2000, a 64-token non-text
- * streak or 20 s of audio without a decoded token, escalating to a full reset
- * (voxtral.c:1189-1239). */
-static int run_decoder(vh_stream_t *s) {
-    const int prompt_len = 1 + 32 + s->ctx->delay_tokens;
-    int st6[6];
-    vox_hip_stream_state(s->st, st6);
-    if (!st6[3] && vox_hip_stream_adapter_tokens(s->st) < prompt_len) return 0;  /* waiting for the prompt */
-    int eos = 0;
-    for (;;) {
-        const double t0 = now_ms();
-        const int first = !s->started_decoding;
-        vox_hip_stream_state(s->st, st6);
-        const int gen0 = st6[5];
-        /* the first call runs the prefill + first token alone, so its time is the
-         * reference's prefill_ms */
-        const int n = vox_hip_stream_decode(s->st, first ? 1 : 4096, 1, s->dec_buf, NULL);
-        if (n < 0) return fail("decoder: %s", vox_hip_last_error());
-        const double dt = now_ms() - t0;
-        if (n == 0) break;
-        if (first) {
-            s->prefill_ms += dt;
-            s->started_decoding = 1;
-        }
-        s->dec_ms += dt;
-        s->generated += n;
-        s->last_decode_sample = s->real_samples;
-        if (s->n_alt > 1) {
-            if (vox_hip_stream_read_alts(s->st, gen0, n, s->alt_buf, NULL))
-                return fail("alternatives: %s", vox_hip_last_error());
+/* stream_enqueue_token for n ids just generated (s->dec_buf; their alternatives records
+ * in s->alt_buf): token classes for the live-mode counters (voxtral.c:1116-1139), records
+ * queued.  Sets *eos when the ids end with EOS. */
+static void consume_tokens(vh_stream_t *s, int n, int *eos) {
+    s->generated += n;
+    s->last_decode_sample = s->real_samples;
+    for (int i = 0; i < n; i++) {
+        const int cls = vh_token_class(s->dec_buf[i]);
+        if (cls == VH_TOK_TEXT) {
+            s->text_since_restart = 1;
+            s->empty_restarts = 0;
+            s->nontext_streak = 0;
+        } else if (cls != VH_TOK_EOS) {
+            s->nontext_streak++;
+            /* alternatives belong to text tokens only (stream_fill_alts is called for
+             * STREAM_TOK_TEXT) */
+            for (int a = 1; a < VH_MAX_ALT; a++) s->alt_buf[i * VH_MAX_ALT + a] = -1;
         } else {
-            for (int i = 0; i < n; i++) {
-                s->alt_buf[i * VH_MAX_ALT] = s->dec_buf[i];
-                for (int a = 1; a < VH_MAX_ALT; a++) s->alt_buf[i * VH_MAX_ALT + a] = -1;
-            }
+            *eos = 1;
         }
-        for (int i = 0; i < n; i++) {
-            const int cls = vh_token_class(s->dec_buf[i]);
-            if (cls == VH_TOK_TEXT) {
-                s->text_since_restart = 1;
-                s->empty_restarts = 0;
-                s->nontext_streak = 0;
-            } else if (cls != VH_TOK_EOS) {
-                s->nontext_streak++;
-                /* alternatives belong to text tokens only (stream_fill_alts is called for
-                 * STREAM_TOK_TEXT) */
-                for (int a = 1; a < VH_MAX_ALT; a++) s->alt_buf[i * VH_MAX_ALT + a] = -1;
-            } else {
-                eos = 1;
-            }
-        }
-        queue_push(s, s->alt_buf, n);
-        if (eos) break;
     }
+    queue_push(s, s->alt_buf, n);
+}
+
+/* alternatives records of the n ids in s->dec_buf (generated from step gen0 on) */
+static int fill_alt_records(vh_stream_t *s, int gen0, int n) {
+    if (s->n_alt > 1) {
+        if (vox_hip_stream_read_alts(s->st, gen0, n, s->alt_buf, NULL))
+            return fail("alternatives: %s", vox_hip_last_error());
+        return 0;
+    }
+    for (int i = 0; i < n; i++) {
+        s->alt_buf[i * VH_MAX_ALT] = s->dec_buf[i];
+        for (int a = 1; a < VH_MAX_ALT; a++) s->alt_buf[i * VH_MAX_ALT + a] = -1;
+    }
+    return 0;
+}
+
+/* the live-mode restart checks after a decoder drain (voxtral.c:1189-1239) */
+static int after_drain(vh_stream_t *s, int eos) {
     if (!s->continuous) return 0;
+    int st6[6];
     vox_hip_stream_state(s->st, st6);
     const int started = st6[3];
     int need = 0;
@@ -798,11 +799,50 @@ static int run_decoder(vh_stream_t *s) {
     return 0;
 }
 
+/* the prompt's adapter rows are there (or the decoder already runs) */
+static int decoder_ready(vh_stream_t *s) {
+    int st6[6];
+    vox_hip_stream_state(s->st, st6);
+    return st6[3] || vox_hip_stream_adapter_tokens(s->st) >= 1 + 32 + s->ctx->delay_tokens;
+}
+
+/* stream_run_decoder (voxtral.c:1013-1240): prefill once the prompt's adapter rows exist,
+ * then every available row; greedy decoding stops after EOS (token 2).  In continuous
+ * (live) mode the decoder restarts afterwards on EOS, KV > 2000, a 64-token non-text
+ * streak or 20 s of audio without a decoded token, escalating to a full reset
+ * (voxtral.c:1189-1239). */
+static int run_decoder(vh_stream_t *s) {
+    if (!decoder_ready(s)) return 0;  /* waiting for the prompt */
+    int eos = 0;
+    for (;;) {
+        const double t0 = now_ms();
+        const int first = !s->started_decoding;
+        int st6[6];
+        vox_hip_stream_state(s->st, st6);
+        const int gen0 = st6[5];
+        /* the first call runs the prefill + first token alone, so its time is the
+         * reference's prefill_ms */
+        const int n = vox_hip_stream_decode(s->st, first ? 1 : 4096, 1, s->dec_buf, NULL);
+        if (n < 0) return fail("decoder: %s", vox_hip_last_error());
+        const double dt = now_ms() - t0;
+        if (n == 0) break;
+        if (first) {
+            s->prefill_ms += dt;
+            s->started_decoding = 1;
+        }
+        s->dec_ms += dt;
+        if (fill_alt_records(s, gen0, n)) return -1;
+        consume_tokens(s, n, &eos);
+        if (eos) break;
+    }
+    return after_drain(s, eos);
+}
+
 int vh_stream_feed(vh_stream_t *s, const float *samples, int n) {
     if (!s || s->finished || n <= 0) return -1;
     if (vox_hip_mel_feed(s->mel, samples, n) < 0) return fail("mel: %s", vox_hip_last_error());
     s->real_samples += n;
-    if (run_encoder(s) || run_decoder(s)) return -1;
+    if (run_encoder(s) || (!s->sched && run_decoder(s))) return -1;
     return 0;
 }
 
@@ -818,7 +858,10 @@ int vh_stream_flush(vh_stream_t *s) {
     if (rc < 0) return fail("mel: %s", vox_hip_last_error());
     const int saved = s->min_new_mel;
     s->min_new_mel = 1;
-    const int e = run_encoder(s) || run_decoder(s);
+    /* a scheduled stream leaves the drain to vh_sched_run, except in live mode: there the
+     * restart checks after this drain (voxtral.c:1189-1239) come before the final chunk of
+     * vox_stream_finish, so the stream drains here on its own path */
+    const int e = run_encoder(s) || ((!s->sched || s->continuous) && run_decoder(s));
     s->min_new_mel = saved;
     return e ? -1 : 0;
 }
@@ -828,7 +871,7 @@ int vh_stream_finish(vh_stream_t *s) {
     if (vh_stream_flush(s)) return -1;
     s->finished = 1;
     if (vox_hip_mel_finish(s->mel, 0) < 0) return fail("mel: %s", vox_hip_last_error());
-    if (run_encoder(s) || run_decoder(s)) return -1;
+    if (run_encoder(s) || (!s->sched && run_decoder(s))) return -1;
     return 0;
 }
 
@@ -862,6 +905,143 @@ void vh_stream_stats(const vh_stream_t *s, vh_stats_t *o) {
     o->prefill_ms = s->prefill_ms;
     o->restarts = s->restarts;
     o->full_resets = s->full_resets;
+}
+
+/* ------------------------------------------------------------------------
+ * Per-GPU stream scheduler (the per-stream token loop of voxtral.c:
+ * 1105-1145 turned into one batched step for every stream that has adapter rows)
+ * ------------------------------------------------------------------------ */
+#define VH_SCHED_STEPS 4096   /* tokens per stream and vox_hip_batch_decode call */
+
+struct vh_sched {
+    vh_ctx_t *ctx;
+    vox_hip_batch_t *batch;   /* made on the first batched step (fragment-major weight copies) */
+    int cap, n;
+    vh_stream_t *s[VH_SCHED_MAX];
+    int *tok;                 /* [cap][VH_SCHED_STEPS] */
+    vh_sched_stats_t stats;
+};
+
+vh_sched_t *vh_sched_create(vh_ctx_t *ctx, int max_streams) {
+    if (!ctx || max_streams < 1 || max_streams > VH_SCHED_MAX) {
+        fail("vh_sched_create: 1..%d streams", VH_SCHED_MAX);
+        return NULL;
+    }
+    vh_sched_t *q = calloc(1, sizeof *q);
+    q->ctx = ctx;
+    q->cap = max_streams;
+    q->tok = malloc(sizeof(int) * (size_t)max_streams * VH_SCHED_STEPS);
+    return q;
+}
+
+void vh_sched_free(vh_sched_t *q) {
+    if (!q) return;
+    for (int i = 0; i < q->n; i++) q->s[i]->sched = NULL;
+    vox_hip_batch_free(q->batch);
+    free(q->tok);
+    free(q);
+}
+
+int vh_sched_attach(vh_sched_t *q, vh_stream_t *s) {
+    if (!q || !s || s->ctx->model != q->ctx->model) return fail("vh_sched_attach: stream of another model");
+    if (s->sched == q) return 0;
+    if (s->sched) return fail("vh_sched_attach: stream already attached to a scheduler");
+    if (q->n == q->cap) return fail("vh_sched_attach: scheduler full (%d streams)", q->cap);
+    q->s[q->n++] = s;
+    s->sched = q;
+    return 0;
+}
+
+int vh_sched_detach(vh_sched_t *q, vh_stream_t *s) {
+    for (int i = 0; i < q->n; i++)
+        if (q->s[i] == s) {
+            q->s[i] = q->s[--q->n];
+            s->sched = NULL;
+            return 0;
+        }
+    return fail("vh_sched_detach: stream not attached");
+}
+
+void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) { *out = q->stats; }
+
+int vh_sched_run(vh_sched_t *q) {
+    const double t_run = now_ms();
+    int total = 0;
+    int eos[VH_SCHED_MAX] = {0}, ran[VH_SCHED_MAX] = {0};
+    /* 1. streams whose decoder is not running yet: prefill + first token alone (the
+     *    reference's prefill_ms); streams with --alt keep the single-stream path, whose steps
+     *    record the candidates (the batched step keeps none) */
+    for (int i = 0; i < q->n; i++) {
+        vh_stream_t *s = q->s[i];
+        if (!decoder_ready(s)) continue;
+        if (s->n_alt > 1) {
+            const int g0 = s->generated;
+            if (run_decoder(s)) return -1;
+            total += s->generated - g0;
+            ran[i] = 2;  /* restart checks done by run_decoder */
+            continue;
+        }
+        ran[i] = 1;
+        if (s->started_decoding) continue;
+        const double t0 = now_ms();
+        const int n = vox_hip_stream_decode(s->st, 1, 1, s->dec_buf, NULL);
+        if (n < 0) return fail("decoder: %s", vox_hip_last_error());
+        if (n == 0) continue;
+        const double dt = now_ms() - t0;
+        s->prefill_ms += dt;
+        s->dec_ms += dt;
+        s->started_decoding = 1;
+        if (fill_alt_records(s, 0, n)) return -1;
+        consume_tokens(s, n, &eos[i]);
+        total += n;
+        q->stats.prefills++;
+    }
+    /* 2. greedy steps batched over every running stream until each has used its adapter
+     *    rows or met EOS (one weight read per step for all of them) */
+    for (;;) {
+        vox_hip_stream_t *hs[VH_SCHED_MAX];
+        int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], nb = 0;
+        for (int i = 0; i < q->n; i++) {
+            vh_stream_t *s = q->s[i];
+            if (ran[i] != 1 || eos[i] || !s->started_decoding) continue;
+            int st6[6];
+            vox_hip_stream_state(s->st, st6);
+            if (st6[4] || vox_hip_stream_adapter_tokens(s->st) - st6[1] <= 0) continue;
+            hs[nb] = s->st;
+            idx[nb++] = i;
+        }
+        if (!nb) break;
+        if (!q->batch) {
+            q->batch = vox_hip_batch_create(q->ctx->model, q->cap);
+            if (!q->batch) return fail("batch: %s", vox_hip_last_error());
+        }
+        const double t0 = now_ms();
+        const int r = vox_hip_batch_decode(q->batch, hs, nb, VH_SCHED_STEPS, 1, q->tok, counts);
+        if (r < 0) return fail("batched decoder: %s", vox_hip_last_error());
+        const double dt = now_ms() - t0;
+        q->stats.batch_calls++;
+        q->stats.batch_ms += dt;
+        int more = 0;
+        for (int k = 0; k < nb; k++) {
+            vh_stream_t *s = q->s[idx[k]];
+            const int n = counts[k];
+            s->dec_ms += dt;
+            if (!n) continue;
+            memcpy(s->dec_buf, q->tok + (size_t)k * VH_SCHED_STEPS, sizeof(int) * (size_t)n);
+            if (fill_alt_records(s, 0, n)) return -1;
+            consume_tokens(s, n, &eos[idx[k]]);
+            total += n;
+            more |= n == VH_SCHED_STEPS;
+        }
+        q->stats.tokens += r;
+        if (r == 0 || !more) break;
+    }
+    /* 3. per-stream live-mode restarts (voxtral.c:1189-1239) */
+    for (int i = 0; i < q->n; i++)
+        if (ran[i] == 1 && after_drain(q->s[i], eos[i])) return -1;
+    q->stats.runs++;
+    q->stats.run_ms += now_ms() - t_run;
+    return total;
 }
 
 /* ------------------------------------------------------------------------

@@ -551,3 +551,136 @@ def encoder_attention(Q, K, V, n_heads, n_kv_heads, head_dim, window, q_offset):
                Q.shape[0], K.shape[0], n_heads, n_kv_heads, head_dim, float(1.0 / np.sqrt(head_dim)),
                window, q_offset)
     return out
+
+
+# ---------------------------------------------------------------------------
+# the C host side (include/vox_hip_host.h, libvox_hip_host.so): vh_stream_* and the per-GPU
+# stream scheduler, over a model this process created
+# ---------------------------------------------------------------------------
+HOST_LIB_PATH = os.path.join(_HERE, "libvox_hip_host.so")
+_host = None
+
+
+class SchedStats(ctypes.Structure):
+    _fields_ = [("runs", ctypes.c_int), ("prefills", ctypes.c_int), ("batch_calls", ctypes.c_int),
+                ("tokens", ctypes.c_longlong), ("run_ms", ctypes.c_double), ("batch_ms", ctypes.c_double)]
+
+
+def host_lib():
+    global _host
+    if _host is not None:
+        return _host
+    lib()  # the C ABI library first (the host library links it)
+    if not os.path.exists(HOST_LIB_PATH):
+        raise RuntimeError(f"{HOST_LIB_PATH} not built (run __graft_entry__.build())")
+    H = ctypes.CDLL(HOST_LIB_PATH)
+    P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    ip = ctypes.POINTER(ctypes.c_int)
+    sig = {
+        "vh_ctx_wrap": (P, [P, P, I]), "vh_free": (None, [P]), "vh_last_error": (ctypes.c_char_p, []),
+        "vh_stream_init": (P, [P]), "vh_stream_free": (None, [P]),
+        "vh_set_processing_interval": (None, [P, F]), "vh_stream_set_continuous": (None, [P, I]),
+        "vh_stream_feed": (I, [P, ctypes.POINTER(ctypes.c_float), I]), "vh_stream_flush": (I, [P]),
+        "vh_stream_finish": (I, [P]), "vh_stream_get": (I, [P, ip, I]),
+        "vh_sched_create": (P, [P, I]), "vh_sched_free": (None, [P]), "vh_sched_attach": (I, [P, P]),
+        "vh_sched_detach": (I, [P, P]), "vh_sched_run": (I, [P]),
+        "vh_sched_stats": (None, [P, ctypes.POINTER(SchedStats)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(H, name)
+        fn.restype = res
+        fn.argtypes = args
+    _host = H
+    return H
+
+
+def _herr(what):
+    msg = host_lib().vh_last_error()
+    raise RuntimeError(f"{what}: {msg.decode() if msg else 'unknown error'}")
+
+
+class HostCtx:
+    """vh_ctx_t over a Model of this process (vh_ctx_wrap: the model stays the Model's)."""
+
+    def __init__(self, model: Model):
+        self.model = model
+        self.h = host_lib().vh_ctx_wrap(model.h, ctypes.byref(model._cfg_c), model.delay_tokens)
+        if not self.h:
+            _herr("vh_ctx_wrap")
+
+    def close(self):
+        if self.h:
+            host_lib().vh_free(self.h)
+            self.h = None
+
+
+class HostStream:
+    """vh_stream_t: vox_stream_feed / flush / finish / get of the C host (voxtral.c:1242-1327)."""
+
+    def __init__(self, ctx: HostCtx, interval_s: float = STREAM_DEFAULT_INTERVAL, continuous: bool = False):
+        H = host_lib()
+        self.h = H.vh_stream_init(ctx.h)
+        if not self.h:
+            _herr("vh_stream_init")
+        H.vh_set_processing_interval(self.h, interval_s)
+        H.vh_stream_set_continuous(self.h, int(continuous))
+
+    def feed(self, samples: np.ndarray):
+        samples = np.ascontiguousarray(samples, np.float32)
+        if host_lib().vh_stream_feed(self.h, fptr(samples), samples.shape[0]) != 0:
+            _herr("vh_stream_feed")
+
+    def flush(self):
+        if host_lib().vh_stream_flush(self.h) != 0:
+            _herr("vh_stream_flush")
+
+    def finish(self):
+        if host_lib().vh_stream_finish(self.h) != 0:
+            _herr("vh_stream_finish")
+
+    def get(self) -> list[int]:
+        out, buf = [], np.empty(4096, np.int32)
+        while True:
+            n = host_lib().vh_stream_get(self.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), 4096)
+            out += buf[:n].tolist()
+            if n < 4096:
+                return out
+
+    def close(self):
+        if self.h:
+            host_lib().vh_stream_free(self.h)
+            self.h = None
+
+
+class Scheduler:
+    """vh_sched_t: up to 16 HostStreams of one model on this GPU; run() decodes every
+    attached stream's pending adapter rows with batched greedy steps."""
+
+    def __init__(self, ctx: HostCtx, max_streams: int):
+        self.h = host_lib().vh_sched_create(ctx.h, max_streams)
+        if not self.h:
+            _herr("vh_sched_create")
+
+    def attach(self, s: HostStream):
+        if host_lib().vh_sched_attach(self.h, s.h) != 0:
+            _herr("vh_sched_attach")
+
+    def detach(self, s: HostStream):
+        if host_lib().vh_sched_detach(self.h, s.h) != 0:
+            _herr("vh_sched_detach")
+
+    def run(self) -> int:
+        n = host_lib().vh_sched_run(self.h)
+        if n < 0:
+            _herr("vh_sched_run")
+        return n
+
+    def stats(self) -> dict:
+        st = SchedStats()
+        host_lib().vh_sched_stats(self.h, ctypes.byref(st))
+        return {f: getattr(st, f) for f, _ in SchedStats._fields_}
+
+    def close(self):
+        if self.h:
+            host_lib().vh_sched_free(self.h)
+            self.h = None

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -219,6 +219,13 @@ int main(int argc, char** argv) {
         while (splits * ATT_BLOCK_KEYS < L) splits *= 2;
         add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, splits, st)); }, iters, st),
             (double)L * DKV * 2 * 4);
+        if (L <= 256) {
+            g_attn_short = 0;
+            snprintf(nm, sizeof nm, "attn decode L=%d k_attn_decode", L);
+            add(nm, timeit([&] { CK(launch_attn_decode(HD, x, Kc, Vc, cap, state, 0, 8192, 0.088f, H, KVH, part, y, splits, st)); }, iters, st),
+                (double)L * DKV * 2 * 4);
+            g_attn_short = 1;
+        }
         for (int lw : {2, 4}) {
             if (L <= 256) continue;
             g_attn_lw = lw;

@@ -1547,6 +1547,97 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     }
 }
 
+// ============================================================================
+// Short-context decode attention of one stream (L <= 256 keys, head_dim 128, window >= 256):
+// before 256 positions nothing has left the window and the ring has not wrapped, so the keys
+// are ring slots 0..lp and a wave's 16 slots (16 * wave ..) are known without the step
+// state.  Every K/V and q load goes out at kernel start beside the state read (in
+// k_attn_decode they waited for it: ~2 us of the 6.4), each wave runs QK / softmax / PV on
+// its own registers (no q staging barrier), and the 16 wave partials meet in LDS behind one
+// barrier, the merge factors recomputed by each output thread.  Keys past lp are masked
+// (their slots hold older, finite values or zeros).  Grid: one block per query head, the 4
+// heads of a kv head on one XCD (blocks y, y + 8, ..: the K/V rows go through one L2).
+// ============================================================================
+template <int HD>
+__global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q, const float* __restrict__ Kc,
+                                                     const float* __restrict__ Vc, const int* __restrict__ state,
+                                                     int pos_host, float scale, int H, int KVH,
+                                                     float* __restrict__ out) {
+    static_assert(HD == 128, "k_attn_short: head_dim 128 layout");
+    constexpr int NWV = 16, DQ = HD / 4, DPL = HD / 64;
+    __shared__ float sM[NWV], sL[NWV];
+    __shared__ __attribute__((aligned(16))) float sO[NWV][HD];
+    const int hpk = H / KVH;
+    const int kvh = (int)blockIdx.x % KVH, h = kvh * hpk + (int)blockIdx.x / KVH;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kvd = KVH * HD, k0 = wave * ATT_CH;
+    const int r = lane >> 3, c = lane & 7;
+    // K: load i covers keys r + 8 (i & 1), quarter row i >> 1 (8 whole lines per instruction)
+    float4 kv[DQ / 4];
+#pragma unroll
+    for (int i = 0; i < DQ / 4; i++)
+        kv[i] = *reinterpret_cast<const float4*>(Kc + (size_t)(k0 + r + 8 * (i & 1)) * kvd + kvh * HD + (i >> 1) * DQ + c * 4);
+    float2 vv[ATT_CH];
+#pragma unroll
+    for (int k = 0; k < ATT_CH; k++) vv[k] = *reinterpret_cast<const float2*>(Vc + (size_t)(k0 + k) * kvd + kvh * HD + lane * DPL);
+    float4 qv[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) qv[j] = *reinterpret_cast<const float4*>(q + (size_t)h * HD + j * DQ + c * 4);
+    const int lp = state ? state[0] : pos_host;
+    const int kn = min(ATT_CH, lp + 1 - k0);  // keys of this wave inside the context (<= 0: none)
+    float aa = 0.f, ab = 0.f;
+#pragma unroll
+    for (int i = 0; i < DQ / 4; i++) {
+        const float4 qq = qv[i >> 1];
+        float& acc = (i & 1) ? ab : aa;
+        acc = fmaf(qq.x, kv[i].x, acc);
+        acc = fmaf(qq.y, kv[i].y, acc);
+        acc = fmaf(qq.z, kv[i].z, acc);
+        acc = fmaf(qq.w, kv[i].w, acc);
+    }
+    aa += dpp<0xB1>(aa); aa += dpp<0x4E>(aa); aa += dpp<0x141>(aa);
+    ab += dpp<0xB1>(ab); ab += dpp<0x4E>(ab); ab += dpp<0x141>(ab);
+    const float sa = (r < kn) ? aa * scale : -INFINITY, sbv = (r + 8 < kn) ? ab * scale : -INFINITY;
+    float mx = fmaxf(sa, sbv);
+    mx = fmaxf(mx, dpp<0x140>(mx));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m = (kn > 0) ? mx : -1e30f;
+    const float p = (r < kn) ? expf(sa - mx) : 0.f, pb = (r + 8 < kn) ? expf(sbv - mx) : 0.f;
+    float t = p + pb;
+    t += dpp<0x140>(t);
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    float o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < ATT_CH; k++) {
+        const float pv = k >= 8 ? pb : p;
+        const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), 8 * (k & 7)));
+        const float2 v = k < kn ? vv[k] : make_float2(0.f, 0.f);
+        o0 = fmaf(pk, v.x, o0);
+        o1 = fmaf(pk, v.y, o1);
+    }
+    if (lane == 0) {
+        sM[wave] = m;
+        sL[wave] = t;
+    }
+    *reinterpret_cast<float2*>(&sO[wave][lane * DPL]) = make_float2(o0, o1);
+    __syncthreads();
+    if (tid < HD) {
+        float M = -1e30f;
+#pragma unroll
+        for (int w = 0; w < NWV; w++) M = fmaxf(M, sM[w]);
+        float den = 0.f, num = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; w++) {
+            const float f = expf(sM[w] - M);
+            den = fmaf(f, sL[w], den);
+            num = fmaf(f, sO[w][tid], num);
+        }
+        out[(size_t)h * HD + tid] = den > 0.f ? num * (1.0f / den) : 0.f;
+    }
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int maxs, int pos_host, int window, int bk,
                                                       uint16_t* __restrict__ xs = nullptr, int H = 0) {
@@ -3078,9 +3169,20 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
 
 // splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
 // step the launch serves); 1 -> one block per query head, no combine kernel.
+int g_attn_short = -1;  // k_attn_short for one stream's contexts <= 256 keys (VOX_HIP_ATT_SHORT=0: off)
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
                               int KVH, float* part, float* out, int splits, hipStream_t st) {
+    if (g_attn_short < 0) {
+        const char* e = getenv("VOX_HIP_ATT_SHORT");
+        g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    if (g_attn_short && splits == 1 && hd == 128 && window >= ATT_BK && cap >= ATT_BK && H % KVH == 0) {
+        // contexts of <= 256 keys (splits == 1) with a window of >= 256: keys = slots 0..lp
+        hipLaunchKernelGGL(k_attn_short<128>, dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host, scale, H, KVH, out);
+        LAUNCH_CHECK();
+        return hipSuccess;
+    }
     AttnPtrs p;
     memset(&p, 0, sizeof p);
     p.q[0] = q; p.Kc[0] = Kc; p.Vc[0] = Vc; p.state[0] = state; p.part[0] = part; p.out[0] = out;

@@ -104,6 +104,8 @@ int main(int argc, char** argv) {
         printf("%-34s %9.2f us  %8.1f GB/s\n", n, us, bytes / us / 1e3);
         fflush(stdout);
     };
+    const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
+    if (!only_gemmf) {
     add("gemv qkv  (6144x3072, norm+rope)", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D * 2);
     add("gemv wo   (3072x4096, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ * 2);
     add("gemv w13  (18432x3072, norm+swiglu)", timeit([&] { gemv(PRO_NORM_ADA, EPI_SWIGLU, w13[layer++ % NL], D, 2 * DH); }, iters, st), 2.0 * DH * D * 2);
@@ -142,6 +144,8 @@ int main(int argc, char** argv) {
     add("q8 gemv w2   (3072x9216)", timeit([&] { gemv(PRO_NONE, EPI_RESID, w2[layer++ % NL], DH, D); }, iters, st), (double)D * DH);
     add("q8 gemv lm   (131072x3072)", timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 10 + 1, st), (double)V * D);
     qs = nullptr;
+    }
+    if (!only_gemmf)
     {
         // M>1 GEMMs of the encoder / prefill (useful TFLOP/s = 2 M N K / t)
         float* ws = (float*)dmalloc((size_t)8 << 22, 0);
@@ -166,6 +170,29 @@ int main(int argc, char** argv) {
             printf("%-34s %9.2f us  %8.1f TFLOP/s (useful)\n", nm, us, 2.0 * g.M * g.N * g.K / us / 1e6);
         }
     }
+    {
+        // k_gemmf (stream-K, planes x fragment-major weights) at the encoder's shapes
+        const size_t wsn = gemmf_ws_floats(gemmf_grid());
+        float* gws = (float*)dmalloc(wsn * 4, 0);
+        int* gfl = (int*)dmalloc(4096 * 4, 0);
+        uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 5120 * 2, 1);
+        uint16_t* go = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 5120 * 2, 0);
+        float* gc = (float*)dmalloc((size_t)1024 * 10240 * 4, 0);
+        int epoch = 0;
+        struct G { const char* n; int epi, N, K; const uint16_t* W; };
+        for (int M : {70, 677, 1024})
+            for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
+                        G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
+                for (int np : {2, 3}) {
+                    double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
+                                                             g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
+                    printf("gemmf %-4s M=%4d %dx%d np%d   %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
+                           g.K, np, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                    fflush(stdout);
+                }
+            }
+    }
+    if (only_gemmf) return 0;
     {
         // batched decode GEMMs (16 streams, fragment-major weights and planes); weights are
         // constant-filled, so the packed layout does not matter for timing

@@ -480,6 +480,9 @@ struct vox_hip_stream {
     uint16_t* exp2;          // k_sklx: the second planes buffer (wo / w2 inputs)
     int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
     float* essq;             // k_sklx row sums of squares per column slice [2][slices][16]
+    uint16_t *gpa, *gpc;     // k_gemmf planes: norm / attention rows (K <= max(enc_dim, heads x hd)), gate rows
+    int* gflags;             // k_gemmf partial-tile flags (gemmf_grid() ints)
+    int gepoch;              // k_gemmf launch epoch on this stream
     int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
     float alt_cutoff;
     int graph_alt;           // alt mode the step graphs were captured with
@@ -616,6 +619,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
     dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2);
+    dfree(s->gpa); dfree(s->gpc); dfree(s->gflags);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
     for (hipEvent_t e : s->pev) hipEventDestroy(e);
@@ -1041,6 +1045,72 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
     return 0;
 }
 
+// Encoder passes of more rows (one-shot chunks: 677 rows for jfk, 1024-row passes of long
+// clips): the projections on k_gemmf (stream-K MFMA over fragment-major weights), their
+// inputs written as planes by the producers (RMSNorm rows, the attention output, the W1|W3
+// SwiGLU epilogue), so no GEMM re-splits f32 activations per column tile.
+static int enc_gemmf_env() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VOX_HIP_GEMMF");
+        v = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return v;
+}
+
+static bool enc_gemmf_ok(const vox_hip_model_t* m, int n) {
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, EQ = c.enc_heads * c.enc_head_dim, EKV = c.enc_kv_heads * c.enc_head_dim;
+    return enc_gemmf_env() && !m->enc[0].sqkv && gemmf_ok(n, EQ + 2 * EKV, ED) && gemmf_ok(n, ED, EQ) &&
+           gemmf_ok(n, 2 * c.enc_hidden, ED) && gemmf_ok(n, ED, c.enc_hidden) && c.enc_hidden % 64 == 0 &&
+           ED <= 4 * 512;
+}
+
+static int gemmf(vox_hip_stream_t* s, int epi, const uint16_t* xs, int K, int n, const uint8_t* W, int N,
+                 const float* bias, float* C, int ldc, uint16_t* xo) {
+    if (++s->gepoch <= 0) s->gepoch = 1;
+    CK(launch_gemmf(epi, gemm_planes_np(), xs, K, n, W, N, bias, C, ldc, xo, s->gws, s->gws_n, s->gflags, s->gepoch,
+                    s->st));
+    return 0;
+}
+
+static int run_encoder_rows_gemmf(vox_hip_stream_t* s, float* x, int n, long long pos0, const float* rope) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, H = c.enc_heads, KVH = c.enc_kv_heads, hd = c.enc_head_dim;
+    const int EQ = H * hd, EKV = KVH * hd, EH = c.enc_hidden, NQKV = EQ + 2 * EKV;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = s->st;
+    if (model_enc_frag(m)) return -1;
+    if (!s->gpa) {
+        const size_t rb = PLANE_MAX_ROWS / SK_ROWS;
+        CK(dalloc(&s->gpa, rb * 3 * SK_ROWS * std::max(ED, EQ)));
+        CK(dalloc(&s->gpc, rb * 3 * SK_ROWS * EH));
+        CK(dalloc(&s->gflags, (size_t)gemmf_grid()));
+    }
+    for (int l = 0; l < c.enc_layers; l++) {
+        const EncLayerD& L = m->enc[l];
+        const DecFragD& F = m->efrag[l];
+        float* Kc = s->ek + (size_t)l * s->ecap * EKV;
+        float* Vc = s->ev + (size_t)l * s->ecap * EKV;
+        // RMSNorm -> planes, QKV (+ bias), RoPE + K/V append (encoder.c:562-607)
+        CK(launch_rmsnorm_fplanes(x, n, ED, L.attn_norm, nullptr, c.enc_eps, s->gpa, nullptr, 0, st));
+        if (gemmf(s, EPI_STORE, s->gpa, ED, n, F.wqkv, NQKV, L.bqkv, s->qkv, NQKV, nullptr)) return -1;
+        CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
+        // windowed attention, output as the wo input planes (encoder.c:609-638)
+        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
+                             s->gws, s->gws_n, s->gpa));
+        // wo + bias residual (encoder.c:640-644)
+        if (gemmf(s, EPI_RESID, s->gpa, EQ, n, F.wo, ED, L.bo, x, ED, nullptr)) return -1;
+        // FFN RMSNorm -> planes, W1|W3 with SwiGLU into the w2 planes, w2 + bias residual (:646-684)
+        CK(launch_rmsnorm_fplanes(x, n, ED, L.ffn_norm, nullptr, c.enc_eps, s->gpa, nullptr, 0, st));
+        if (gemmf(s, EPI_SWIGLU, s->gpa, ED, n, F.w13, 2 * EH, nullptr, nullptr, EH, s->gpc)) return -1;
+        if (gemmf(s, EPI_RESID, s->gpc, EH, n, F.w2, ED, L.b2, x, ED, nullptr)) return -1;
+    }
+    CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, n, ED, c.enc_eps, st));
+    return 0;
+}
+
 static int enc_skinny_env() {
     static int v = -1;
     if (v < 0) {
@@ -1059,6 +1129,7 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
     hipStream_t st = s->st;
     if (n > ENC_SUB) return set_err("encoder pass of %d rows > %d", n, ENC_SUB);
     if (n <= enc_skinny_rows() && enc_skinny_env() && enc_skinny_ok(c)) return run_encoder_rows_skinny(s, x, n, pos0, rope);
+    if (enc_gemmf_ok(m, n)) return run_encoder_rows_gemmf(s, x, n, pos0, rope);
     for (int l = 0; l < c.enc_layers; l++) {
         const EncLayerD& L = m->enc[l];
         float* Kc = s->ek + (size_t)l * s->ecap * EKV;

@@ -1,0 +1,398 @@
+// vox_hip_gemmf.hip -- k_gemmf: the stream-K MFMA GEMM of the encoder's multi-row chunks.
+//
+// C[m][n] (op)= sum_k x[m][k] W[n][k] (voxtral_kernels.c:197-240: vox_linear_bf16's sgemm
+// on the bf16->f32 weights, M > 1), with x given as bf16 planes hi + mid (+ lo) of the f32
+// rows (the NP-term split of k_gemm2: products with the exact bf16 weights are exact, the
+// planes carry x to ~2^-16 (NP = 2) or exactly (NP = 3)) and both operands in the
+// fragment-major layout of k_frag_pack / frag_at: every 1 KiB of either is one
+// v_mfma_f32_16x16x32_bf16 operand fragment (16 rows x 32 k, lane-linear).
+//
+// Block = 4 waves, tile = RB row blocks of 16 x 4 NG column groups of 16; wave w owns column
+// groups w NG .. w NG + NG - 1 against every row block (W fragments are per wave, the planes
+// are shared).  K runs in 64-deep stages:
+//   * planes: global_load_lds (LDS-DMA, no VGPRs) into a 3-slot LDS ring, 2 stages ahead;
+//     each 1 KiB chunk lands lane-linear and is read back by one conflict-free ds_read_b128;
+//   * weights: straight to VGPRs through a buffer descriptor, a 3-deep register ring, 2
+//     stages ahead;
+//   * one counted s_waitcnt vmcnt + one raw s_barrier per stage (the barrier retires the
+//     stage's DMA for every wave and frees the slot the next DMA overwrites).
+// Work = tiles x stages, split evenly over one block per CU (stream-K: M = 677 has 288 QKV
+// tiles, N = 1280 only 60, so a fixed tile grid leaves CUs idle or needs a split-K reduce
+// kernel).  A block walks its unit range in order; a tile whose stages span several blocks
+// is finished by the block holding its stage 0 -- it reaches that tile at the END of its
+// range, when the blocks holding the tile's later stages (at the START of theirs) have long
+// published their partial tiles: write-through (sc1) stores, every wave's vmcnt drain, a
+// barrier, one relaxed agent-scope flag store of the launch epoch (MI355X_MICROARCH.md
+// "Valid forms", row 1).  The owner polls the flag from one lane (bounded), reads the
+// partial with sc1 loads and adds the partials in block order, then runs the epilogue.  A
+// wait that times out (another kernel holding the CUs the publishing block needs) makes the
+// owner compute that stage range itself: the same code and summation order, the same bits.
+#include "vox_hip_internal.h"
+#include "vox_hip_dev.h"
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+namespace vox {
+
+#ifndef VOX_GF_DIAG
+#define VOX_GF_DIAG 0  // tools/kbench diagnostics only: 1 = no MFMA, 2 = no DMA (stale LDS)
+#endif
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void g_void_t;
+
+// s_waitcnt with only the vector-memory counter bounded (gfx9 encoding: vmcnt [3:0] and
+// [15:14], expcnt [6:4] = 7, lgkmcnt [11:8] = 15: no wait on those)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+struct GemmfArgs {
+    const uint16_t* xs;  // planes [rb][3][16][K] (frag_at)
+    int K, M;
+    const uint8_t* W;    // fragment-major bf16 [N / 16][K / 64][2][1 KiB]
+    int N;
+    const float* bias;   // [N] or null
+    float* C;            // f32 output [M][ldc] (SWIGLU: [M][N / 2]) unless xo
+    int ldc;
+    uint16_t* xo;        // SWIGLU: the gate rows as planes [rb][3][16][N / 2] (the w2 input)
+    float* ws;           // [G][4 waves x RB x NG x 64 lanes x 4] partial tiles: slot b = block b's
+    int* flags;          // [G] epoch of the partial tile block b published
+    int epoch;
+    int S, NT, T;        // K stages, column tiles, tiles
+    long long U;         // T * S work units
+};
+
+constexpr int GF_TIMEOUT_TICKS = 5000;  // s_memrealtime ticks (100 MHz): 50 us of waiting
+
+// NWV = 4 WR waves: wave w takes column slot w % 4 (NG groups) and row share w / 4 (RB / WR
+// row blocks); with WR = 2 two waves share each SIMD, so one's fragment reads overlap the
+// other's MFMAs
+template <int NP, int RB, int NG, int WR>
+struct GfCfg {
+    static constexpr int NWV = 4 * WR;              // waves per block
+    static constexpr int RBW = RB / WR;             // row blocks per wave
+    static constexpr int CH = RB * NP * 2;          // 1 KiB plane chunks per stage
+    static constexpr int CW = 4 * NG * 2;           // 1 KiB weight chunks per stage (4 column slots)
+    static constexpr int NA = CH / NWV;             // plane chunks per wave
+    static constexpr int NB = CW / NWV;             // weight chunks per wave
+    static constexpr int SLOT = (CH + CW) * 512;    // bf16 elements per LDS slot: planes, then weights
+    static_assert(CH % NWV == 0 && CW % NWV == 0 && RB % WR == 0, "chunks must split over the waves");
+};
+
+// one stage's loads into ring slot SL, all LDS-DMA (no VGPR-destination load in the loop:
+// hipcc waits vmcnt(0) at the use of one, which would drain the DMA ring every stage)
+template <int NP, int RB, int NG, int WR, int SL>
+__device__ __forceinline__ void gf_issue(const uint16_t* xb, size_t plane, const uint8_t* wt, int KB, int s,
+                                         uint16_t* lds, int wave, int lane) {
+    using C = GfCfg<NP, RB, NG, WR>;
+    if (VOX_GF_DIAG == 2) return;
+    uint16_t* dst = lds + SL * C::SLOT;
+#pragma unroll
+    for (int i = 0; i < C::NA; i++) {
+        const int c = wave + C::NWV * i;  // chunk: row block c / (2 NP), plane (c / 2) % NP, half c % 2
+        const int rb = c / (NP * 2), p = (c >> 1) % NP, t = c & 1;
+        const uint16_t* src = xb + ((size_t)rb * 3 + p) * plane + (size_t)(s * 2 + t) * 512 + lane * 8;
+        __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(dst + c * 512), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < C::NB; i++) {
+        const int j = wave + C::NWV * i;  // weight chunk: column group j / 2 of the tile, half j % 2
+        const uint8_t* src = wt + ((size_t)(j >> 1) * KB + s) * 2048 + (j & 1) * 1024 + lane * 16;
+        __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(dst + (C::CH + j) * 512), 16, 0, 0);
+    }
+}
+
+// the MFMAs of the stage in ring slot SL (every row block of the wave's share: rows past M
+// are computed and discarded, which keeps the fragment reads and MFMAs one branch-free
+// block).  All fragments are read before the MFMAs (hipcc otherwise sinks each read to its
+// first use and waits on it there; the partner wave on the SIMD covers the read phase).
+template <int NP, int RB, int NG, int WR, int SL>
+__device__ __forceinline__ void gf_mma(const uint16_t* lds, int wave, int lane, f32x4 (&acc)[RB / WR][NG]) {
+    using C = GfCfg<NP, RB, NG, WR>;
+    const uint16_t* src = lds + SL * C::SLOT;
+    const int wc = wave & 3, r0 = (wave >> 2) * C::RBW;
+    bf16x8 wf[2][NG], xf[2][C::RBW][NP];
+    auto rd = [&](int t) {
+#pragma unroll
+        for (int g = 0; g < NG; g++)
+            wf[t][g] = *reinterpret_cast<const bf16x8*>(src + (C::CH + (wc * NG + g) * 2 + t) * 512 + lane * 8);
+#pragma unroll
+        for (int i = 0; i < C::RBW; i++)
+#pragma unroll
+            for (int p = 0; p < NP; p++)
+                xf[t][i][p] = *reinterpret_cast<const bf16x8*>(src + (((r0 + i) * NP + p) * 2 + t) * 512 + lane * 8);
+    };
+    auto mm = [&](int t) {
+        if (VOX_GF_DIAG == 1) {
+            acc[0][0][0] += __builtin_bit_cast(float, (uint32_t)xf[t][0][0][0] & 0x3f00u);  // keep the reads live
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < C::RBW; i++)
+#pragma unroll
+            for (int p = 0; p < NP; p++)
+#pragma unroll
+                for (int g = 0; g < NG; g++)
+                    acc[i][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][g], xf[t][i][p], acc[i][g], 0, 0, 0);
+    };
+    // order pinned by sched barriers (hipcc otherwise sinks each read to its first use and
+    // waits there): the second half's reads go out before the first half's MFMAs, which then
+    // wait only for their own reads (a partial lgkmcnt: <= 15 reads per half)
+    rd(0);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(1);
+}
+
+// stages [s0, s1) of tile (mt, nt) accumulated into acc.
+// Stage s0 + 3 i + j uses ring slot j (compile-time LDS indices); stage s + 2 is issued at
+// stage s, after the barrier that retired stage s - 1's reads of its slot.
+template <int NP, int RB, int NG, int WR>
+__device__ __forceinline__ void gf_stages(const GemmfArgs& a, uint16_t* lds, int mt, int nt, int s0, int s1,
+                                          f32x4 (&acc)[RB / WR][NG]) {
+    using C = GfCfg<NP, RB, NG, WR>;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int KB = a.K >> 6;
+    const size_t plane = (size_t)SK_ROWS * a.K;                 // elements per plane of a row block
+    const uint16_t* xb = a.xs + (size_t)(mt * RB) * 3 * plane;  // this row tile's planes
+    const uint8_t* wt = a.W + (size_t)nt * 4 * NG * KB * 2048;  // this column tile's weight groups
+    gf_issue<NP, RB, NG, WR, 0>(xb, plane, wt, KB, s0, lds, wave, lane);
+    if (s0 + 1 < s1) gf_issue<NP, RB, NG, WR, 1>(xb, plane, wt, KB, s0 + 1, lds, wave, lane);
+#define GF_STAGE(J)                                                                                                 \
+    if (s + J < s1) {                                                                                               \
+        /* stage s + J landed for this wave (the next stage's loads may stay in flight) */                         \
+        if (VOX_GF_DIAG == 2) {                                                                                     \
+        } else if (s + J + 1 < s1) wait_vm<C::NA + C::NB>();                                                        \
+        else wait_vm<0>();                                                                                          \
+        asm volatile("" ::: "memory");                                                                              \
+        __builtin_amdgcn_s_barrier(); /* every wave's DMA landed; slot (J + 2) % 3 is free */                       \
+        asm volatile("" ::: "memory");                                                                              \
+        if (s + J + 2 < s1) gf_issue<NP, RB, NG, WR, (J + 2) % 3>(xb, plane, wt, KB, s + J + 2, lds, wave, lane);   \
+        gf_mma<NP, RB, NG, WR, J>(lds, wave, lane, acc);                                                            \
+    }
+    for (int s = s0; s < s1; s += 3) {
+        GF_STAGE(0)
+        GF_STAGE(1)
+        GF_STAGE(2)
+    }
+#undef GF_STAGE
+    // the ring is reused by the next range: every wave done reading before anyone re-issues
+    __builtin_amdgcn_s_barrier();
+}
+
+__device__ __forceinline__ long long gf_bound(long long U, int G, int b) { return U * b / G; }
+
+template <int EPI, int NP, int RB, int NG, int WR>
+__global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
+    using C = GfCfg<NP, RB, NG, WR>;
+    constexpr int RBW = C::RBW;
+    extern __shared__ __attribute__((aligned(16))) uint16_t gf_lds[];
+    int* s_ok = reinterpret_cast<int*>(gf_lds + 3 * C::SLOT);   // one word past the ring (same array)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wc = wave & 3, r0 = (wave >> 2) * RBW;
+    const int G = gridDim.x, b = blockIdx.x;
+    const long long u0 = gf_bound(a.U, G, b), u1 = gf_bound(a.U, G, b + 1);
+    constexpr int TILE = C::NWV * RBW * NG * 256;  // floats of one partial tile (waves x RBW x NG x 64 lanes x 4)
+    const int rbm = (a.M + 15) >> 4;                // row blocks holding rows
+    const __amdgpu_buffer_rsrc_t Ws = __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, 0x7fffffff, 0x00020000);
+    // this lane's f32x4 of (wave, i, g) in a partial tile
+    auto poff = [&](int slotb, int i, int g) {
+        return (int)(((size_t)slotb * TILE + ((size_t)(wave * RBW + i) * NG + g) * 256 + lane * 4) * 4);
+    };
+    long long u = u0;
+    while (u < u1) {
+        const int t = (int)(u / a.S), s0 = (int)(u % a.S);
+        const int s1 = (int)min((long long)a.S, s0 + (u1 - u));
+        const int mt = t / a.NT, nt = t % a.NT;
+        f32x4 acc[RBW][NG];
+#pragma unroll
+        for (int i = 0; i < RBW; i++)
+#pragma unroll
+            for (int g = 0; g < NG; g++) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, s0, s1, acc);
+        u += s1 - s0;
+        if (s0 > 0) {
+            // a later part of tile t: publish it for the tile's owner (write-through stores,
+            // every wave drains, one flag store)
+#pragma unroll
+            for (int i = 0; i < RBW; i++)
+#pragma unroll
+                for (int g = 0; g < NG; g++)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][g]), Ws, poff(b, i, g), 0, 16);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&a.flags[b], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        // stage 0 is ours: add the later parts in block order, then the epilogue
+        const long long tend = (long long)(t + 1) * a.S;
+        for (int pb = b + 1; pb < G && gf_bound(a.U, G, pb) < tend; pb++) {
+            if (tid == 0) {
+                int ok = 0;
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    if (__hip_atomic_load(&a.flags[pb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch) {
+                        ok = 1;
+                        break;
+                    }
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > GF_TIMEOUT_TICKS) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                *s_ok = ok;
+            }
+            __syncthreads();
+            const int ok = *s_ok;
+            __syncthreads();
+            f32x4 part[RBW][NG];
+            if (ok) {
+#pragma unroll
+                for (int i = 0; i < RBW; i++)
+#pragma unroll
+                    for (int g = 0; g < NG; g++)
+                        part[i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Ws, poff(pb, i, g), 0, 16));
+            } else {
+                // the publishing block has not run: its stage range of this tile, computed here
+#pragma unroll
+                for (int i = 0; i < RBW; i++)
+#pragma unroll
+                    for (int g = 0; g < NG; g++) part[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const int q0 = (int)(gf_bound(a.U, G, pb) - (long long)t * a.S);
+                const int q1 = (int)(min(gf_bound(a.U, G, pb + 1), tend) - (long long)t * a.S);
+                gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, q0, q1, part);
+            }
+#pragma unroll
+            for (int i = 0; i < RBW; i++)
+#pragma unroll
+                for (int g = 0; g < NG; g++) acc[i][g] += part[i][g];
+        }
+        // epilogue: lane holds outputs n = group * 16 + (lane >> 4) * 4 + e for row m = rb * 16 + (lane & 15)
+#pragma unroll
+        for (int i = 0; i < RBW; i++) {
+            const int rb = mt * RB + r0 + i;
+            if (rb >= rbm) break;
+            const int m = rb * 16 + (lane & 15);
+            if (m >= a.M) continue;
+            if (EPI == EPI_SWIGLU) {
+                // groups (2u, 2u + 1) = (w1, w3) rows of 16 hidden units (upload_w13 interleave)
+#pragma unroll
+                for (int g = 0; g < NG; g += 2) {
+                    const int gg = (nt * 4 + wc) * NG + g;  // even global group
+                    const int h0 = (gg >> 1) * 16 + (lane >> 4) * 4;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = silu(acc[i][g][e]) * acc[i][g + 1][e];
+                    if (a.xo) {
+                        const int H = a.N >> 1;
+                        uint32_t hp[2], mp[2], lq[2];
+#pragma unroll
+                        for (int e = 0; e < 4; e += 2) {
+                            uint16_t h_0, m_0, l_0, h_1, m_1, l_1;
+                            split3(v[e], h_0, m_0, l_0);
+                            split3(v[e + 1], h_1, m_1, l_1);
+                            hp[e / 2] = h_0 | ((uint32_t)h_1 << 16);
+                            mp[e / 2] = m_0 | ((uint32_t)m_1 << 16);
+                            lq[e / 2] = l_0 | ((uint32_t)l_1 << 16);
+                        }
+                        *reinterpret_cast<uint2*>(a.xo + frag_at(m, H, 0, h0)) = make_uint2(hp[0], hp[1]);
+                        *reinterpret_cast<uint2*>(a.xo + frag_at(m, H, 1, h0)) = make_uint2(mp[0], mp[1]);
+                        *reinterpret_cast<uint2*>(a.xo + frag_at(m, H, 2, h0)) = make_uint2(lq[0], lq[1]);
+                    } else {
+                        *reinterpret_cast<float4*>(a.C + (size_t)m * a.ldc + h0) = make_float4(v[0], v[1], v[2], v[3]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int g = 0; g < NG; g++) {
+                    const int n = ((nt * 4 + wc) * NG + g) * 16 + (lane >> 4) * 4;
+                    float4 v = make_float4(acc[i][g][0], acc[i][g][1], acc[i][g][2], acc[i][g][3]);
+                    if (a.bias) {
+                        const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
+                        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+                    }
+                    float4* cp = reinterpret_cast<float4*>(a.C + (size_t)m * a.ldc + n);
+                    if (EPI == EPI_RESID) {
+                        const float4 o = *cp;
+                        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+                    } else if (EPI == EPI_GELU) {
+                        v.x = gelu_tanh(v.x); v.y = gelu_tanh(v.y); v.z = gelu_tanh(v.z); v.w = gelu_tanh(v.w);
+                    } else if (EPI == EPI_GELU_ERF) {
+                        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+                    }
+                    *cp = v;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+static int g_cus = 0;
+int g_gemmf_blocks = 0;  // tools/kbench knob: grid size (0 = one block per CU)
+
+template <int EPI, int NP, int RB, int NG, int WR>
+static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
+    using C = GfCfg<NP, RB, NG, WR>;
+    static bool attr = false;
+    const size_t lds = (size_t)3 * C::SLOT * 2 + 16;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemmf<EPI, NP, RB, NG, WR>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_gemmf<EPI, NP, RB, NG, WR>), dim3(G), dim3(256 * WR), lds, st, a);
+    return hipGetLastError();
+}
+
+size_t gemmf_ws_floats(int blocks) { return (size_t)blocks * (8 * 2 * 4 * 256); }
+
+int gemmf_grid() {
+    if (!g_cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_cus <= 0)
+            g_cus = 256;
+    }
+    return g_gemmf_blocks ? g_gemmf_blocks : g_cus;
+}
+
+bool gemmf_ok(int M, int N, int K) { return M > 0 && M <= 1024 && K % 64 == 0 && N % 128 == 0; }
+
+hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
+                        float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
+                        hipStream_t st) {
+    // tiles: 128 x 128 with two planes; 64 x 128 with three (a 3-slot ring of 8 row blocks'
+    // three planes would not fit the 160 KB of LDS); 8 waves (two per SIMD)
+    constexpr int NG = 2, WR = 2;
+    if (!gemmf_ok(M, N, K) || (np != 2 && np != 3) || !ws || !flags) return hipErrorInvalidValue;
+    const int RB = np == 2 ? 8 : 4;
+    GemmfArgs a;
+    a.xs = xs; a.K = K; a.M = M; a.W = static_cast<const uint8_t*>(Wf); a.N = N; a.bias = bias; a.C = C; a.ldc = ldc;
+    a.xo = xo; a.ws = ws; a.flags = flags; a.epoch = epoch;
+    a.S = K / 64;
+    a.NT = N / (64 * NG);
+    a.T = ((M + 16 * RB - 1) / (16 * RB)) * a.NT;
+    a.U = (long long)a.T * a.S;
+    // one block per CU, but every block at least half a tile's stages (and 4): a tile split
+    // over many blocks costs its owner one partial-tile read per extra block
+    const long long minu = std::max(4, (a.S + 1) / 2);
+    int G = gemmf_grid();
+    if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
+    if (gemmf_ws_floats(G) > ws_floats) return hipErrorInvalidValue;
+#define GF_EPI(E)                                                                               \
+    if (epi == E) return np == 2 ? gemmf_launch<E, 2, 8, NG, WR>(a, G, st) : gemmf_launch<E, 3, 4, NG, WR>(a, G, st);
+    GF_EPI(EPI_STORE) GF_EPI(EPI_RESID) GF_EPI(EPI_GELU) GF_EPI(EPI_GELU_ERF) GF_EPI(EPI_SWIGLU)
+#undef GF_EPI
+    return hipErrorInvalidValue;
+}
+
+}  // namespace vox

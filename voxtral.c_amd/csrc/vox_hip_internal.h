@@ -132,6 +132,7 @@ hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, 
 constexpr int SK_ROWS = 16;
 constexpr int SK_MAX_ROWS = 96;  // rows of one skinny launch: up to 6 row blocks of 16
                                  // (planes [rb][3][16][K], slabs [rb][S][16][N])
+constexpr int PLANE_MAX_ROWS = 1024;  // rows of a planes buffer (one encoder pass, ENC_SUB)
 hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hipStream_t st);
 // RMSNorm (+ ada) of nb rows into planes; S > 0: x += the S split slabs of part first
 hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
@@ -185,6 +186,17 @@ int sklx_slices(int N, int K);
 constexpr int SKX_TICKETS = 4 * 1024;
 hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const void* Wf, int N, int nb,
                             const SklFused& f, hipStream_t st);
+// k_gemmf (vox_hip_gemmf.hip): stream-K MFMA GEMM, planes x fragment-major bf16 weights;
+// epi in {STORE, RESID, GELU, GELU_ERF, SWIGLU}; SWIGLU with xo writes the gate rows as
+// planes [rb][3][16][N / 2].  ws: gemmf_ws_floats(gemmf_grid()) floats of partial tiles,
+// flags: gemmf_grid() ints (zeroed once), epoch: > 0, new for every launch on the stream.
+bool gemmf_ok(int M, int N, int K);
+int gemmf_grid();
+size_t gemmf_ws_floats(int blocks);
+hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
+                        float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
+                        hipStream_t st);
+int gemm_planes_np();  // activation planes of the M > 1 GEMMs (2, or 3 with VOX_HIP_GEMM_PLANES=3)
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

@@ -416,6 +416,7 @@ static int gemm_planes() {
     }
     return g_gemm_planes;
 }
+int gemm_planes_np() { return gemm_planes(); }
 
 // ============================================================================
 // Split-K finish: sum the S partial tiles in slice order (deterministic), then the GEMM
@@ -2950,7 +2951,7 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
                              uint16_t* xs) {
     if (M <= 0) return hipSuccess;
     if (hd != 64 && hd != 128) return hipErrorInvalidValue;
-    if (xs && (M > SK_MAX_ROWS || ldo != H * hd)) return hipErrorInvalidValue;
+    if (xs && (M > PLANE_MAX_ROWS || ldo != H * hd)) return hipErrorInvalidValue;
     // 16 queries per block: 32 (each K/V tile of a 25-row streaming chunk read once per head
     // instead of twice) measured slower, 15.7 vs 14.6 us (tools/kbench)
     const int QT = g_attn_qt ? g_attn_qt : 16;
@@ -3287,7 +3288,8 @@ hipError_t launch_frag_pack(const void* src, int N, int K, int q8, void* dst, hi
 
 hipError_t launch_rmsnorm_fplanes(float* x, int nb, int D, const float* w, const float* ada, float eps,
                                   uint16_t* xs, const float* part, int S, hipStream_t st, const float* bias) {
-    if (nb < 1 || nb > SK_MAX_ROWS || D % 64) return hipErrorInvalidValue;
+    // slabs (S > 0) come from k_skl launches of <= SK_MAX_ROWS rows; plain rows: any row set
+    if (nb < 1 || nb > (S > 0 ? SK_MAX_ROWS : PLANE_MAX_ROWS) || D % 64) return hipErrorInvalidValue;
     if (D <= 4 * 512 && D % 4 == 0) {
         hipLaunchKernelGGL(k_resid_rmsnorm_fplanes<4>, dim3(nb), dim3(512), 0, st, x, D, part, S, bias, w, ada, eps, xs);
         LAUNCH_CHECK();
@@ -3324,7 +3326,7 @@ hipError_t launch_slabs_rows(const float* part, int S, int nb, int N, const floa
 }
 
 hipError_t launch_split_fplanes(const float* x, int nb, int K, uint16_t* xs, hipStream_t st) {
-    if (nb < 1 || nb > SK_MAX_ROWS || K % 64) return hipErrorInvalidValue;
+    if (nb < 1 || nb > PLANE_MAX_ROWS || K % 64) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_split_fplanes, dim3((K / 8 + 255) / 256, nb), dim3(256), 0, st, x, K, xs);
     LAUNCH_CHECK();
     return hipSuccess;

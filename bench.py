@@ -67,6 +67,12 @@ def parse():
                          "(vh_sched_*), fed -I 0.5 pieces of the 7 sample lengths cycled, staggered starts")
     ap.add_argument("--serve-seconds", type=float, default=120.0,
                     help="--stagger: audio each stream serves (clips back to back)")
+    ap.add_argument("--kv-fp16", action="store_true",
+                    help="the reference's fp16 decoder KV cache (VOX_DECODER_KV_FP16): IEEE half K/V rings")
+    ap.add_argument("--long-context", type=int, default=0,
+                    help="long-context decode line: prime the decoder KV to this many positions (8192 = the "
+                         "full window), then time --long-steps greedy steps")
+    ap.add_argument("--long-steps", type=int, default=200, help="--long-context: timed steps (>= 100)")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: placeholder host step, same launcher and JSON")
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1,
@@ -294,6 +300,8 @@ def main():
     if args.q8:
         w = quantize_q8(w)
     model = vox_hip.Model(cfg, w)
+    if args.kv_fp16:
+        model.set_kv_fp16(True)  # before any stream exists
     keep_host = d.rank == 0 and d.world == 1 and not args.no_cpu_baseline
     if not keep_host:
         del w
@@ -302,6 +310,8 @@ def main():
     rng = np.random.default_rng(1234 + d.rank)
     mel = rng.uniform(-0.6, 1.4, size=(sum(JFK_CHUNKS), cfg.mel_bins)).astype(np.float32)
     mel_dev = vox_hip.DeviceArray(mel)
+    if args.long_context > 0:
+        return bench_long(args, d, cfg, model, st)
     if args.stagger:
         return bench_serve(args, d, cfg, model, st)
     if args.streams > 1:
@@ -384,7 +394,7 @@ def main():
     # (f32 K and V, positions 39..186 of the jfk schedule), SURVEY.md 8d
     L_avg = (39 + 38 + steps_local // args.steps) / 2.0
     w_tok = (6857687040 // 2) if args.q8 else 6857687040
-    tok_bytes = w_tok + 2 * cfg.dec_layers * cfg.dec_kv_heads * cfg.dec_head_dim * 4 * L_avg
+    tok_bytes = w_tok + kv_bytes_per_position(cfg, args.kv_fp16) * L_avg
     ms_tok = dec_s * 1000.0 / max(1, steps_local)
     out["decoder_roofline"] = {"bound": "hbm", "bytes_per_token": int(tok_bytes),
                                "achieved": round(tok_bytes / (ms_tok * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -401,6 +411,72 @@ def main():
                                "issued_frac": round(gemm_planes() * enc_tf / MFMA_BF16_TFLOPS, 4)}
     if keep_host:
         out["cpu_baseline"] = cpu_baseline(cfg, w, mel, args.cpu_steps, q8=args.q8)
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    mel_dev.free()
+    st.close()
+    model.close()
+
+
+def kv_bytes_per_position(cfg, kv16):
+    """decoder K + V bytes one attention step reads per key position (all layers): 212,992
+    for f32 rings, 106,496 for IEEE half"""
+    return 2 * cfg.dec_layers * cfg.dec_kv_heads * cfg.dec_head_dim * (2 if kv16 else 4)
+
+
+def bench_long(args, d, cfg, model, st):
+    """Long-context decode (north_star's 8192-slot rolling KV): one stream encodes enough
+    synthetic mel for --long-context + --long-steps adapter rows, decodes untimed until the
+    attention spans min(position + 1, window) = --long-context keys, then times --long-steps
+    greedy steps (graph replay, device-held positions, the attention's key-split buckets up
+    to the window's 32).  Per-token bytes = weights + K/V bytes per key x keys."""
+    import vox_hip
+    L, n_time = args.long_context, max(100, args.long_steps)
+    rows = L + n_time + 64
+    rng = np.random.default_rng(4321 + d.rank)
+    mel = rng.uniform(-0.6, 1.4, size=(8 * rows, cfg.mel_bins)).astype(np.float32)
+    mel_dev = vox_hip.DeviceArray(mel)
+    st.reset()
+    for off in range(0, mel.shape[0], 4096):
+        n = min(4096, mel.shape[0] - off)
+        st.encode_mel_device(mel_dev.ptr + off * cfg.mel_bins * 4, n)
+    first = st.decode(max_steps=1, stop_at_eos=False)          # 38-row prefill + first token
+    prompt = st.state()["kv_pos"]
+    prime = max(0, L - prompt)
+    st.decode(max_steps=prime, stop_at_eos=False)
+    st.sync()
+    pos0 = st.state()["kv_pos"]
+    d.barrier()
+    st.sync()
+    t0 = time.perf_counter()
+    ids = st.decode(max_steps=n_time, stop_at_eos=False)
+    st.sync()
+    t1 = time.perf_counter()
+    d.barrier()
+    assert len(ids) == n_time, (len(ids), n_time)
+    wall = d.max(t1 - t0)
+    tok_s = d.sum(len(ids)) / wall
+    keys = min(L, cfg.dec_window)
+    w_tok = (6857687040 // 2) if args.q8 else 6857687040
+    kvb = kv_bytes_per_position(cfg, args.kv_fp16)
+    tok_bytes = w_tok + kvb * keys
+    ms_tok = wall * 1000.0 / len(ids)
+    out = {
+        "metric": "decoder tokens/sec at a full 8192-key window, Voxtral-4B bf16 (long-context decode)",
+        "value": round(tok_s, 2), "unit": "tokens/s", "n_gpus": d.world, "steps": len(ids), "warmup": prime,
+        "ms_per_step": round(ms_tok, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "weights_dtype": "q8" if args.q8 else "bf16",
+        "kv_dtype": "f16 (IEEE half, VOX_DECODER_KV_FP16)" if args.kv_fp16 else "f32",
+        "data": "synthetic (seeded random weights of the exact architecture; synthetic log-mel)",
+        "config": {"workload": f"one stream primed to {L} decoder positions ({prime} untimed greedy steps after the "
+                               f"prompt), then {n_time} timed greedy steps attending {keys} keys each",
+                   "model": "Voxtral-Mini-4B-Realtime", "global_batch": d.world, "seq_len": keys,
+                   "streams_per_gpu": 1, "parallelism": f"replicas x{d.world} (no collective)"},
+        "first_timed_position": pos0, "first_token": int(first[0]) if len(first) else None,
+        "decoder_roofline": {"bound": "hbm", "bytes_per_token": int(tok_bytes), "kv_bytes_per_key": kvb,
+                             "achieved": round(tok_bytes / (ms_tok * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(tok_bytes / (ms_tok * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+    }
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     mel_dev.free()

@@ -97,11 +97,21 @@ void vox_hip_model_free(vox_hip_model_t *m);
 int vox_hip_model_set_delay(vox_hip_model_t *m, int delay_tokens);
 /* ada_scale [dec_layers*dec_dim] as computed on the host (for tests). */
 int vox_hip_model_ada_scale(vox_hip_model_t *m, float *out);
+/* The reference's fp16 decoder KV cache (VOX_DECODER_KV_FP16, voxtral.c:189-190, the Metal
+ * default; voxtral_decoder.c:180-243 allocates the dual-format cache): streams created after
+ * this call keep their decoder K/V rings in IEEE half (stores round to nearest even, all
+ * attention arithmetic f32), halving the ring's HBM bytes per decode step.  Opt-in here: off
+ * unless VOX_DECODER_KV_FP16 is set nonzero at model creation or on = 1 is passed; the
+ * default f32 ring is the CPU reference's (voxtral_decoder.c:232-234).  head_dim 128 only
+ * (Voxtral's); returns 0, or -1 (vox_hip_last_error) for another head_dim. */
+int vox_hip_model_set_kv_fp16(vox_hip_model_t *m, int on);
 
 /* Per-stream device state: encoder/decoder rolling KV, conv-stem tails, adapter buffer,
  * scratch and a HIP stream.  One model serves many streams. */
 vox_hip_stream_t *vox_hip_stream_create(vox_hip_model_t *m);
 void vox_hip_stream_free(vox_hip_stream_t *s);
+/* 1 if the stream's decoder KV rings hold IEEE half (vox_hip_model_set_kv_fp16), else 0 */
+int vox_hip_stream_kv_fp16(const vox_hip_stream_t *s);
 /* stream_reset_full_state (voxtral.c:786-814) / stream_reset_decoder_state (:766-783) */
 int vox_hip_stream_reset(vox_hip_stream_t *s);
 int vox_hip_stream_reset_decoder(vox_hip_stream_t *s);

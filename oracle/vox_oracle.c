@@ -30,6 +30,38 @@ static int g_threads = 1;
 static int g_no_compact = 0;
 void vo_set_no_compaction(int on) { g_no_compact = on; }
 
+/* The fp16 decoder KV cache (VOX_DECODER_KV_FP16, voxtral.c:189-190): the Metal path stores
+ * K (after RoPE) and V as IEEE half and attention reads them back widened to f32
+ * (voxtral_decoder.c:151-178 f16_to_f32; the store is the shader's half(x), round to nearest
+ * even).  Restated as a rounding of every value appended to the decoder cache. */
+static int g_kv_fp16 = 0;
+void vo_set_kv_fp16(int on) { g_kv_fp16 = on; }
+
+/* f32 -> IEEE half (round to nearest even, subnormals kept, overflow to inf) -> f32 */
+static float f16_round(float f) {
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    const uint32_t sign = x & 0x80000000u, ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return f;                 /* inf / nan */
+    if (ax >= 0x477ff000u) {                         /* >= 65520: rounds past 65504 */
+        uint32_t r = sign | 0x7f800000u;
+        float o;
+        memcpy(&o, &r, 4);
+        return o;
+    }
+    if (ax < 0x38800000u) {                          /* below 2^-14: multiples of 2^-24 */
+        float a = fabsf(f) * 16777216.0f;            /* exact (power of two), < 1024 */
+        float q = rintf(a) / 16777216.0f;            /* rintf: nearest even (default mode) */
+        return sign ? -q : q;
+    }
+    uint32_t r = ax + 0xfffu + ((ax >> 13) & 1u);    /* 13 dropped mantissa bits, ties to even */
+    r = (r & ~0x1fffu) | sign;
+    float o;
+    memcpy(&o, &r, 4);
+    return o;
+}
+void vo_f16_round(const float *x, int n, float *out) { for (int i = 0; i < n; i++) out[i] = f16_round(x[i]); }
+
 void vo_set_threads(int n) {
     g_threads = n < 1 ? 1 : n;
     scipy_openblas_set_num_threads(g_threads);
@@ -781,6 +813,8 @@ static void dec_layers(vo_stream_t *s, float *x, int seq, int start_pos, const f
         vo_apply_rope(q, rope, seq, H, hd);
         vo_apply_rope(k, rope, seq, KVH, hd);
         float *kc = s->dk + l * lstride, *vc = s->dv + l * lstride;
+        if (g_kv_fp16)
+            for (size_t i = 0; i < (size_t)seq * kvd; i++) { k[i] = f16_round(k[i]); v[i] = f16_round(v[i]); }
         memcpy(kc + (size_t)start_pos * kvd, k, sizeof(float) * (size_t)seq * kvd);
         memcpy(vc + (size_t)start_pos * kvd, v, sizeof(float) * (size_t)seq * kvd);
         vo_causal_attention(att, q, kc, vc, seq, start_pos + seq, H, KVH, hd, scale,

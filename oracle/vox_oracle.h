@@ -63,6 +63,10 @@ typedef struct vo_stream vo_stream_t;
 void vo_set_threads(int n);
 /* test-only: 1 = grow the KV caches instead of compacting them (invariance tests) */
 void vo_set_no_compaction(int on);
+/* decoder KV appends rounded to IEEE half (the reference's VOX_DECODER_KV_FP16 cache) */
+void vo_set_kv_fp16(int on);
+/* f32 -> half -> f32 of n values (for tests of the rounding) */
+void vo_f16_round(const float *x, int n, float *out);
 void vo_linear_bf16(float *y, const float *x, const uint16_t *W, const float *b,
                     int M, int in_dim, int out_dim);
 /* vox_linear_q8 / vox_linear_nobias_q8 / vox_matmul_t_q8 (voxtral_kernels.c:277-393) */

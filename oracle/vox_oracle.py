@@ -40,6 +40,7 @@ def lib():
         P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         sig = {
             "vo_set_threads": (None, [I]), "vo_set_no_compaction": (None, [I]),
+            "vo_set_kv_fp16": (None, [I]), "vo_f16_round": (None, [fp, I, fp]),
             "vo_linear_bf16": (None, [fp, fp, P, fp, I, I, I]),
             "vo_linear_q8": (None, [fp, fp, P, fp, fp, I, I, I]),
             "vo_rms_norm": (None, [fp, fp, fp, I, I, F]),
@@ -80,6 +81,19 @@ def set_threads(n: int):
 def set_no_compaction(on: bool):
     """test-only: grow the KV caches instead of compacting them (invariance tests)"""
     lib().vo_set_no_compaction(int(on))
+
+
+def set_kv_fp16(on: bool):
+    """the reference's fp16 decoder KV cache (VOX_DECODER_KV_FP16): every decoder K/V append
+    rounded to IEEE half (process-wide, like set_no_compaction)"""
+    lib().vo_set_kv_fp16(int(on))
+
+
+def f16_round(x):
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    out = np.empty_like(x)
+    lib().vo_f16_round(f(x), x.size, f(out))
+    return out
 
 
 # ---- per-op restatements -------------------------------------------------

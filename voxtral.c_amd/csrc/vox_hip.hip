@@ -170,6 +170,7 @@ struct vox_hip_model {
     std::vector<DecFragD> dfrag;   // fragment-major decoder matrices (empty until a batch exists)
     std::vector<DecFragD> efrag;   // fragment-major encoder matrices (empty until a short chunk)
     uint8_t* lm_frag;              // fragment-major LM head (tied embeddings)
+    int kv16;                      // decoder KV rings of streams created from now on in IEEE half
 };
 
 static int upload(void* dst, const void* src, size_t bytes) {
@@ -322,6 +323,12 @@ extern "C" vox_hip_model_t* vox_hip_model_create(const vox_hip_config_t* cfg,
     memset(&m->c, 0, sizeof m->c);
     m->c = *cfg;
     m->delay_tokens = delay_tokens;
+    {
+        // the reference's VOX_DECODER_KV_FP16 (voxtral.c:189-190); opt-in here (unset = f32,
+        // the CPU reference's cache), vox_hip_model_set_kv_fp16 overrides
+        const char* e = getenv("VOX_DECODER_KV_FP16");
+        m->kv16 = (e && atoi(e) != 0 && cfg->dec_head_dim == 128) ? 1 : 0;
+    }
     m->conv0_w = m->conv1_w = nullptr;
     m->ad0 = m->ad1 = m->tok_emb = nullptr;
     m->ad0_s = m->ad1_s = m->tok_emb_s = nullptr;
@@ -435,6 +442,14 @@ extern "C" int vox_hip_model_set_delay(vox_hip_model_t* m, int delay_tokens) {
     return model_update_ada(m);
 }
 
+extern "C" int vox_hip_model_set_kv_fp16(vox_hip_model_t* m, int on) {
+    if (on && m->c.dec_head_dim != 128) return set_err("16-bit decoder KV: head_dim 128 only (got %d)", m->c.dec_head_dim);
+    m->kv16 = on ? 1 : 0;
+    return 0;
+}
+
+extern "C" int vox_hip_stream_kv_fp16(const vox_hip_stream_t* s);
+
 extern "C" int vox_hip_model_ada_scale(vox_hip_model_t* m, float* out) {
     memcpy(out, m->ada_host.data(), m->ada_host.size() * 4);
     return 0;
@@ -454,8 +469,9 @@ struct vox_hip_stream {
     unsigned long long uid;  // unique per stream object ever created (batch graph keys)
     hipStream_t st;
     // rolling KV caches [layers][cap][kv_dim]
-    float *ek, *ev, *dk, *dv;
+    float *ek, *ev, *dk, *dv;   // dk / dv: f32 elements, or IEEE half ones when kv16
     int ecap, dcap;
+    int kv16;
     long long enc_pos;  // next encoder logical position
     // conv stem
     float *mel_p, *mel_tail, *c0_p, *c0_tail, *c0_res, *im2col;
@@ -570,10 +586,12 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     const int EQ = c.enc_heads * c.enc_head_dim;
     s->ecap = c.enc_window + ENC_SUB + 64;
     s->dcap = c.dec_window + DEC_SLACK;
+    s->kv16 = m->kv16;
     TRYH(dalloc(&s->ek, (size_t)c.enc_layers * s->ecap * EKV));
     TRYH(dalloc(&s->ev, (size_t)c.enc_layers * s->ecap * EKV));
-    TRYH(dalloc(&s->dk, (size_t)c.dec_layers * s->dcap * DKV));
-    TRYH(dalloc(&s->dv, (size_t)c.dec_layers * s->dcap * DKV));
+    // (dalloc counts floats: a half ring takes half of them; DKV is even)
+    TRYH(dalloc(&s->dk, (size_t)c.dec_layers * s->dcap * DKV / (s->kv16 ? 2 : 1)));
+    TRYH(dalloc(&s->dv, (size_t)c.dec_layers * s->dcap * DKV / (s->kv16 ? 2 : 1)));
     TRYH(dalloc(&s->mel_tail, (size_t)2 * c.mel_bins));
     TRYH(dalloc(&s->c0_tail, (size_t)2 * c.enc_dim));
     TRYH(dalloc(&s->c0_res, (size_t)c.enc_dim));
@@ -605,6 +623,15 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
         return fail();
     if (vox_hip_stream_reset(s)) return fail();
     return s;
+}
+
+extern "C" int vox_hip_stream_kv_fp16(const vox_hip_stream_t* s) { return s->kv16; }
+
+// layer l's decoder K or V ring (base = s->dk or s->dv) in the stream's element type
+static float* dec_ring(const vox_hip_stream_t* s, float* base, int l) {
+    const vox_hip_config_t& c = s->m->c;
+    const size_t elems = (size_t)l * s->dcap * c.dec_kv_heads * c.dec_head_dim;
+    return reinterpret_cast<float*>(reinterpret_cast<char*>(base) + elems * (s->kv16 ? 2 : 4));
 }
 
 extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
@@ -1264,13 +1291,13 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
     if (n > DEC_SLACK + 1 && pos0 > 0) return set_err("prefill of %d rows on a non-empty cache", n);
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
-        float* Kc = s->dk + (size_t)l * s->dcap * DKV;
-        float* Vc = s->dv + (size_t)l * s->dcap * DKV;
+        float* Kc = dec_ring(s, s->dk, l);
+        float* Vc = dec_ring(s, s->dv, l);
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.attn_norm, nullptr, n, DD, c.dec_eps, st));
         CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, L.sqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st, s->gws, s->gws_n));
-        CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st));
+        CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st, s->kv16));
         CK(launch_attn_tiled(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st,
-                             s->gws, s->gws_n));
+                             s->gws, s->gws_n, nullptr, s->kv16));
         CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, L.so, DQ, n, DD, nullptr, x, DD, st, s->gws, s->gws_n));
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, n, DD, c.dec_eps, st));
         CK(launch_gemm(EPI_SWIGLU, 3, s->xnd, DD, L.w13, L.s13, DD, n, 2 * DH, nullptr, s->gated, DH, st, s->gws, s->gws_n));
@@ -1294,8 +1321,8 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
     hipStream_t st = s->st;
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
-        float* Kc = s->dk + (size_t)l * s->dcap * DKV;
-        float* Vc = s->dv + (size_t)l * s->dcap * DKV;
+        float* Kc = dec_ring(s, s->dk, l);
+        float* Vc = dec_ring(s, s->dv, l);
         GemvArgs a;
         memset(&a, 0, sizeof a);
         // norm -> QKV -> RoPE -> KV append (decoder.c:709-722)
@@ -1304,11 +1331,11 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         a.qd = DQ; a.kvd = DKV; a.hd = hd;
         a.state = state; a.pos = pos;
         a.rope = state ? m->rope_dec : rope_row - (size_t)pos * hd;
-        a.Kc = Kc; a.Vc = Vc; a.cap = s->dcap;
+        a.Kc = Kc; a.Vc = Vc; a.cap = s->dcap; a.kv16 = s->kv16;
         CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
         // attention over the last min(pos+1, window) keys (decoder.c:724-733)
         CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
-                              s->part, s->attd, splits, st));
+                              s->part, s->attd, splits, st, s->kv16));
         // wo + residual (decoder.c:735-740)
         memset(&a, 0, sizeof a);
         a.x = s->attd; a.K = DQ; a.W = L.wo; a.wscale = L.so; a.rows = DD; a.y = s->xd;
@@ -2066,13 +2093,16 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         ap.part[i] = ss[i]->part;
         ap.out[i] = b->att + (size_t)i * DQ;
     }
-    const int cap = ss[0]->dcap;
+    const int cap = ss[0]->dcap, kv16 = ss[0]->kv16;
+    for (int i = 1; i < nb; i++)
+        if (ss[i]->kv16 != kv16) return set_err("batched step over streams of different KV element types");
+    sp.kv16 = kv16;
     const int Sres = skl_splits(DH);  // slabs the previous layer's w2 left for the residual
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         for (int i = 0; i < nb; i++) {
-            sp.Kc[i] = ss[i]->dk + (size_t)l * cap * DKV;
-            sp.Vc[i] = ss[i]->dv + (size_t)l * cap * DKV;
+            sp.Kc[i] = dec_ring(ss[i], ss[i]->dk, l);
+            sp.Vc[i] = dec_ring(ss[i], ss[i]->dv, l);
             ap.Kc[i] = sp.Kc[i];
             ap.Vc[i] = sp.Vc[i];
         }
@@ -2087,10 +2117,10 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
             // combine kernel past 256 keys)
             AttnFuse af;
             af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
-            CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st));
+            CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
         } else {
             CK(launch_rope_kv_batch(b->part, skl_splits(DD), nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
-            CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st));
+            CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
             CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
         }
         CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
@@ -2166,6 +2196,8 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
     const int D = c.dec_dim;
     for (int i = 0; i < n; i++) {
         if (!streams[i] || streams[i]->m != m) return set_err("batch streams must share the batch's model");
+        if (streams[i]->kv16 != streams[0]->kv16)
+            return set_err("batch streams must share the decoder KV element type (vox_hip_model_set_kv_fp16)");
         for (int j = 0; j < i; j++)
             if (streams[j] == streams[i]) return set_err("stream listed twice in a batch");
         counts_out[i] = 0;

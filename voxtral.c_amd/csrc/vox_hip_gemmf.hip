@@ -108,54 +108,59 @@ __device__ __forceinline__ void gf_issue(const uint16_t* xb, size_t plane, const
     }
 }
 
-// the MFMAs of the stage in ring slot SL (every row block of the wave's share: rows past M
-// are computed and discarded, which keeps the fragment reads and MFMAs one branch-free
-// block).  All fragments are read before the MFMAs (hipcc otherwise sinks each read to its
-// first use and waits on it there; the partner wave on the SIMD covers the read phase).
-template <int NP, int RB, int NG, int WR, int SL>
-__device__ __forceinline__ void gf_mma(const uint16_t* lds, int wave, int lane, f32x4 (&acc)[RB / WR][NG]) {
+// The fragments of one half stage (32 of the 64 k) in registers (every row block of the
+// wave's share: rows past M are computed and discarded, which keeps the reads and MFMAs
+// branch-free).
+template <int NP, int RB, int NG, int WR>
+struct GfHalf {
+    bf16x8 w[NG];
+    bf16x8 x[RB / WR][NP];
+};
+
+// read half T of ring slot SL's fragments (10 ds_read_b128 for 128 x 128 tiles, two planes)
+template <int NP, int RB, int NG, int WR, int SL, int T>
+__device__ __forceinline__ void gf_read(const uint16_t* lds, int wave, int lane, GfHalf<NP, RB, NG, WR>& f) {
     using C = GfCfg<NP, RB, NG, WR>;
     const uint16_t* src = lds + SL * C::SLOT;
     const int wc = wave & 3, r0 = (wave >> 2) * C::RBW;
-    bf16x8 wf[2][NG], xf[2][C::RBW][NP];
-    auto rd = [&](int t) {
 #pragma unroll
-        for (int g = 0; g < NG; g++)
-            wf[t][g] = *reinterpret_cast<const bf16x8*>(src + (C::CH + (wc * NG + g) * 2 + t) * 512 + lane * 8);
+    for (int g = 0; g < NG; g++)
+        f.w[g] = *reinterpret_cast<const bf16x8*>(src + (C::CH + (wc * NG + g) * 2 + T) * 512 + lane * 8);
 #pragma unroll
-        for (int i = 0; i < C::RBW; i++)
+    for (int i = 0; i < C::RBW; i++)
 #pragma unroll
-            for (int p = 0; p < NP; p++)
-                xf[t][i][p] = *reinterpret_cast<const bf16x8*>(src + (((r0 + i) * NP + p) * 2 + t) * 512 + lane * 8);
-    };
-    auto mm = [&](int t) {
-        if (VOX_GF_DIAG == 1) {
-            acc[0][0][0] += __builtin_bit_cast(float, (uint32_t)xf[t][0][0][0] & 0x3f00u);  // keep the reads live
-            return;
-        }
-#pragma unroll
-        for (int i = 0; i < C::RBW; i++)
-#pragma unroll
-            for (int p = 0; p < NP; p++)
-#pragma unroll
-                for (int g = 0; g < NG; g++)
-                    acc[i][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][g], xf[t][i][p], acc[i][g], 0, 0, 0);
-    };
-    // order pinned by sched barriers (hipcc otherwise sinks each read to its first use and
-    // waits there): the second half's reads go out before the first half's MFMAs, which then
-    // wait only for their own reads (a partial lgkmcnt: <= 15 reads per half)
-    rd(0);
-    __builtin_amdgcn_sched_barrier(0);
-    rd(1);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(0);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(1);
+        for (int p = 0; p < NP; p++)
+            f.x[i][p] = *reinterpret_cast<const bf16x8*>(src + (((r0 + i) * NP + p) * 2 + T) * 512 + lane * 8);
 }
 
-// stages [s0, s1) of tile (mt, nt) accumulated into acc.
-// Stage s0 + 3 i + j uses ring slot j (compile-time LDS indices); stage s + 2 is issued at
-// stage s, after the barrier that retired stage s - 1's reads of its slot.
+template <int NP, int RB, int NG, int WR>
+__device__ __forceinline__ void gf_mma(const GfHalf<NP, RB, NG, WR>& f, f32x4 (&acc)[RB / WR][NG]) {
+    if (VOX_GF_DIAG == 1) {
+        acc[0][0][0] += __builtin_bit_cast(float, (uint32_t)f.x[0][0][0] & 0x3f00u);  // keep the reads live
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < RB / WR; i++)
+#pragma unroll
+        for (int p = 0; p < NP; p++)
+#pragma unroll
+            for (int g = 0; g < NG; g++)
+                acc[i][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[g], f.x[i][p], acc[i][g], 0, 0, 0);
+}
+
+// lgkmcnt(0) only (vmcnt 63, expcnt 7: no wait on those)
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4)); }
+
+// stages [s0, s1) of tile (mt, nt) accumulated into acc, software-pipelined by half stages:
+//   LDS ring of 3 slots (stage x in slot (x - s0) % 3), DMA three stages ahead;
+//   while the MFMAs of one half stage run, the wave reads the next half stage's fragments
+//   (H0 = k 0..31, H1 = k 32..63 of a stage), so within the wave the matrix pipe and the LDS
+//   reads overlap instead of alternating.
+// Iteration s (H0 of stage s already in registers):
+//   read H1(s) | MFMAs H0(s) | lgkmcnt(0)
+//   wait for stage s + 1's DMA (stage s + 2's may stay in flight) -> barrier (every wave's DMA
+//   landed; every wave done reading stage s's slot) -> DMA stage s + 3 into stage s's slot ->
+//   read H0(s + 1) | MFMAs H1(s) | lgkmcnt(0)
 template <int NP, int RB, int NG, int WR>
 __device__ __forceinline__ void gf_stages(const GemmfArgs& a, uint16_t* lds, int mt, int nt, int s0, int s1,
                                           f32x4 (&acc)[RB / WR][NG]) {
@@ -165,19 +170,41 @@ __device__ __forceinline__ void gf_stages(const GemmfArgs& a, uint16_t* lds, int
     const size_t plane = (size_t)SK_ROWS * a.K;                 // elements per plane of a row block
     const uint16_t* xb = a.xs + (size_t)(mt * RB) * 3 * plane;  // this row tile's planes
     const uint8_t* wt = a.W + (size_t)nt * 4 * NG * KB * 2048;  // this column tile's weight groups
+    GfHalf<NP, RB, NG, WR> H0, H1;
     gf_issue<NP, RB, NG, WR, 0>(xb, plane, wt, KB, s0, lds, wave, lane);
     if (s0 + 1 < s1) gf_issue<NP, RB, NG, WR, 1>(xb, plane, wt, KB, s0 + 1, lds, wave, lane);
-#define GF_STAGE(J)                                                                                                 \
-    if (s + J < s1) {                                                                                               \
-        /* stage s + J landed for this wave (the next stage's loads may stay in flight) */                         \
-        if (VOX_GF_DIAG == 2) {                                                                                     \
-        } else if (s + J + 1 < s1) wait_vm<C::NA + C::NB>();                                                        \
-        else wait_vm<0>();                                                                                          \
-        asm volatile("" ::: "memory");                                                                              \
-        __builtin_amdgcn_s_barrier(); /* every wave's DMA landed; slot (J + 2) % 3 is free */                       \
-        asm volatile("" ::: "memory");                                                                              \
-        if (s + J + 2 < s1) gf_issue<NP, RB, NG, WR, (J + 2) % 3>(xb, plane, wt, KB, s + J + 2, lds, wave, lane);   \
-        gf_mma<NP, RB, NG, WR, J>(lds, wave, lane, acc);                                                            \
+    if (s0 + 2 < s1) gf_issue<NP, RB, NG, WR, 2>(xb, plane, wt, KB, s0 + 2, lds, wave, lane);
+    // stage s0's DMA landed (stages s0 + 1, s0 + 2 may stay in flight)
+    if (VOX_GF_DIAG == 2) {
+    } else if (s0 + 2 < s1) wait_vm<2 * (C::NA + C::NB)>();
+    else if (s0 + 1 < s1) wait_vm<C::NA + C::NB>();
+    else wait_vm<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    gf_read<NP, RB, NG, WR, 0, 0>(lds, wave, lane, H0);
+    wait_lgkm0();
+#define GF_STAGE(J)                                                                                              \
+    if (s + J < s1) {                                                                                            \
+        gf_read<NP, RB, NG, WR, J, 1>(lds, wave, lane, H1);                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                                       \
+        gf_mma<NP, RB, NG, WR>(H0, acc);                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                                       \
+        wait_lgkm0();                                                                                            \
+        if (s + J + 1 < s1) {                                                                                    \
+            if (VOX_GF_DIAG == 2) {                                                                              \
+            } else if (s + J + 2 < s1) wait_vm<C::NA + C::NB>();                                                 \
+            else wait_vm<0>();                                                                                   \
+            asm volatile("" ::: "memory");                                                                       \
+            __builtin_amdgcn_s_barrier();                                                                        \
+            asm volatile("" ::: "memory");                                                                       \
+            if (s + J + 3 < s1) gf_issue<NP, RB, NG, WR, J>(xb, plane, wt, KB, s + J + 3, lds, wave, lane);      \
+            gf_read<NP, RB, NG, WR, (J + 1) % 3, 0>(lds, wave, lane, H0);                                        \
+        }                                                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                                       \
+        gf_mma<NP, RB, NG, WR>(H1, acc);                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                                       \
+        wait_lgkm0();                                                                                            \
     }
     for (int s = s0; s < s1; s += 3) {
         GF_STAGE(0)
@@ -337,6 +364,8 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
 // ---------------------------------------------------------------------------
 static int g_cus = 0;
 int g_gemmf_blocks = 0;  // tools/kbench knob: grid size (0 = one block per CU)
+int g_gemmf_rb = 0;      // tools/kbench knob: row blocks per tile with two planes (0 = by shape; 4 or 8)
+int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
 
 template <int EPI, int NP, int RB, int NG, int WR>
 static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
@@ -373,8 +402,13 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     // tiles: 128 x 128 with two planes; 64 x 128 with three (a 3-slot ring of 8 row blocks'
     // three planes would not fit the 160 KB of LDS); 8 waves (two per SIMD)
     constexpr int NG = 2, WR = 2;
-    if (!gemmf_ok(M, N, K) || (np != 2 && np != 3) || !ws || !flags) return hipErrorInvalidValue;
-    const int RB = np == 2 ? 8 : 4;
+    if (!gemmf_ok(M, N, K) || (np != 2 && np != 3) || !ws || !flags || (g_gemmf_rb && g_gemmf_rb != 4 && g_gemmf_rb != 8))
+        return hipErrorInvalidValue;
+    // two planes: 128-row tiles while they alone give every CU a tile; narrower outputs (the
+    // N = 1280 wo / W2 passes: 10 column tiles) take 64-row tiles -- a stream-K tile split over
+    // many blocks costs more than the lower weight reuse (kbench, profiles/r3_gemmf_sweep.txt)
+    const int t8 = ((M + 127) / 128) * (N / (64 * NG));
+    const int RB = np == 3 ? 4 : g_gemmf_rb ? g_gemmf_rb : (t8 >= gemmf_grid() ? 8 : 4);
     GemmfArgs a;
     a.xs = xs; a.K = K; a.M = M; a.W = static_cast<const uint8_t*>(Wf); a.N = N; a.bias = bias; a.C = C; a.ldc = ldc;
     a.xo = xo; a.ws = ws; a.flags = flags; a.epoch = epoch;
@@ -384,12 +418,14 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     a.U = (long long)a.T * a.S;
     // one block per CU, but every block at least half a tile's stages (and 4): a tile split
     // over many blocks costs its owner one partial-tile read per extra block
-    const long long minu = std::max(4, (a.S + 1) / 2);
+    const long long minu = g_gemmf_minu ? g_gemmf_minu : std::max(4, (a.S + 1) / 2);
     int G = gemmf_grid();
     if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
     if (gemmf_ws_floats(G) > ws_floats) return hipErrorInvalidValue;
 #define GF_EPI(E)                                                                               \
-    if (epi == E) return np == 2 ? gemmf_launch<E, 2, 8, NG, WR>(a, G, st) : gemmf_launch<E, 3, 4, NG, WR>(a, G, st);
+    if (epi == E)                                                                               \
+        return np == 3 ? gemmf_launch<E, 3, 4, NG, WR>(a, G, st)                                \
+               : RB == 8 ? gemmf_launch<E, 2, 8, NG, WR>(a, G, st) : gemmf_launch<E, 2, 4, NG, WR>(a, G, st);
     GF_EPI(EPI_STORE) GF_EPI(EPI_RESID) GF_EPI(EPI_GELU) GF_EPI(EPI_GELU_ERF) GF_EPI(EPI_SWIGLU)
 #undef GF_EPI
     return hipErrorInvalidValue;

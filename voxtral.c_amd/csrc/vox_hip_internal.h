@@ -31,9 +31,10 @@ struct GemvArgs {
     const float* rope;     // rope table [pos][hd]
     const int* state;      // device state (state[0] = logical position) or null
     int pos;               // logical position when state == null
-    float* Kc;
+    float* Kc;             // decoder ring (f32, or IEEE half when kv16)
     float* Vc;
     int cap;
+    int kv16 = 0;
     // EPI_LOGITS(_ALT)
     float* part_val;
     int* part_idx;
@@ -50,6 +51,8 @@ struct AttnPtrs {
     float* part[VOX_MAX_BATCH];
     float* out[VOX_MAX_BATCH];
 };
+// Kc / Vc of the decoder rings point at f32 elements, or at IEEE half ones in the 16-bit
+// mode (the kv16 argument of the launchers, VOX_DECODER_KV_FP16)
 
 // batched decode attention with the QKV epilogue folded in (k_attn_decode<.., FUSE = 1>):
 // RoPE of q / k and the KV append read the QKV projection's split-K slabs, and the output
@@ -69,6 +72,7 @@ struct StepPtrs {
     int* tokens[VOX_MAX_BATCH];         // the stream's token log (tokens_cap entries)
     const float* adapter[VOX_MAX_BATCH];
     int adapter_rows[VOX_MAX_BATCH];
+    int kv16 = 0;                       // rings of IEEE half elements
 };
 constexpr int ARGB = 64;                // argmax partial blocks per row
 
@@ -84,11 +88,11 @@ hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void*
                        int ldc, hipStream_t st, float* ws = nullptr, size_t ws_elems = 0);
 int gemm_ksplit(int M, int N, int K, size_t ws_elems);
 hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, const float* rope,
-                          int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st);
+                          int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st, int kv16 = 0);
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
                              int k_first, int window, float scale, hipStream_t st, float* ws = nullptr,
-                             size_t ws_elems = 0, uint16_t* xs = nullptr);
+                             size_t ws_elems = 0, uint16_t* xs = nullptr, int kv16 = 0);
 // xs: the output also (or only, through the combine kernel) as fragment-major planes
 // the skinny encoder's QKV slabs (+ bias) -> RoPE'd q rows and the K/V ring slots (one pass)
 hipError_t launch_slabs_rope_kv(const float* part, int S, int M, const float* bias, int qd, int kvd, int hd,
@@ -100,15 +104,15 @@ hipError_t launch_gemv_timed(int pro, int epi, const GemvArgs& a, hipEvent_t sta
 int gemv_occupancy(const void* fn);
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
-                              int KVH, float* part, float* out, int splits, hipStream_t st);
+                              int KVH, float* part, float* out, int splits, hipStream_t st, int kv16 = 0);
 // the same over nb streams at once (device state positions; pointers per stream)
 hipError_t launch_attn_decode_batch(int hd, const AttnPtrs& p, int nb, int cap, int window, float scale,
-                                    int H, int KVH, int splits, hipStream_t st);
+                                    int H, int KVH, int splits, hipStream_t st, int kv16 = 0);
 constexpr int ATT_BLOCK_KEYS = 256;  // keys one decode-attention block covers
 // the batched step's attention: RoPE + KV append from the QKV slabs, output as planes
 // (one block per stream x kv head x 256-key split; splits > 1 adds the combine kernel)
 hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window,
-                                   float scale, int H, int KVH, int splits, hipStream_t st);
+                                   float scale, int H, int KVH, int splits, hipStream_t st, int kv16 = 0);
 
 constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,

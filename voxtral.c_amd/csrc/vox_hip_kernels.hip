@@ -6,6 +6,7 @@
 //                decoder/encoder Q|K|V merged row-wise, W1|W3 interleaved in 16-row groups
 //                (rows 32g..32g+15 = w1[16g..], rows 32g+16..32g+31 = w3[16g..])
 //   KV caches    f32 rolling buffers [cap][kv_heads*head_dim] per layer, slot = pos % cap
+//                (decoder: IEEE half in the opt-in 16-bit mode, VOX_DECODER_KV_FP16)
 //   rope tables  f32 [pos][head_dim/2][2] (cos, sin) computed on the host with the
 //                reference's float powf/cosf/sinf (voxtral_kernels.c:617-629)
 //
@@ -25,6 +26,46 @@
 #include <stdlib.h>
 
 namespace vox {
+
+// ============================================================================
+// Decoder KV element type.  f32 by default (the CPU reference's cache); the opt-in 16-bit
+// mode (VOX_DECODER_KV_FP16, voxtral.c:189-190, voxtral_decoder.c:180-243) stores IEEE half:
+// stores round to nearest even, loads widen to f32, all arithmetic stays f32.  Kernels that
+// read the ring are templated on the element type; the two single-store epilogues (decode
+// QKV GEMV, batched RoPE + append) take it as a uniform runtime flag.
+// ============================================================================
+typedef _Float16 kvh_t;
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+template <class T> __device__ __forceinline__ float4 kv_ld4(const T* p) {
+    if constexpr (sizeof(T) == 4) {
+        return *reinterpret_cast<const float4*>(p);
+    } else {
+        const h16x4 h = *reinterpret_cast<const h16x4*>(p);
+        return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+    }
+}
+template <class T> __device__ __forceinline__ float2 kv_ld2(const T* p) {
+    if constexpr (sizeof(T) == 4) {
+        return *reinterpret_cast<const float2*>(p);
+    } else {
+        const h16x2 h = *reinterpret_cast<const h16x2*>(p);
+        return make_float2((float)h[0], (float)h[1]);
+    }
+}
+template <class T> __device__ __forceinline__ float kv_round(float v) { return (float)(T)v; }
+template <class T> __device__ __forceinline__ void kv_st2(T* p, float a, float b) {
+    if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float2*>(p) = make_float2(a, b);
+    } else {
+        *reinterpret_cast<h16x2*>(p) = h16x2{(T)a, (T)b};
+    }
+}
+// element e of a ring (f32 or half by the flag) written as the pair (a, b) at e, e + 1
+__device__ __forceinline__ void kv_st2_rt(float* base, size_t e, float a, float b, int kv16) {
+    if (kv16) kv_st2(reinterpret_cast<kvh_t*>(base) + e, a, b);
+    else kv_st2(base + e, a, b);
+}
 
 // ============================================================================
 // Row-wise RMSNorm (+ optional ada scale), M>1 paths.  voxtral_kernels.c:475-492,
@@ -462,6 +503,7 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
 // RoPE + KV append for M>1 rows (voxtral_encoder.c:580-607, voxtral_decoder.c:531-541).
 // qkv [M, qd + 2*kvd] -> q [M, qd] roped; K/V ring slots (pos0 + i) % cap.
 // ============================================================================
+template <class KT>
 __global__ __launch_bounds__(256) void k_rope_kv(const float* __restrict__ qkv, int M, int qd,
                                                  int kvd, int hd, const float* __restrict__ rope,
                                                  int pos0, float* __restrict__ q,
@@ -472,8 +514,8 @@ __global__ __launch_bounds__(256) void k_rope_kv(const float* __restrict__ qkv, 
     const float* row = qkv + (size_t)i * ld;
     const float* rp = rope + (size_t)i * hd;  // rope rows for rows i (pos0 + i)
     const int slot = (pos0 + i) % cap;
-    float* kr = Kc + (size_t)slot * kvd;
-    float* vr = Vc + (size_t)slot * kvd;
+    KT* kr = reinterpret_cast<KT*>(Kc) + (size_t)slot * kvd;
+    KT* vr = reinterpret_cast<KT*>(Vc) + (size_t)slot * kvd;
     for (int p = threadIdx.x; p < qd / 2; p += 256) {
         int d = (2 * p) % hd / 2;
         float c = rp[2 * d], s = rp[2 * d + 1];
@@ -485,10 +527,9 @@ __global__ __launch_bounds__(256) void k_rope_kv(const float* __restrict__ qkv, 
         int d = (2 * p) % hd / 2;
         float c = rp[2 * d], s = rp[2 * d + 1];
         float x0 = row[qd + 2 * p], x1 = row[qd + 2 * p + 1];
-        kr[2 * p] = x0 * c - x1 * s;
-        kr[2 * p + 1] = x0 * s + x1 * c;
+        kv_st2(kr + 2 * p, x0 * c - x1 * s, x0 * s + x1 * c);
     }
-    for (int p = threadIdx.x; p < kvd; p += 256) vr[p] = row[qd + kvd + p];
+    for (int p = threadIdx.x; p < kvd / 2; p += 256) kv_st2(vr + 2 * p, row[qd + kvd + 2 * p], row[qd + kvd + 2 * p + 1]);
 }
 
 // ============================================================================
@@ -500,7 +541,7 @@ __global__ __launch_bounds__(256) void k_rope_kv(const float* __restrict__ qkv, 
 // KPL keys of a tile for Q.K and DPT dims for P.V.  K/V tiles of 64 keys staged in LDS;
 // online softmax.
 // ============================================================================
-template <int HD, int QT>
+template <int HD, int QT, class ET = float>
 __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q, int ldq,
                                                     const float* __restrict__ Kc,
                                                     const float* __restrict__ Vc, int cap,
@@ -552,8 +593,8 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
             float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
             if (kp <= kend) {
                 size_t off = (size_t)(kp % cap) * kvd + kvh * HD + c4 * 4;
-                kv = *reinterpret_cast<const float4*>(Kc + off);
-                vv = *reinterpret_cast<const float4*>(Vc + off);
+                kv = kv_ld4(reinterpret_cast<const ET*>(Kc) + off);
+                vv = kv_ld4(reinterpret_cast<const ET*>(Vc) + off);
             }
             *reinterpret_cast<float4*>(&sK[r][c4 * 4]) = kv;
             *reinterpret_cast<float4*>(&sV[r][c4 * 4]) = vv;
@@ -651,7 +692,7 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
 // computes.  The four waves' (o, m, l) meet in LDS at the end.  The VALU kernel staged K / V
 // tiles in LDS and was bound by their reads (160 ds_read_b128 per thread per 64-key tile).
 // ============================================================================
-template <int HD>
+template <int HD, class KT = float>
 __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, int ldq, const float* __restrict__ Kc,
                                                  const float* __restrict__ Vc, int cap, float* __restrict__ O,
                                                  int ldo, int M, int H, int KVH, int q_pos0, int k_first, int window,
@@ -692,18 +733,18 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
     // past kend are clamped to it (their scores are masked)
     float kv[DG], vv[4][NB];
     auto load = [&](int kb, float* kd, float (*vd)[NB]) {
-        const float* kr = Kc + (size_t)(min(kb + j, kend) % cap) * kvd + kvh * HD + g * DG;
+        const KT* kr = reinterpret_cast<const KT*>(Kc) + (size_t)(min(kb + j, kend) % cap) * kvd + kvh * HD + g * DG;
 #pragma unroll
         for (int t = 0; t < DG; t += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(kr + t);
+            const float4 v = kv_ld4(kr + t);
             kd[t] = v.x; kd[t + 1] = v.y; kd[t + 2] = v.z; kd[t + 3] = v.w;
         }
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            const float* vr = Vc + (size_t)(min(kb + 4 * g + c, kend) % cap) * kvd + kvh * HD + NB * j;
+            const KT* vr = reinterpret_cast<const KT*>(Vc) + (size_t)(min(kb + 4 * g + c, kend) % cap) * kvd + kvh * HD + NB * j;
 #pragma unroll
             for (int b = 0; b < NB; b += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(vr + b);
+                const float4 v = kv_ld4(vr + b);
                 vd[c][b] = v.x; vd[c][b + 1] = v.y; vd[c][b + 2] = v.z; vd[c][b + 3] = v.w;
             }
         }
@@ -1141,14 +1182,10 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                         a.y[er0] = o0;
                         a.y[er1] = o1;
                     } else {
-                        float* kr = a.Kc + (size_t)(lp % a.cap) * a.kvd + (er0 - a.qd);
-                        kr[0] = o0;
-                        kr[1] = o1;
+                        kv_st2_rt(a.Kc, (size_t)(lp % a.cap) * a.kvd + (er0 - a.qd), o0, o1, a.kv16);
                     }
                 } else {
-                    float* vr = a.Vc + (size_t)(lp % a.cap) * a.kvd + (er0 - a.qd - a.kvd);
-                    vr[0] = v0;
-                    vr[1] = v1;
+                    kv_st2_rt(a.Vc, (size_t)(lp % a.cap) * a.kvd + (er0 - a.qd - a.kvd), v0, v1, a.kv16);
                 }
             }
         }
@@ -1211,15 +1248,15 @@ constexpr int ATT_LBK = ATT_CH * ATT_LWAVES;  // keys per long-context block
 constexpr int ATT_MIN_BK = 64;      // smallest block (kbench variant): sizes the partials
 constexpr int ATT_MAX_PARTS = 128;  // partials per head the combine kernel merges
 
-template <int HD, int HPB, int DBG = 0, int FUSE = 0, int NWV = ATT_WAVES>
+template <int HD, int HPB, int DBG = 0, int FUSE = 0, int NWV = ATT_WAVES, class KT = float>
 __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int cap, int pos_host,
                                                           int window, float scale, int H, int KVH,
                                                           int maxs, const AttnFuse F = AttnFuse{}) {
     constexpr int NT = NWV * 64, BK = NWV * ATT_CH;
     const int zb = blockIdx.z;  // stream of a batched step (0 for a single stream)
     const float* __restrict__ q = P.q[zb];
-    const float* __restrict__ Kc = P.Kc[zb];
-    const float* __restrict__ Vc = P.Vc[zb];
+    const KT* __restrict__ Kc = reinterpret_cast<const KT*>(P.Kc[zb]);
+    const KT* __restrict__ Vc = reinterpret_cast<const KT*>(P.Vc[zb]);
     const int* __restrict__ state = P.state[zb];
     float* __restrict__ part = P.part[zb];
     float* __restrict__ out = P.out[zb];
@@ -1272,26 +1309,26 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
                 const int key = (lane >> 3) + 8 * (i & 1);
                 int sk = slot0 + (key < kn ? key : 0);
                 sk = sk >= cap ? sk - cap : sk;
-                kv[i] = *reinterpret_cast<const float4*>(Kc + (size_t)sk * kvd + kvh * HD + (i >> 1) * DQ + (lane & 7) * 4);
+                kv[i] = kv_ld4(Kc + (size_t)sk * kvd + kvh * HD + (i >> 1) * DQ + (lane & 7) * 4);
             }
         } else {
             int sk = slot0 + (kk < kn ? kk : 0);
             sk = sk >= cap ? sk - cap : sk;
-            const float4* kr = reinterpret_cast<const float4*>(Kc + (size_t)sk * kvd + kvh * HD + dq * DQ);
+            const KT* kr = Kc + (size_t)sk * kvd + kvh * HD + dq * DQ;
 #pragma unroll
-            for (int i = 0; i < DQ / 4; i++) kv[i] = kr[i];
+            for (int i = 0; i < DQ / 4; i++) kv[i] = kv_ld4(kr + 4 * i);
         }
 #pragma unroll
         for (int k = 0; k < ATT_CH; k++) {
             int sv = slot0 + (k < kn ? k : 0);
             sv = sv >= cap ? sv - cap : sv;
-            const float* vr = Vc + (size_t)sv * kvd + kvh * HD + lane * DPL;
+            const KT* vr = Vc + (size_t)sv * kvd + kvh * HD + lane * DPL;
             if (DPL == 2) {
-                const float2 t = *reinterpret_cast<const float2*>(vr);
+                const float2 t = kv_ld2(vr);
                 vv[k][0] = t.x;
                 vv[k][DPL - 1] = t.y;
             } else {
-                vv[k][0] = vr[0];
+                vv[k][0] = (float)vr[0];
             }
         }
     }
@@ -1320,17 +1357,16 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
                 const float2 xx = psum2(F.qkv, F.S, F.N, zb, col);
                 const float x0 = xx.x, x1 = xx.y;
                 const float c = rp[2 * d], sn = rp[2 * d + 1];
-                const float k0v = x0 * c - x1 * sn, k1v = x0 * sn + x1 * c;
+                // the new key as the cache holds it (rounded in the 16-bit mode)
+                const float k0v = kv_round<KT>(x0 * c - x1 * sn), k1v = kv_round<KT>(x0 * sn + x1 * c);
                 sKn[2 * d] = k0v;
                 sKn[2 * d + 1] = k1v;
-                float* kw = const_cast<float*>(Kc) + slot + 2 * d;
-                kw[0] = k0v;
-                kw[1] = k1v;
+                kv_st2(const_cast<KT*>(Kc) + slot + 2 * d, k0v, k1v);
             } else {
                 const int e = j - nq - HD / 2;
-                const float v = psum(F.qkv, F.S, F.N, zb, qd + kvd + kvh * HD + e);
+                const float v = kv_round<KT>(psum(F.qkv, F.S, F.N, zb, qd + kvd + kvh * HD + e));
                 sVn[e] = v;
-                const_cast<float*>(Vc)[slot + e] = v;
+                const_cast<KT*>(Vc)[slot + e] = (KT)v;
             }
         }
     } else {
@@ -1559,9 +1595,9 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
 // (their slots hold older, finite values or zeros).  Grid: one block per query head, the 4
 // heads of a kv head on one XCD (blocks y, y + 8, ..: the K/V rows go through one L2).
 // ============================================================================
-template <int HD>
-__global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q, const float* __restrict__ Kc,
-                                                     const float* __restrict__ Vc, const int* __restrict__ state,
+template <int HD, class KT = float>
+__global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q, const KT* __restrict__ Kc,
+                                                     const KT* __restrict__ Vc, const int* __restrict__ state,
                                                      int pos_host, float scale, int H, int KVH,
                                                      float* __restrict__ out) {
     static_assert(HD == 128, "k_attn_short: head_dim 128 layout");
@@ -1577,10 +1613,10 @@ __global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q
     float4 kv[DQ / 4];
 #pragma unroll
     for (int i = 0; i < DQ / 4; i++)
-        kv[i] = *reinterpret_cast<const float4*>(Kc + (size_t)(k0 + r + 8 * (i & 1)) * kvd + kvh * HD + (i >> 1) * DQ + c * 4);
+        kv[i] = kv_ld4(Kc + (size_t)(k0 + r + 8 * (i & 1)) * kvd + kvh * HD + (i >> 1) * DQ + c * 4);
     float2 vv[ATT_CH];
 #pragma unroll
-    for (int k = 0; k < ATT_CH; k++) vv[k] = *reinterpret_cast<const float2*>(Vc + (size_t)(k0 + k) * kvd + kvh * HD + lane * DPL);
+    for (int k = 0; k < ATT_CH; k++) vv[k] = kv_ld2(Vc + (size_t)(k0 + k) * kvd + kvh * HD + lane * DPL);
     float4 qv[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) qv[j] = *reinterpret_cast<const float4*>(q + (size_t)h * HD + j * DQ + c * 4);
@@ -1907,9 +1943,7 @@ __global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__
     const int ld = qd + 2 * kvd;
     const int pos = sp.state[i][0];
     const float* rp = rope + (size_t)pos * hd;
-    const int slot = pos % cap;
-    float* kr = sp.Kc[i] + (size_t)slot * kvd;
-    float* vr = sp.Vc[i] + (size_t)slot * kvd;
+    const size_t slot = (size_t)(pos % cap) * kvd;
     const int t0 = blockIdx.y * 256 + threadIdx.x, tn = gridDim.y * 256;
     for (int p = t0; p < qd / 2; p += tn) {
         const int d = (2 * p) % hd / 2;
@@ -1924,13 +1958,11 @@ __global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__
         const float c = rp[2 * d], sn = rp[2 * d + 1];
         const float2 xx = psum2(part, S, ld, i, qd + 2 * p);
         const float x0 = xx.x, x1 = xx.y;
-        kr[2 * p] = x0 * c - x1 * sn;
-        kr[2 * p + 1] = x0 * sn + x1 * c;
+        kv_st2_rt(sp.Kc[i], slot + 2 * p, x0 * c - x1 * sn, x0 * sn + x1 * c, sp.kv16);
     }
     for (int p = t0; p < kvd / 2; p += tn) {
         const float2 xx = psum2(part, S, ld, i, qd + kvd + 2 * p);
-        vr[2 * p] = xx.x;
-        vr[2 * p + 1] = xx.y;
+        kv_st2_rt(sp.Vc[i], slot + 2 * p, xx.x, xx.y, sp.kv16);
     }
 }
 
@@ -2934,9 +2966,13 @@ hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void*
 }
 
 hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, const float* rope,
-                          int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st) {
+                          int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st, int kv16) {
     if (M <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rope_kv, dim3(M), dim3(256), 0, st, qkv, M, qd, kvd, hd, rope, pos0, q, Kc, Vc, cap);
+    if (kvd % 2) return hipErrorInvalidValue;
+    if (kv16)
+        hipLaunchKernelGGL(k_rope_kv<kvh_t>, dim3(M), dim3(256), 0, st, qkv, M, qd, kvd, hd, rope, pos0, q, Kc, Vc, cap);
+    else
+        hipLaunchKernelGGL(k_rope_kv<float>, dim3(M), dim3(256), 0, st, qkv, M, qd, kvd, hd, rope, pos0, q, Kc, Vc, cap);
     LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2948,7 +2984,7 @@ int g_attn_blocks = 0;  // tools/kbench knob: target grid size of the key-range 
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
                              int k_first, int window, float scale, hipStream_t st, float* ws, size_t ws_elems,
-                             uint16_t* xs) {
+                             uint16_t* xs, int kv16) {
     if (M <= 0) return hipSuccess;
     if (hd != 64 && hd != 128) return hipErrorInvalidValue;
     if (xs && (M > PLANE_MAX_ROWS || ldo != H * hd)) return hipErrorInvalidValue;
@@ -2972,7 +3008,12 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
 #define VOX_TILED(HD, QQ)                                                                                       \
     hipLaunchKernelGGL((k_attn_tiled<HD, QQ>), grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, \
                        q_pos0, k_first, window, scale, ns, ws)
-    if (!g_attn_valu && QT == 16) {
+    if (kv16) {
+        // the 16-bit decoder ring (prefill): the MFMA kernel only
+        if (hd != 128 || QT != 16) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_attn_mf<128, kvh_t>), grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH,
+                           q_pos0, k_first, window, scale, ns, ws);
+    } else if (!g_attn_valu && QT == 16) {
         if (hd == 64)
             hipLaunchKernelGGL(k_attn_mf<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
                                k_first, window, scale, ns, ws);
@@ -3123,10 +3164,10 @@ int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 int g_attn_lw = 0;  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
 
 // past 256 keys: blocks of NWV x 16 keys per (kv head, key range), then the combine kernel
-template <int HD, int NWV>
+template <int HD, int NWV, class KT>
 static void attn_long(const AttnPtrs& p, int nb, int cap, int pos_host, int window, float scale, int H, int KVH,
                       int splits, int maxs, hipStream_t st) {
-    hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, NWV>), dim3(splits * (ATT_BK / (NWV * ATT_CH)), KVH, nb),
+    hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, NWV, KT>), dim3(splits * (ATT_BK / (NWV * ATT_CH)), KVH, nb),
                        dim3(NWV * 64), 0, st, p, cap, pos_host, window, scale, H, KVH, maxs);
     hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H, nb), dim3(256), 0, st, p, maxs, pos_host, window, NWV * ATT_CH);
 }
@@ -3135,6 +3176,7 @@ static void attn_long(const AttnPtrs& p, int nb, int cap, int pos_host, int wind
 // step the launch serves).  1: 1024-thread blocks of 256 keys, no combine kernel.  > 1:
 // 512-thread blocks of 128 keys per (kv head, span half) and k_attn_combine -- a 256-key
 // block per CU had read K/V at the per-CU rate (L = 1000: 32 blocks, 12.3 us; now 10.0).
+template <class KT>
 static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int pos_host, int window, float scale,
                               int H, int KVH, int splits, hipStream_t st) {
     const int maxs = attn_maxch(window);
@@ -3145,20 +3187,20 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
     // heads (16 streams: 15.8 -> ~10 us per layer); a single stream needs the 32 blocks
 #define VOX_ATT(HD)                                                                                        \
     if (splits == 1 && nb >= 4) {                                                                         \
-        hipLaunchKernelGGL((k_attn_decode<HD, 4>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, pos_host,  \
-                           window, scale, H, KVH, maxs);                                                   \
+        hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, ATT_WAVES, KT>), dim3(1, KVH, nb), dim3(1024), 0, st, p, \
+                           cap, pos_host, window, scale, H, KVH, maxs);                                    \
     } else if (splits == 1) {                                                                              \
-        hipLaunchKernelGGL((k_attn_decode<HD, 1>), dim3(1, H, nb), dim3(1024), 0, st, p, cap, pos_host,    \
-                           window, scale, H, KVH, maxs);                                                   \
+        hipLaunchKernelGGL((k_attn_decode<HD, 1, 0, 0, ATT_WAVES, KT>), dim3(1, H, nb), dim3(1024), 0, st, p,   \
+                           cap, pos_host, window, scale, H, KVH, maxs);                                    \
     } else if (g_attn_lw == 4 || (g_attn_lw == 2 && splits * 8 <= maxs)) {                                \
-        if (g_attn_lw == 4) attn_long<HD, 4>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st); \
-        else attn_long<HD, 2>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);              \
+        if (g_attn_lw == 4) attn_long<HD, 4, KT>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st); \
+        else attn_long<HD, 2, KT>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);          \
     } else {                                                                                               \
-        attn_long<HD, ATT_LWAVES>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);          \
+        attn_long<HD, ATT_LWAVES, KT>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);      \
     }
     if (hd == 128) {
         VOX_ATT(128)
-    } else if (hd == 64) {
+    } else if (hd == 64 && sizeof(KT) == 4) {
         VOX_ATT(64)
     } else {
         return hipErrorInvalidValue;
@@ -3173,46 +3215,61 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
 int g_attn_short = -1;  // k_attn_short for one stream's contexts <= 256 keys (VOX_HIP_ATT_SHORT=0: off)
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
-                              int KVH, float* part, float* out, int splits, hipStream_t st) {
+                              int KVH, float* part, float* out, int splits, hipStream_t st, int kv16) {
     if (g_attn_short < 0) {
         const char* e = getenv("VOX_HIP_ATT_SHORT");
         g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
     }
     if (g_attn_short && splits == 1 && hd == 128 && window >= ATT_BK && cap >= ATT_BK && H % KVH == 0) {
         // contexts of <= 256 keys (splits == 1) with a window of >= 256: keys = slots 0..lp
-        hipLaunchKernelGGL(k_attn_short<128>, dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host, scale, H, KVH, out);
+        if (kv16)
+            hipLaunchKernelGGL((k_attn_short<128, kvh_t>), dim3(H), dim3(1024), 0, st, q,
+                               reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
+                               scale, H, KVH, out);
+        else
+            hipLaunchKernelGGL((k_attn_short<128, float>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host, scale,
+                               H, KVH, out);
         LAUNCH_CHECK();
         return hipSuccess;
     }
     AttnPtrs p;
     memset(&p, 0, sizeof p);
     p.q[0] = q; p.Kc[0] = Kc; p.Vc[0] = Vc; p.state[0] = state; p.part[0] = part; p.out[0] = out;
-    return attn_launch(hd, p, 1, cap, pos_host, window, scale, H, KVH, splits, st);
+    return kv16 ? attn_launch<kvh_t>(hd, p, 1, cap, pos_host, window, scale, H, KVH, splits, st)
+                : attn_launch<float>(hd, p, 1, cap, pos_host, window, scale, H, KVH, splits, st);
 }
 
 hipError_t launch_attn_decode_batch(int hd, const AttnPtrs& p, int nb, int cap, int window, float scale,
-                                    int H, int KVH, int splits, hipStream_t st) {
-    return attn_launch(hd, p, nb, cap, 0, window, scale, H, KVH, splits, st);
+                                    int H, int KVH, int splits, hipStream_t st, int kv16) {
+    return kv16 ? attn_launch<kvh_t>(hd, p, nb, cap, 0, window, scale, H, KVH, splits, st)
+                : attn_launch<float>(hd, p, nb, cap, 0, window, scale, H, KVH, splits, st);
 }
 
-hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window,
-                                   float scale, int H, int KVH, int splits, hipStream_t st) {
-    const int maxs = attn_maxch(window);
-    if (hd != 128 || H % KVH || H / KVH > 4 || maxs > ATT_MAX_PARTS || splits < 1 || splits > attn_maxsplits(window) ||
-        nb < 1 || nb > VOX_MAX_BATCH || !f.qkv || !f.rope || !f.xs || f.S < 1 || f.N != (H + 2 * KVH) * hd)
-        return hipErrorInvalidValue;
+template <class KT>
+static hipError_t attn_batch_fused(const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window, float scale,
+                                   int H, int KVH, int splits, int maxs, hipStream_t st) {
     if (splits == 1) {
-        hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, 0, window,
-                           scale, H, KVH, maxs, f);
+        hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_WAVES, KT>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, 0,
+                           window, scale, H, KVH, maxs, f);
         LAUNCH_CHECK();
         return hipSuccess;
     }
-    hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_LWAVES>), dim3(splits * (ATT_BK / ATT_LBK), KVH, nb),
+    hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_LWAVES, KT>), dim3(splits * (ATT_BK / ATT_LBK), KVH, nb),
                        dim3(ATT_LWAVES * 64), 0, st, p, cap, 0, window, scale, H, KVH, maxs, f);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(k_attn_combine<128>, dim3(H, nb), dim3(256), 0, st, p, maxs, 0, window, ATT_LBK, f.xs, H);
     LAUNCH_CHECK();
     return hipSuccess;
+}
+
+hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window,
+                                   float scale, int H, int KVH, int splits, hipStream_t st, int kv16) {
+    const int maxs = attn_maxch(window);
+    if (hd != 128 || H % KVH || H / KVH > 4 || maxs > ATT_MAX_PARTS || splits < 1 || splits > attn_maxsplits(window) ||
+        nb < 1 || nb > VOX_MAX_BATCH || !f.qkv || !f.rope || !f.xs || f.S < 1 || f.N != (H + 2 * KVH) * hd)
+        return hipErrorInvalidValue;
+    return kv16 ? attn_batch_fused<kvh_t>(p, f, nb, cap, window, scale, H, KVH, splits, maxs, st)
+                : attn_batch_fused<float>(p, f, nb, cap, window, scale, H, KVH, splits, maxs, st);
 }
 // diagnostic variants for tools/kbench (not used by the engine)
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,

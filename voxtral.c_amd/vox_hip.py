@@ -36,7 +36,8 @@ EXPORTS = [
     "vox_hip_init", "vox_hip_available", "vox_hip_shutdown", "vox_hip_memory_used",
     "vox_hip_last_error", "vox_hip_clear_error", "vox_hip_set_device", "vox_hip_config_voxtral_4b",
     "vox_hip_model_create", "vox_hip_model_free", "vox_hip_model_set_delay",
-    "vox_hip_model_ada_scale", "vox_hip_stream_create", "vox_hip_stream_free",
+    "vox_hip_model_ada_scale", "vox_hip_model_set_kv_fp16", "vox_hip_stream_kv_fp16",
+    "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
     "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode", "vox_hip_batch_read_logits",
@@ -70,6 +71,7 @@ def lib():
         "vox_hip_config_voxtral_4b": (None, [P]),
         "vox_hip_model_create": (P, [P, P, I]), "vox_hip_model_free": (None, [P]),
         "vox_hip_model_set_delay": (I, [P, I]), "vox_hip_model_ada_scale": (I, [P, fp]),
+        "vox_hip_model_set_kv_fp16": (I, [P, I]), "vox_hip_stream_kv_fp16": (I, [P]),
         "vox_hip_stream_create": (P, [P]), "vox_hip_stream_free": (None, [P]),
         "vox_hip_stream_reset": (I, [P]), "vox_hip_stream_reset_decoder": (I, [P]),
         "vox_hip_stream_encode_mel": (I, [P, P, I, I]),
@@ -147,6 +149,12 @@ class Model:
         if lib().vox_hip_model_set_delay(self.h, self.delay_tokens) != 0:
             _err("set_delay")
 
+    def set_kv_fp16(self, on: bool):
+        """VOX_DECODER_KV_FP16 (voxtral.c:189-190): streams created afterwards keep their
+        decoder K/V rings in IEEE half"""
+        if lib().vox_hip_model_set_kv_fp16(self.h, int(on)) != 0:
+            _err("set_kv_fp16")
+
     def ada_scale(self):
         c = self.cfg
         out = np.empty(c.dec_layers * c.dec_dim, np.float32)
@@ -172,6 +180,10 @@ class Stream:
     def reset(self):
         if lib().vox_hip_stream_reset(self.h) != 0:
             _err("reset")
+
+    @property
+    def kv_fp16(self) -> bool:
+        return bool(lib().vox_hip_stream_kv_fp16(self.h))
 
     def encode_mel(self, mel: np.ndarray) -> int:
         mel = np.ascontiguousarray(mel, dtype=np.float32)

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_attn_kvfast; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
     float* Kc = (float*)dmalloc((size_t)cap * DKV * 4, 1);
     float* Vc = (float*)dmalloc((size_t)cap * DKV * 4, 1);
     float* rope = (float*)dmalloc((size_t)16384 * HD * 4, 1);
-    float* part = (float*)dmalloc((size_t)H * 128 * (HD + 2) * 4, 0);
+    float* part = (float*)dmalloc((size_t)H * 128 * (HD + 2) * 4 + 4096, 0);  // + arrival counts
     float* pv = (float*)dmalloc(4096 * 4, 0);
     int* pi = (int*)dmalloc(4096 * 4, 0);
     int* state;
@@ -105,6 +105,47 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attn")) {
+        // long-context decode attention as the decode step sees it: 26 layers' rings (f32:
+        // 1.76 GB, half: 0.88 GB, far past the 256 MB MALL), one launch per layer in turn
+        const int NLd = 26, rcap = 8192 + 64;
+        for (int kv16 : {0, 1}) {
+            const size_t esz = kv16 ? 2 : 4, per = (size_t)rcap * DKV;
+            std::vector<float*> Ks(NLd), Vs(NLd);
+            for (int l = 0; l < NLd; l++) {
+                Ks[l] = (float*)dmalloc(per * esz, 1);
+                Vs[l] = (float*)dmalloc(per * esz, 1);
+            }
+            for (int L : {1024, 2048, 4096, 8192}) {
+                int st4[4] = {L - 1, 0, 0, 0};
+                CK(hipMemcpy(state, st4, 16, hipMemcpyHostToDevice));
+                int splits = 1;
+                while (splits * ATT_BLOCK_KEYS < L) splits *= 2;
+                for (int v : {0, 1, 16}) {
+                    // v: 0 = key-range-major grid, 1 = kv heads of a key range adjacent (default),
+                    // 16 = the same with 256-key blocks of 16 waves
+                    g_attn_kvfast = v != 0;
+                    g_attn_lw = v == 16 ? 16 : 0;
+                    int l = 0;
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "attn decode L=%d %s 26 layers %d-key blocks%s", L, kv16 ? "half" : "f32",
+                             v == 16 ? 256 : 128, g_attn_kvfast ? " kv-fast" : "");
+                    add(nm, timeit([&] {
+                            CK(launch_attn_decode(HD, x, Ks[l % NLd], Vs[l % NLd], rcap, state, 0, 8192, 0.088f, H, KVH,
+                                                  part, y, splits, st, kv16));
+                            l++;
+                        }, 260, st), (double)L * DKV * 2 * esz);
+                }
+                g_attn_lw = 0;
+                g_attn_kvfast = 1;
+            }
+            for (int l = 0; l < NLd; l++) {
+                CK(hipFree(Ks[l]));
+                CK(hipFree(Vs[l]));
+            }
+        }
+        return 0;
+    }
     if (!only_gemmf) {
     add("gemv qkv  (6144x3072, norm+rope)", timeit([&] { gemv(PRO_NORM, EPI_QKV, wqkv[layer++ % NL], D, DQ + 2 * DKV); }, iters, st), (DQ + 2.0 * DKV) * D * 2);
     add("gemv wo   (3072x4096, resid)", timeit([&] { gemv(PRO_NONE, EPI_RESID, wo[layer++ % NL], DQ, D); }, iters, st), (double)D * DQ * 2);

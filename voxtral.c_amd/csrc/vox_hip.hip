@@ -602,7 +602,9 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->att, (size_t)ENC_SUB * EQ));
     TRYH(dalloc(&s->gate, (size_t)ENC_SUB * c.enc_hidden));
     TRYH(dalloc(&s->ad_mid, (size_t)(ENC_SUB / 4 + 4) * c.dec_dim));
-    TRYH(dalloc(&s->part, (size_t)c.dec_heads * attn_maxch(c.dec_window) * (c.dec_head_dim + 2)));
+    // decode-attention partials + one arrival count per kv head after them (zeroed here,
+    // reset by the merging block after every launch)
+    TRYH(dalloc(&s->part, (size_t)c.dec_heads * attn_maxch(c.dec_window) * (c.dec_head_dim + 2) + c.dec_kv_heads));
     TRYH(dalloc(&s->part_alt, (size_t)GEMV_MAX_BLOCKS * ALT_PART));
     s->gws_n = GEMM_WS_ELEMS;
     TRYH(dalloc(&s->gws, s->gws_n));

@@ -102,6 +102,8 @@ const void* gemv_kernel(int pro, int epi, const GemvArgs& a);
 hipError_t launch_gemv_timed(int pro, int epi, const GemvArgs& a, hipEvent_t start, hipEvent_t stop,
                              hipStream_t st);
 int gemv_occupancy(const void* fn);
+// part: H * attn_maxch(window) * (hd + 2) floats of partials, then KVH ints (zeroed before
+// the first launch) that count the split blocks' arrivals
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
                               int KVH, float* part, float* out, int splits, hipStream_t st, int kv16 = 0);

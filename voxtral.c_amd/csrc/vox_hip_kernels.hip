@@ -1235,7 +1235,8 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 // that the 4 blocks of one kv head land on one XCD (blocks b and b+8 share an L2) and read
 // the K/V rows through the same L2.  HPB = 4 (long contexts): one block per kv head and
 // 256-key split, K/V read once.  With one split the block writes the attention output
-// directly; otherwise it writes an (o, m, l) partial and k_attn_combine merges the splits.
+// directly; otherwise it writes an (o, m, l) partial and the last of the split blocks of a
+// kv head to arrive merges them (arrival count past the partials).
 // ============================================================================
 // NWV = waves per block: 16 (256 keys: one block per head covers short contexts, no
 // combine) or 8 (128-key blocks for long contexts: twice the blocks, half the K/V bytes per
@@ -1246,12 +1247,12 @@ constexpr int ATT_BK = ATT_CH * ATT_WAVES;  // keys per short-context block
 constexpr int ATT_LWAVES = 8;   // waves per long-context block (512 threads)
 constexpr int ATT_LBK = ATT_CH * ATT_LWAVES;  // keys per long-context block
 constexpr int ATT_MIN_BK = 64;      // smallest block (kbench variant): sizes the partials
-constexpr int ATT_MAX_PARTS = 128;  // partials per head the combine kernel merges
+constexpr int ATT_MAX_PARTS = 128;  // partials per head the merging block combines
 
 template <int HD, int HPB, int DBG = 0, int FUSE = 0, int NWV = ATT_WAVES, class KT = float>
 __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int cap, int pos_host,
                                                           int window, float scale, int H, int KVH,
-                                                          int maxs, const AttnFuse F = AttnFuse{}) {
+                                                          int maxs, const AttnFuse F = AttnFuse{}, int kvfast = 0) {
     constexpr int NT = NWV * 64, BK = NWV * ATT_CH;
     const int zb = blockIdx.z;  // stream of a batched step (0 for a single stream)
     const float* __restrict__ q = P.q[zb];
@@ -1268,10 +1269,12 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     __shared__ __attribute__((aligned(16))) float sO[NWV][HPB][HD];
     __shared__ __attribute__((aligned(16))) float sKn[FUSE ? HD : 1], sVn[FUSE ? HD : 1];  // the new key's K / V
     const int hpk = H / KVH;
-    const int kvh = HPB == 1 ? (int)blockIdx.y % KVH : (int)blockIdx.y;
+    // kvfast (HPB 4): grid x = key range * KVH + kv head, so the kv heads of one key range (the
+    // 8 slices of the same K/V rows) are neighbouring blocks
+    const int kvh = HPB == 1 ? (int)blockIdx.y % KVH : kvfast ? (int)blockIdx.x % KVH : (int)blockIdx.y;
     const int h0 = HPB == 1 ? kvh * hpk + (int)blockIdx.y / KVH : kvh * hpk;  // first query head
     const int nh = HPB == 1 ? 1 : hpk;  // heads in this block (<= 4)
-    const int sb = blockIdx.x;
+    const int sb = (HPB != 1 && kvfast) ? (int)blockIdx.x / KVH : (int)blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kvd = KVH * HD;
     unsigned long long ts[10];
@@ -1388,7 +1391,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
                 for (int i = 0; i < DQ / 4; i++)
                     if ((i & 1) == (kl >> 3)) kv[i] = *reinterpret_cast<const float4*>(&sKn[(i >> 1) * DQ + (lane & 7) * 4]);
             }
-        } else if (k0 + kk == lp) {
+        } else if (kk == kl) {
 #pragma unroll
             for (int i = 0; i < DQ / 4; i++) kv[i] = *reinterpret_cast<const float4*>(&sKn[dq * DQ + 4 * i]);
         }
@@ -1556,6 +1559,9 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
         }
         return;
     }
+    // partials (S > 1) go out write-through (sc1, like k_gemmf's partial tiles): the block
+    // that merges them may sit on another XCD, behind another L2
+    const __amdgpu_buffer_rsrc_t Pr = __builtin_amdgcn_make_buffer_rsrc(part, 0, 0x7fffffff, 0x00020000);
     for (int e = tid; e < nh * HD; e += NT) {
         const int h = e / HD, d = e % HD;
         float num = 0.f;
@@ -1566,13 +1572,117 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
         if (S == 1) {
             out[(size_t)hh * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
         } else {
-            float* pp = part + ((size_t)hh * maxs + sb) * (HD + 2);
-            pp[d] = num;
+            const int po = (int)(((size_t)hh * maxs + sb) * (HD + 2)) * 4;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(num), Pr, po + d * 4, 0, 16);
             if (d == 0) {
-                pp[HD] = sMax[h];
-                pp[HD + 1] = den;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sMax[h]), Pr, po + HD * 4, 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(den), Pr, po + (HD + 1) * 4, 0, 16);
             }
         }
+    }
+    if (S > 1 && DBG == 0) {
+        // the last of the S blocks of this kv head to finish merges the S partials of its
+        // heads (the former k_attn_combine, one launch and its gap fewer per layer): stores
+        // drained, one arrival count per (stream, kv head) just past the partials, reset by
+        // the merging block for the next launch
+        __shared__ int sLast;
+        __shared__ float sCf[4][ATT_MAX_PARTS];
+        __shared__ float sCden[4];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* cnt = reinterpret_cast<int*>(part + (size_t)H * maxs * (HD + 2)) + kvh;
+        if (tid == 0) sLast = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+        __syncthreads();
+        if (!sLast) return;
+        auto pnum = [&](int h, int k, int d) {
+            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                Pr, (int)(((size_t)(h0 + h) * maxs + k) * (HD + 2) + d) * 4, 0, 16));
+        };
+        // output (h, d) = e of thread tid: its first 32 partial values go out before the merge
+        // factors are known, so partials, maxima and sums share one round trip
+        constexpr int PRE = 32;
+        const bool own = tid < nh * HD;
+        const int he = own ? tid / HD : 0, de = tid % HD;
+        float t0[PRE];
+#pragma unroll
+        for (int j = 0; j < PRE; j++) t0[j] = (own && j < S) ? pnum(he, j, de) : 0.f;
+        // merge factors per head (k_attn_combine's order): f_k = exp(m_k - M), den = the
+        // wave sum of each lane's f_k l_k over k = lane, lane + 64
+        for (int h = wave; h < nh; h += NWV) {
+            const int hh = h0 + h;
+            float mk[2], lk[2], mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int k = lane + 64 * j;
+                const int po = (int)(((size_t)hh * maxs + k) * (HD + 2) + HD) * 4;
+                mk[j] = k < S ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(Pr, po, 0, 16)) : -INFINITY;
+                lk[j] = k < S ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(Pr, po + 4, 0, 16)) : 0.f;
+                mx = fmaxf(mx, mk[j]);
+            }
+            mx = wave_max(mx);
+            float den = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int k = lane + 64 * j;
+                if (k < S) {
+                    const float f = expf(mk[j] - mx);
+                    sCf[h][k] = f;
+                    den = fmaf(f, lk[j], den);
+                }
+            }
+            den = wave_sum(den);
+            if (lane == 0) sCden[h] = den;
+        }
+        __syncthreads();
+        __shared__ __attribute__((aligned(16))) float sRow[FUSE ? 4 : 1][FUSE ? HD : 1];
+        for (int e = tid; e < nh * HD; e += NT) {
+            const int h = e / HD, d = e % HD;
+            float num = 0.f;
+            int k = 0;
+            if (e == tid) {
+#pragma unroll
+                for (int j = 0; j < PRE; j++)
+                    if (j < S) num = fmaf(sCf[h][j], t0[j], num);
+                k = PRE;
+            }
+            // past the preloaded ones: 16 partial loads in flight per step, in block order
+            for (; k + 16 <= S; k += 16) {
+                float t[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) t[j] = pnum(h, k + j, d);
+#pragma unroll
+                for (int j = 0; j < 16; j++) num = fmaf(sCf[h][k + j], t[j], num);
+            }
+            for (; k < S; k++) num = fmaf(sCf[h][k], pnum(h, k, d), num);
+            const float den = sCden[h];
+            const float v = den > 0.f ? num * (1.0f / den) : 0.f;
+            if (FUSE) sRow[h][d] = v;
+            else out[(size_t)(h0 + h) * HD + d] = v;
+        }
+        if (FUSE) {
+            // the attention row of stream zb into the wo input planes, 8 dims per thread
+            __syncthreads();
+            const size_t Pn = (size_t)SK_ROWS * H * HD;
+            for (int e = tid; e < nh * HD / 8; e += NT) {
+                const int h = e / (HD / 8), d0 = (e % (HD / 8)) * 8;
+                uint32_t hp[4], mp[4], lq[4];
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    uint16_t a0, b0, c0, a1, b1, c1;
+                    split3(sRow[h][d0 + i], a0, b0, c0);
+                    split3(sRow[h][d0 + i + 1], a1, b1, c1);
+                    hp[i / 2] = a0 | ((uint32_t)a1 << 16);
+                    mp[i / 2] = b0 | ((uint32_t)b1 << 16);
+                    lq[i / 2] = c0 | ((uint32_t)c1 << 16);
+                }
+                const size_t o = frag_off(zb, (h0 + h) * HD + d0);
+                *reinterpret_cast<uint4*>(F.xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+                *reinterpret_cast<uint4*>(F.xs + Pn + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+                *reinterpret_cast<uint4*>(F.xs + 2 * Pn + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+            }
+        }
+        if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
     }
     if (DBG == 4) {
         ts[5] = __builtin_amdgcn_s_memtime();
@@ -1675,66 +1785,6 @@ __global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q
     }
 }
 
-template <int HD>
-__global__ __launch_bounds__(256) void k_attn_combine(const AttnPtrs ptrs, int maxs, int pos_host, int window, int bk,
-                                                      uint16_t* __restrict__ xs = nullptr, int H = 0) {
-    const float* __restrict__ part = ptrs.part[blockIdx.y];
-    const int* __restrict__ state = ptrs.state[blockIdx.y];
-    float* __restrict__ out = ptrs.out[blockIdx.y];
-    __shared__ float sf[ATT_MAX_PARTS];
-    __shared__ float sden;
-    const int h = blockIdx.x, tid = threadIdx.x;
-    const int lp = state ? state[0] : pos_host;
-    const int L = min(lp + 1, window);
-    const int P = (L + bk - 1) / bk;  // bk: keys per block of the attention launch
-    if (P <= 1) return;  // the attention blocks already wrote the output
-    const float* ph = part + (size_t)h * maxs * (HD + 2);
-    if (tid < 64) {
-        float mx = -INFINITY;
-        for (int i = tid; i < P; i += 64) mx = fmaxf(mx, ph[(size_t)i * (HD + 2) + HD]);
-        mx = wave_max(mx);
-        float den = 0.f;
-        for (int i = tid; i < P; i += 64) {
-            const float f = expf(ph[(size_t)i * (HD + 2) + HD] - mx);
-            sf[i] = f;
-            den = fmaf(f, ph[(size_t)i * (HD + 2) + HD + 1], den);
-        }
-        den = wave_sum(den);
-        if (tid == 0) sden = den;
-    }
-    __syncthreads();
-    if (xs) {
-        // batched step: stream blockIdx.y's row of the wo input planes, 8 dims per thread
-        if (tid < HD / 8) {
-            const int d0 = tid * 8;
-            uint32_t hp[4], mp[4], lq[4];
-            for (int i = 0; i < 8; i += 2) {
-                float v2[2];
-                for (int u = 0; u < 2; u++) {
-                    float num = 0.f;
-                    for (int k = 0; k < P; k++) num = fmaf(sf[k], ph[(size_t)k * (HD + 2) + d0 + i + u], num);
-                    v2[u] = sden > 0.f ? num * (1.0f / sden) : 0.f;
-                }
-                uint16_t a0, b0, c0, a1, b1, c1;
-                split3(v2[0], a0, b0, c0);
-                split3(v2[1], a1, b1, c1);
-                hp[i / 2] = a0 | ((uint32_t)a1 << 16);
-                mp[i / 2] = b0 | ((uint32_t)b1 << 16);
-                lq[i / 2] = c0 | ((uint32_t)c1 << 16);
-            }
-            const size_t Pn = (size_t)SK_ROWS * H * HD, o = frag_off(blockIdx.y, h * HD + d0);
-            *reinterpret_cast<uint4*>(xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
-            *reinterpret_cast<uint4*>(xs + Pn + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
-            *reinterpret_cast<uint4*>(xs + 2 * Pn + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
-        }
-        return;
-    }
-    for (int d = tid; d < HD; d += 256) {
-        float num = 0.f;
-        for (int i = 0; i < P; i++) num = fmaf(sf[i], ph[(size_t)i * (HD + 2) + d], num);
-        out[(size_t)h * HD + d] = sden > 0.f ? num * (1.0f / sden) : 0.f;
-    }
-}
 
 // ============================================================================
 // Step input: x = adapter[gen] + tok_emb[prev] (voxtral.c:1106-1113); the embedding row
@@ -3162,14 +3212,22 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
 int attn_maxch(int window) { return (window + ATT_MIN_BK - 1) / ATT_MIN_BK; }
 int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 int g_attn_lw = 0;  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
+int g_attn_kvfast = 1;  // long-context grid with the kv heads of a key range adjacent (tools/kbench: 0 = off)
 
-// past 256 keys: blocks of NWV x 16 keys per (kv head, key range), then the combine kernel
+// past 256 keys: blocks of NWV x 16 keys per (kv head, key range); the last block of a kv
+// head merges the partials
+// (kv heads of one key range on neighbouring blocks, kvfast: L = 8192 f32 over 26 layers'
+// rings 27.4 -> 22.9 us per layer, tools/kbench VOX_KB_ONLY=attn)
 template <int HD, int NWV, class KT>
 static void attn_long(const AttnPtrs& p, int nb, int cap, int pos_host, int window, float scale, int H, int KVH,
                       int splits, int maxs, hipStream_t st) {
-    hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, NWV, KT>), dim3(splits * (ATT_BK / (NWV * ATT_CH)), KVH, nb),
-                       dim3(NWV * 64), 0, st, p, cap, pos_host, window, scale, H, KVH, maxs);
-    hipLaunchKernelGGL(k_attn_combine<HD>, dim3(H, nb), dim3(256), 0, st, p, maxs, pos_host, window, NWV * ATT_CH);
+    const int nsb = splits * (ATT_BK / (NWV * ATT_CH));  // key-range blocks per kv head
+    if (g_attn_kvfast)
+        hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, NWV, KT>), dim3(nsb * KVH, 1, nb), dim3(NWV * 64), 0, st, p,
+                           cap, pos_host, window, scale, H, KVH, maxs, AttnFuse{}, 1);
+    else
+        hipLaunchKernelGGL((k_attn_decode<HD, 4, 0, 0, NWV, KT>), dim3(nsb, KVH, nb), dim3(NWV * 64), 0, st, p, cap,
+                           pos_host, window, scale, H, KVH, maxs);
 }
 
 // splits = 256-key spans provided per head group (>= the context's ceil(L / 256) for every
@@ -3195,6 +3253,8 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
     } else if (g_attn_lw == 4 || (g_attn_lw == 2 && splits * 8 <= maxs)) {                                \
         if (g_attn_lw == 4) attn_long<HD, 4, KT>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st); \
         else attn_long<HD, 2, KT>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);          \
+    } else if (g_attn_lw == 16) {                                                                          \
+        attn_long<HD, 16, KT>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);              \
     } else {                                                                                               \
         attn_long<HD, ATT_LWAVES, KT>(p, nb, cap, pos_host, window, scale, H, KVH, splits, maxs, st);      \
     }
@@ -3254,10 +3314,8 @@ static hipError_t attn_batch_fused(const AttnPtrs& p, const AttnFuse& f, int nb,
         LAUNCH_CHECK();
         return hipSuccess;
     }
-    hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_LWAVES, KT>), dim3(splits * (ATT_BK / ATT_LBK), KVH, nb),
-                       dim3(ATT_LWAVES * 64), 0, st, p, cap, 0, window, scale, H, KVH, maxs, f);
-    LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_attn_combine<128>, dim3(H, nb), dim3(256), 0, st, p, maxs, 0, window, ATT_LBK, f.xs, H);
+    hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_LWAVES, KT>), dim3(splits * (ATT_BK / ATT_LBK) * KVH, 1, nb),
+                       dim3(ATT_LWAVES * 64), 0, st, p, cap, 0, window, scale, H, KVH, maxs, f, 1);
     LAUNCH_CHECK();
     return hipSuccess;
 }

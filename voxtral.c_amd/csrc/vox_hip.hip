@@ -442,6 +442,13 @@ extern "C" int vox_hip_model_set_delay(vox_hip_model_t* m, int delay_tokens) {
     return model_update_ada(m);
 }
 
+extern "C" int vox_hip_set_gemm_planes(int planes) {
+    if (set_gemm_planes(planes)) return set_err("gemm planes: 2 or 3 (got %d)", planes);
+    return 0;
+}
+
+extern "C" int vox_hip_gemm_planes(void) { return gemm_planes_np(); }
+
 extern "C" int vox_hip_model_set_kv_fp16(vox_hip_model_t* m, int on) {
     if (on && m->c.dec_head_dim != 128) return set_err("16-bit decoder KV: head_dim 128 only (got %d)", m->c.dec_head_dim);
     m->kv16 = on ? 1 : 0;

@@ -203,6 +203,7 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
                         float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
                         hipStream_t st);
 int gemm_planes_np();  // activation planes of the M > 1 GEMMs (2, or 3 with VOX_HIP_GEMM_PLANES=3)
+int set_gemm_planes(int np);  // 2 or 3 (vox_hip_set_gemm_planes); -1 otherwise
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,
                           hipStream_t st);
 hipError_t launch_mel_tail(const float* melp, int n_new, int MB, float* tail, hipStream_t st);

@@ -458,6 +458,11 @@ static int gemm_planes() {
     return g_gemm_planes;
 }
 int gemm_planes_np() { return gemm_planes(); }
+int set_gemm_planes(int np) {
+    if (np != 2 && np != 3) return -1;
+    g_gemm_planes = np;
+    return 0;
+}
 
 // ============================================================================
 // Split-K finish: sum the S partial tiles in slice order (deterministic), then the GEMM

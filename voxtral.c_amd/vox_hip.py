@@ -37,6 +37,7 @@ EXPORTS = [
     "vox_hip_last_error", "vox_hip_clear_error", "vox_hip_set_device", "vox_hip_config_voxtral_4b",
     "vox_hip_model_create", "vox_hip_model_free", "vox_hip_model_set_delay",
     "vox_hip_model_ada_scale", "vox_hip_model_set_kv_fp16", "vox_hip_stream_kv_fp16",
+    "vox_hip_set_gemm_planes", "vox_hip_gemm_planes",
     "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
@@ -72,6 +73,7 @@ def lib():
         "vox_hip_model_create": (P, [P, P, I]), "vox_hip_model_free": (None, [P]),
         "vox_hip_model_set_delay": (I, [P, I]), "vox_hip_model_ada_scale": (I, [P, fp]),
         "vox_hip_model_set_kv_fp16": (I, [P, I]), "vox_hip_stream_kv_fp16": (I, [P]),
+        "vox_hip_set_gemm_planes": (I, [I]), "vox_hip_gemm_planes": (I, []),
         "vox_hip_stream_create": (P, [P]), "vox_hip_stream_free": (None, [P]),
         "vox_hip_stream_reset": (I, [P]), "vox_hip_stream_reset_decoder": (I, [P]),
         "vox_hip_stream_encode_mel": (I, [P, P, I, I]),
@@ -119,6 +121,16 @@ def fptr(a: np.ndarray):
 def _err(what):
     msg = lib().vox_hip_last_error()
     raise RuntimeError(f"{what}: {msg.decode() if msg else 'unknown error'}")
+
+
+def set_gemm_planes(planes: int):
+    """bf16 activation planes of the M > 1 GEMMs: 2 (default) or 3 (exact f32 activations)"""
+    if lib().vox_hip_set_gemm_planes(int(planes)) != 0:
+        _err("set_gemm_planes")
+
+
+def gemm_planes() -> int:
+    return lib().vox_hip_gemm_planes()
 
 
 def init(device: int | None = None):

@@ -41,6 +41,30 @@ static double timeit(F f, int iters, hipStream_t st) {
     return ms * 1000.0 / iters;
 }
 
+// prefetch probe (VOX_KB_ONLY=pf): block h reads the first row group of block h of the GEMV
+// that follows (rows as gemv_rows maps them), so that group sits in the L2 of the XCD block h
+// of the GEMV will run on
+__global__ __launch_bounds__(256) void k_touch_rows(const uint16_t* __restrict__ W, int rowbytes, int rb, int swiglu,
+                                                    int* __restrict__ sink) {
+    const int h = blockIdx.x;
+    unsigned acc = 0;
+    for (int i = 0; i < rb; i++) {
+        int row;
+        if (swiglu) {
+            const int u = h * (rb / 2) + (i >> 1);
+            row = ((u >> 4) << 5) + (u & 15) + ((i & 1) << 4);
+        } else {
+            row = h * rb + i;
+        }
+        const uint4* rp = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(W) + (size_t)row * rowbytes);
+        for (int c = threadIdx.x; c < rowbytes / 16; c += 256) {
+            const uint4 v = rp[c];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9e3779b9u) sink[0] = (int)acc;
+}
+
 int main(int argc, char** argv) {
     int iters = argc > 1 ? atoi(argv[1]) : 200;
     hipStream_t st;
@@ -105,6 +129,32 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "pf")) {
+        // does an L2-hot first row group shorten a decode GEMV?  A: GEMV alone (26 rotating
+        // layers, cold); B: touch kernel + GEMV; C: touch kernel alone.  GEMV with a hot first
+        // group ~ B - C.
+        int* sink = (int*)dmalloc(64, 0);
+        struct O { const char* n; int pro, epi, K, rows, rb; std::vector<uint16_t*>* w; };
+        for (O o : {O{"qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 4, &wqkv}, O{"wo", PRO_NONE, EPI_RESID, DQ, D, 2, &wo},
+                    O{"w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 4, &w13}, O{"w2", PRO_NONE, EPI_RESID, DH, D, 2, &w2}}) {
+            const int G = gemv_grid(o.rows);
+            const int sw = o.epi == EPI_SWIGLU;
+            char nm[96];
+            snprintf(nm, sizeof nm, "pf %-4s A gemv cold", o.n);
+            add(nm, timeit([&] { gemv(o.pro, o.epi, (*o.w)[layer++ % NL], o.K, o.rows); }, iters, st), (double)o.rows * o.K * 2);
+            snprintf(nm, sizeof nm, "pf %-4s B touch + gemv", o.n);
+            add(nm, timeit([&] {
+                    const uint16_t* W = (*o.w)[layer++ % NL];
+                    hipLaunchKernelGGL(k_touch_rows, dim3(G), dim3(256), 0, st, W, o.K * 2, o.rb, sw, sink);
+                    gemv(o.pro, o.epi, W, o.K, o.rows);
+                }, iters, st), (double)o.rows * o.K * 2);
+            snprintf(nm, sizeof nm, "pf %-4s C touch alone (grid %d)", o.n, G);
+            add(nm, timeit([&] {
+                    hipLaunchKernelGGL(k_touch_rows, dim3(G), dim3(256), 0, st, (*o.w)[layer++ % NL], o.K * 2, o.rb, sw, sink);
+                }, iters, st), (double)G * o.rb * o.K * 2);
+        }
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attn")) {
         // long-context decode attention as the decode step sees it: 26 layers' rings (f32:
         // 1.76 GB, half: 0.88 GB, far past the 256 MB MALL), one launch per layer in turn

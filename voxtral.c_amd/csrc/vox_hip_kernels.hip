@@ -3218,7 +3218,9 @@ int attn_maxch(int window) { return (window + ATT_MIN_BK - 1) / ATT_MIN_BK; }
 int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 int g_attn_lw = 0;  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
 int g_attn_kvfast = 1;  // long-context grid with the kv heads of a key range adjacent (tools/kbench: 0 = off)
-int g_attn_bsplit = -1;  // batched step, <= 256 keys: 128-key blocks when (stream, kv head) blocks < 256 (VOX_HIP_ATT_BSPLIT=1: on)
+// batched step, <= 256 keys: 128-key blocks when (stream, kv head) blocks < 256 (16 streams
+// 6582 -> 6695 tok/s, 8 streams 3556 -> 3632; VOX_HIP_ATT_BSPLIT=0: off)
+int g_attn_bsplit = -1;
 
 // past 256 keys: blocks of NWV x 16 keys per (kv head, key range); the last block of a kv
 // head merges the partials
@@ -3316,7 +3318,7 @@ static hipError_t attn_batch_fused(const AttnPtrs& p, const AttnFuse& f, int nb,
                                    int H, int KVH, int splits, int maxs, hipStream_t st) {
     if (g_attn_bsplit < 0) {
         const char* e = getenv("VOX_HIP_ATT_BSPLIT");
-        g_attn_bsplit = (e && atoi(e) == 1) ? 1 : 0;
+        g_attn_bsplit = (e && atoi(e) == 0) ? 0 : 1;
     }
     // contexts <= 256 keys: one 1024-thread block per (stream, kv head) -- unless those blocks
     // cannot fill the chip (16 streams x 8 kv heads = 128 blocks on 256 CUs): then the 128-key

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_attn_kvfast; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_attn_kvfast, g_attn_bsplit; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -153,6 +153,79 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL(k_touch_rows, dim3(G), dim3(256), 0, st, (*o.w)[layer++ % NL], o.K * 2, o.rb, sw, sink);
                 }, iters, st), (double)G * o.rb * o.K * 2);
         }
+        return 0;
+    }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "skb")) {
+        // batched decode projections at 16 rows: split-K k_skl (slabs, a row kernel sums them)
+        // against whole-K k_skf (final rows: the row kernel's slab sum could go)
+        uint16_t* xp = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * 9216 * 2, 1);
+        float* Cs = (float*)dmalloc((size_t)16 * 131072 * 4, 0);
+        float* part = (float*)dmalloc((size_t)2 * 16 * 18 * 18432 * 4, 0);
+        struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
+        const S shapes[] = {S{"qkv 6144x3072", DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
+                            S{"wo  3072x4096", D, DQ, wo.data(), (double)D * DQ * 2},
+                            S{"w13 18432x3072", 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
+                            S{"w2  3072x9216", D, DH, w2.data(), (double)D * DH * 2}};
+        for (const S& g : shapes) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "skl %s nb16", g.n);
+            add(nm, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
+            const int Rs[] = {1, 1, 2, 2, 2, 4, 4}, NWs[] = {4, 8, 4, 4, 8, 4, 8}, Ds[] = {2, 2, 2, 3, 2, 2, 2};
+            for (int c = 0; c < 7; c++) {
+                if ((g.N / 16) % Rs[c]) continue;
+                g_skf_r = Rs[c];
+                g_skf_nw = NWs[c];
+                g_skf_d = Ds[c];
+                snprintf(nm, sizeof nm, "skf %s R%d NW%d D%d (%d blocks)", g.n, Rs[c], NWs[c], Ds[c], g.N / 16 / Rs[c]);
+                add(nm, timeit([&] { CK(launch_gemm_skf(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, Cs, g.N, st)); }, iters, st), g.bytes);
+            }
+            g_skf_r = g_skf_nw = g_skf_d = 0;
+        }
+        return 0;
+    }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attb")) {
+        // batched fused decode attention (QKV slabs in, wo planes out) at 16 / 8 streams:
+        // each stream its own ring (26 layers rotated so K/V come from HBM)
+        const int rcap = 8192 + 64, NLd = 26, S6 = 6, N = DQ + 2 * DKV;
+        float* slabs = (float*)dmalloc((size_t)S6 * 16 * N * 4, 1);
+        uint16_t* xs = (uint16_t*)dmalloc((size_t)3 * 16 * DQ * 2, 0);
+        std::vector<float*> Ks(16 * 2), Vs(16 * 2);
+        for (int i = 0; i < 16 * 2; i++) {
+            Ks[i] = (float*)dmalloc((size_t)rcap * DKV * 4 * 13, 1);  // 13 layers per buffer
+            Vs[i] = (float*)dmalloc((size_t)rcap * DKV * 4 * 13, 1);
+        }
+        int* states = nullptr;
+        CK(hipMalloc(&states, 16 * 16));
+        float* parts = (float*)dmalloc((size_t)16 * (H * 128 * (HD + 2) * 4 + 4096), 0);
+        for (int nb : {16, 8})
+            for (int L : {64, 128, 190, 256}) {
+                std::vector<int> hs(16 * 4, 0);
+                for (int z = 0; z < 16; z++) hs[z * 4] = L - 1;
+                CK(hipMemcpy(states, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+                for (int bs : {0, 1}) {
+                    g_attn_bsplit = bs;
+                    int l = 0;
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "attn batch fused nb=%d L=%d bsplit=%d", nb, L, bs);
+                    add(nm, timeit([&] {
+                            AttnPtrs p;
+                            memset(&p, 0, sizeof p);
+                            const int lay = l % NLd;
+                            for (int z = 0; z < nb; z++) {
+                                p.q[z] = nullptr;
+                                p.Kc[z] = Ks[z * 2 + lay / 13] + (size_t)(lay % 13) * rcap * DKV;
+                                p.Vc[z] = Vs[z * 2 + lay / 13] + (size_t)(lay % 13) * rcap * DKV;
+                                p.state[z] = states + z * 4;
+                                p.part[z] = parts + (size_t)z * (H * 128 * (HD + 2) + 1024);
+                                p.out[z] = nullptr;
+                            }
+                            AttnFuse f{slabs, S6, N, rope, xs};
+                            CK(launch_attn_batch_fused(HD, p, f, nb, rcap, 8192, 0.088f, H, KVH, 1, st, 0));
+                            l++;
+                        }, iters, st), (double)nb * L * DKV * 2 * 4);
+                }
+            }
+        g_attn_bsplit = -1;
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attn")) {

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_attn_kvfast, g_attn_bsplit; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -155,12 +155,33 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "grid")) {
+        // decode GEMV grid cap (blocks of 256 threads): 1024 = 4 per CU (default) and larger
+        // grids for the Q8 rows, whose waves keep a third of the bf16 bytes in flight
+        struct O { const char* n; int pro, epi, K, rows, q8; std::vector<uint16_t*>* w; };
+        for (O o : {O{"qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 0, &wqkv}, O{"wo", PRO_NONE, EPI_RESID, DQ, D, 0, &wo},
+                    O{"w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 0, &w13}, O{"w2", PRO_NONE, EPI_RESID, DH, D, 0, &w2},
+                    O{"q8 qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 1, &wqkv}, O{"q8 wo", PRO_NONE, EPI_RESID, DQ, D, 1, &wo},
+                    O{"q8 w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 1, &w13}, O{"q8 w2", PRO_NONE, EPI_RESID, DH, D, 1, &w2}})
+            for (int mb : {1024, 1536, 2048, 3072}) {
+                g_gemv_maxb = mb;
+                qs = o.q8 ? wsc : nullptr;
+                char nm[96];
+                snprintf(nm, sizeof nm, "gemv %-6s cap %4d (grid %4d)", o.n, mb, gemv_grid(o.rows));
+                add(nm, timeit([&] { gemv(o.pro, o.epi, (*o.w)[layer++ % NL], o.K, o.rows); }, iters, st),
+                    (double)o.rows * o.K * (o.q8 ? 1 : 2));
+            }
+        g_gemv_maxb = 0;
+        qs = nullptr;
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "skb")) {
         // batched decode projections at 16 rows: split-K k_skl (slabs, a row kernel sums them)
         // against whole-K k_skf (final rows: the row kernel's slab sum could go)
         uint16_t* xp = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * 9216 * 2, 1);
         float* Cs = (float*)dmalloc((size_t)16 * 131072 * 4, 0);
         float* part = (float*)dmalloc((size_t)2 * 16 * 18 * 18432 * 4, 0);
+        int* sinkb = (int*)dmalloc(64, 0);
         struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
         const S shapes[] = {S{"qkv 6144x3072", DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
                             S{"wo  3072x4096", D, DQ, wo.data(), (double)D * DQ * 2},
@@ -170,6 +191,25 @@ int main(int argc, char** argv) {
             char nm[96];
             snprintf(nm, sizeof nm, "skl %s nb16", g.n);
             add(nm, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
+            // the same buffer every launch: the weights come from the Infinity Cache (MALL)
+            snprintf(nm, sizeof nm, "skl %s nb16 MALL-hot", g.n);
+            add(nm, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[0], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
+            // a touch kernel warms the first F bytes (default policy) just before the GEMM:
+            // B - C is the GEMM with a warm head
+            for (int mb : {16, 32}) {
+                const size_t F = std::min((size_t)mb << 20, (size_t)g.bytes);
+                const int G = (int)(F / (256 * 16 * 4));
+                snprintf(nm, sizeof nm, "skl %s B touch %d MB + gemm", g.n, mb);
+                add(nm, timeit([&] {
+                        const uint16_t* W = g.W[layer++ % NL];
+                        hipLaunchKernelGGL(k_touch_rows, dim3(G), dim3(256), 0, st, W, 256 * 16 * 4, 1, 0, sinkb);
+                        CK(launch_gemm_skl(xp, g.K, W, nullptr, g.N, 16, part, st));
+                    }, iters, st), g.bytes);
+                snprintf(nm, sizeof nm, "skl %s C touch %d MB alone", g.n, mb);
+                add(nm, timeit([&] {
+                        hipLaunchKernelGGL(k_touch_rows, dim3(G), dim3(256), 0, st, g.W[layer++ % NL], 256 * 16 * 4, 1, 0, sinkb);
+                    }, iters, st), (double)F);
+            }
             const int Rs[] = {1, 1, 2, 2, 2, 4, 4}, NWs[] = {4, 8, 4, 4, 8, 4, 8}, Ds[] = {2, 2, 2, 3, 2, 2, 2};
             for (int c = 0; c < 7; c++) {
                 if ((g.N / 16) % Rs[c]) continue;

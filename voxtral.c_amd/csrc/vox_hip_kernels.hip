@@ -2670,10 +2670,16 @@ __global__ __launch_bounds__(NW * 64) void k_sklx(const uint16_t* __restrict__ x
                 u32x4{__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]), __float_as_uint(acc[3])}, Pd,
                 (((s * SK_ROWS + j) * N) + g * 16 + (lane >> 4) * 4) * 4, 0, 16);
     }
+    // Publication order (MI355X_MICROARCH.md "handoff-flag": sc1 payload -> vmcnt(0) -> flag):
+    // the slab stores above are write-through (sc1), so once vmcnt(0) retires them they sit
+    // past every XCD's L2; the finisher reads them with sc1 loads, which miss its own L2.  No
+    // dirty line is involved on either side, so no agent-scope release / acquire fence (an L2
+    // write-back / invalidate per block) is needed; the ticket itself is a relaxed agent-scope
+    // add, issued by one lane after the whole block has drained.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* tk = f.ticket + z * X + xi;
-    if (tid == 0) s_fin = S == 1 || atomicAdd(tk, 1) == S - 1;
+    if (tid == 0) s_fin = S == 1 || __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
     __syncthreads();
     if (!s_fin) return;
     if (tid == 0 && S > 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3120,14 +3126,16 @@ static int gemv_rb(int rows) {
     return 2;
 }
 
+int g_gemv_maxb = 0;  // tools/kbench knob: grid cap other than GEMV_MAX_BLOCKS (no LM head)
 int gemv_grid(int rows) {
     // the largest divisor of the group count that fits 4 blocks per CU: every block then
-    // runs the same number of groups (no tail)
-    const int ng = rows / gemv_rb(rows);
+    // runs the same number of groups (no tail); tools/kbench VOX_KB_ONLY=grid: 1536-2304
+    // blocks were slower on every decode shape, bf16 and Q8 (profiles/r3_kbench_gemv_grid.txt)
+    const int ng = rows / gemv_rb(rows), maxb = g_gemv_maxb ? g_gemv_maxb : GEMV_MAX_BLOCKS;
     int best = 1;
-    for (int gsz = 1; gsz <= GEMV_MAX_BLOCKS && gsz <= ng; gsz++)
+    for (int gsz = 1; gsz <= maxb && gsz <= ng; gsz++)
         if (ng % gsz == 0) best = gsz;
-    if (best < 256 && ng > GEMV_MAX_BLOCKS) best = GEMV_MAX_BLOCKS;  // no good divisor: accept a tail
+    if (best < 256 && ng > maxb) best = maxb;  // no good divisor: accept a tail
     return best;
 }
 

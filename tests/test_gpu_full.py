@@ -61,6 +61,37 @@ def test_full_jfk_transcription(full, jfk_samples):
     os_.close()
 
 
+def test_full_night1968_5s_transcription(full):
+    """C2's shortest benchmark clip, the reference's samples/benchmark/night1968/
+    5s_dont_worry_about_him.wav (a recording, not synthetic audio; kept as a fixture like
+    jfk.wav): one-shot schedule, every greedy step's id and logits against the oracle."""
+    import vox_hip
+    import vox_oracle
+    cfg, hm, om = full
+    samples = vox_oracle.read_wav(os.path.join(os.path.dirname(__file__), "golden", "night1968_5s.wav"))
+    assert abs(len(samples) / 16000.0 - 5.0) < 0.01
+    events = vox_oracle.transcribe_mel_schedule(samples)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    h_tok, o_tok, h_log, o_log = [], [], [], []
+    for kind, mel in events:
+        cur = {"feed": 0, "flush": events[0][1].shape[0], "finish": events[1][1].shape[0]}[kind]
+        for s, toks, logs in ((hs, h_tok, h_log), (os_, o_tok, o_log)):
+            s.encode_mel(mel[cur:])
+            t, lg = s.decode(stop_at_eos=False, want_logits=True)
+            toks += t.tolist()
+            logs.append(lg.copy())
+    assert hs.adapter_tokens == os_.adapter_tokens
+    ra = rel(hs.read_adapter(), os_.read_adapter())
+    rl = rel(np.concatenate(h_log), np.concatenate(o_log))
+    print(f"night1968 5 s: {hs.adapter_tokens} adapter rows rel err {ra:.2e}, {len(o_tok)} ids, logits rel err {rl:.2e}")
+    assert ra < TOL, ra
+    assert len(o_tok) > 50
+    assert h_tok == o_tok
+    assert rl < TOL, rl
+    hs.close()
+    os_.close()
+
+
 def synth_audio(seconds, seed):
     """Speech-band synthetic audio (no recording offline; the path's work depends only on
     the length): noise bursts under a slow envelope plus drifting tones."""

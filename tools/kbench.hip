@@ -221,6 +221,22 @@ int main(int argc, char** argv) {
             }
             g_skf_r = g_skf_nw = g_skf_d = 0;
         }
+        // the rows between the projections: one 512-thread block per row vs one wave per
+        // (256-column slice, row)
+        float* xr = (float*)dmalloc((size_t)16 * 9216 * 4, 1);
+        float* ssq = (float*)dmalloc(16 * 16 * 4, 0);
+        for (int S : {8, 18}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "resid(%d)+rmsnorm fplanes 16x3072", S);
+            add(nm, timeit([&] { CK(launch_rmsnorm_fplanes(xr, 16, D, xr, xr, 1e-5f, xp, part, S, st)); }, iters, st), 16.0 * D * (10 + 4 * S));
+            snprintf(nm, sizeof nm, "resid(%d)+xw fplanes 16x3072 (12 slices)", S);
+            add(nm, timeit([&] { CK(launch_resid_xw_fplanes(xr, 16, D, xr, xr, xp, part, S, nullptr, ssq, st)); }, iters, st), 16.0 * D * (10 + 4 * S));
+        }
+        for (const S& g : {shapes[0], shapes[2]}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "skl %s nb16 + rms scale", g.n);
+            add(nm, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st, ssq, 12, 1e-5f)); }, iters, st), g.bytes);
+        }
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attb")) {

@@ -1985,6 +1985,7 @@ struct vox_hip_batch {
     hipStream_t st;
     float *x, *q, *att, *logits, *pval;
     float* part;     // split-K slabs of the current projection (k_skl), consumed by the next kernel
+    float* ssq;      // row sums of squares per 256-column slice (k_resid_xw_fplanes -> k_skl)
     int* pidx;
     uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows (fragment order)
     // one captured step for the current active set (kernel arguments hold per-stream
@@ -2034,7 +2035,7 @@ static int model_frag(vox_hip_model_t* m) {
 extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     if (!b) return;
     if (b->st) hipStreamSynchronize(b->st);
-    dfree(b->x); dfree(b->part); dfree(b->q); dfree(b->att);
+    dfree(b->x); dfree(b->part); dfree(b->ssq); dfree(b->q); dfree(b->att);
     dfree(b->logits); dfree(b->pval); dfree(b->pidx);
     dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h);
     if (b->gexec) hipGraphExecDestroy(b->gexec);
@@ -2067,6 +2068,7 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
         }
         TRYH(dalloc(&b->part, (size_t)SK_ROWS * n));
     }
+    TRYH(dalloc(&b->ssq, (size_t)SK_MAX_ROWS * SKL_MAX_SLICES));
     TRYH(dalloc(&b->q, B * c.dec_heads * c.dec_head_dim));
     TRYH(dalloc(&b->att, B * c.dec_heads * c.dec_head_dim));
     TRYH(dalloc(&b->logits, B * c.vocab));
@@ -2107,6 +2109,12 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         if (ss[i]->kv16 != kv16) return set_err("batched step over streams of different KV element types");
     sp.kv16 = kv16;
     const int Sres = skl_splits(DH);  // slabs the previous layer's w2 left for the residual
+    static int xw_env = -1;
+    if (xw_env < 0) {
+        const char* e = getenv("VOX_HIP_BATCH_XW");
+        xw_env = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    const bool xw = xw_env && DD % 256 == 0 && DD / 256 <= SKL_MAX_SLICES;
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         for (int i = 0; i < nb; i++) {
@@ -2119,8 +2127,16 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         // skinny MFMA GEMMs over fragment-major weights: the streams are the 16-column B
         // operand, every weight byte read once per step; each projection leaves split-K slabs
         // in b->part that the next kernel sums (with the residual for wo / w2)
-        CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, b->part, l ? Sres : 0, st));
-        CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
+        // residual + RMSNorm: slice-parallel rows (x * w planes + slice sums of squares, the
+        // inverse RMS applied by the projection) or one block per row (VOX_HIP_BATCH_XW=0)
+        if (xw) {
+            CK(launch_resid_xw_fplanes(b->x, nb, DD, L.attn_norm, nullptr, b->xp_d, b->part, l ? Sres : 0, nullptr,
+                                       b->ssq, st));
+            CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
+        } else {
+            CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, b->part, l ? Sres : 0, st));
+            CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
+        }
         if (hd == 128) {
             // RoPE + KV append + attention, output into the wo planes (one launch; + the
             // combine kernel past 256 keys)
@@ -2133,9 +2149,15 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
             CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
         }
         CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
-        CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d, b->part,
-                                  skl_splits(DQ), st));
-        CK(launch_gemm_skl(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st));
+        if (xw) {
+            CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
+                                       skl_splits(DQ), nullptr, b->ssq, st));
+            CK(launch_gemm_skl(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
+        } else {
+            CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d,
+                                      b->part, skl_splits(DQ), st));
+            CK(launch_gemm_skl(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st));
+        }
         CK(launch_swiglu_fplanes(b->part, skl_splits(DD), DH, nb, b->xp_h, st));
         CK(launch_gemm_skl(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
     }

@@ -155,8 +155,15 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
                            int ldc, hipStream_t st);
 // split-K slabs part[s][16][N], s < skl_splits(K) (projections: k_skl)
 int skl_splits(int K);
+// ssq: RMSNorm applied to the results (planes from launch_resid_xw_fplanes, nsl slices per row)
+constexpr int SKL_MAX_SLICES = 12;  // D <= 3072
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
-                           float* part, hipStream_t st);
+                           float* part, hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f);
+// x += the S slabs (+ bias); planes of x * w (* (1 + ada)); the row's sums of squares per
+// 256-column slice to ssq[row / 16][D / 256][row % 16] (the inverse RMS is applied by
+// launch_gemm_skl)
+hipError_t launch_resid_xw_fplanes(float* x, int nb, int D, const float* w, const float* ada, uint16_t* xs,
+                                   const float* part, int S, const float* bias, float* ssq, hipStream_t st);
 // k_sklx: k_skl with the neighbouring row kernels folded in (bf16 weights).  Inputs are
 // always planes; SKX_PRO_SCALE planes hold x * w (* (1 + ada)) of an RMSNorm whose inverse RMS
 // is applied to the MFMA results, computed from the row sums of squares that the producer left

@@ -2482,11 +2482,16 @@ __global__ __launch_bounds__(NW * 64) void k_skf(const uint16_t* __restrict__ xs
 // kernel runs and the result does not depend on timing.  Re-reading the planes from L2 per
 // 16-row group (k_skf at R = 1) moved 3x the weight bytes through the load path.
 // ============================================================================
-template <int WQ8, int NW, int KS>
+// ssq != null: the planes hold x * w (* (1 + ada)) of an RMSNorm (k_resid_xw_fplanes) and
+// every result of stream row j is multiplied by 1 / sqrt(sum_t ssq[z][t][j] / K + eps), the
+// row's sum of squares from its nsl column slices added in slice order.
+template <int WQ8, int NW, int KS, int SC = 0>
 __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs, int K,
                                                  const uint8_t* __restrict__ W, const float* __restrict__ wscale,
-                                                 int N, int nb, float* __restrict__ part) {
+                                                 int N, int nb, float* __restrict__ part,
+                                                 const float* __restrict__ ssq = nullptr, int nsl = 0, float eps = 0.f) {
     __shared__ uint4 xb[KS * 6 * 64];  // [block][plane][half][lane]
+    __shared__ float s_sq[SC ? SK_ROWS * SKL_MAX_SLICES : 1];
     constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
     constexpr int NF = KS * 6 / NW;  // 16-B plane pieces per thread
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2520,6 +2525,10 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
         const int p = rem >> 7, t = (rem >> 6) & 1, l = rem & 63;
         f[i] = *reinterpret_cast<const uint4*>(xs + p * P + (size_t)((kb0 + blk) * 2 + t) * 512 + l * 8);
     }
+    // SC: the slice sums of squares ssq[z][t][j] travel with the planes (one value per
+    // thread into LDS), the epilogue adds them up per row
+    float sqv = 0.f;
+    if (SC) sqv = ssq[(size_t)z * nsl * SK_ROWS + min(tid, nsl * SK_ROWS - 1)];
     const __amdgpu_buffer_rsrc_t Wd =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g * KB * FB, 0, KB * FB, 0x00020000);
     u32x4 a[KS][NH];
@@ -2529,6 +2538,7 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
         for (int t = 0; t < NH; t++) a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(Wd, lane * 16 + t * 1024, (kb0 + kb) * FB, 2);
 #pragma unroll
     for (int i = 0; i < NF; i++) xb[tid + i * NW * 64] = f[i];
+    if (SC && tid < nsl * SK_ROWS) s_sq[tid] = sqv;
     __syncthreads();
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2549,6 +2559,19 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
                                                              acc, 0, 0, 0);
         }
     const int j = lane & 15;
+    if (SC) {
+        // all reads out together (one LDS latency), then added in slice order
+        float sv[SKL_MAX_SLICES];
+#pragma unroll
+        for (int t = 0; t < SKL_MAX_SLICES; t++) sv[t] = s_sq[min(t, nsl - 1) * SK_ROWS + j];
+        float ss = 0.f;
+#pragma unroll
+        for (int t = 0; t < SKL_MAX_SLICES; t++)
+            if (t < nsl) ss += sv[t];
+        const float inv = 1.0f / sqrtf(ss / (float)K + eps);
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[i] *= inv;
+    }
     if (j < nb) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -2556,6 +2579,76 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
             part[((size_t)s * SK_ROWS + j) * N + row] = WQ8 ? acc[i] * wscale[row] : acc[i];
         }
     }
+}
+
+// Residual + the planes of an RMSNorm without its row reduction: x += the S slabs of the
+// previous projection (+ bias, summed in split order as k_resid_rmsnorm_fplanes), the row
+// written back, the planes of x * w (* (1 + ada)) -- the inverse RMS is applied by the next
+// projection (k_skl ssq) -- and the sum of squares of this block's column slice to
+// ssq[row block][slice][row % 16].  One wave per (256-column slice, row): a row's slab bytes spread over
+// D / 256 CUs instead of one (the batched step's rows are latency-bound at 16 blocks).
+__global__ __launch_bounds__(64) void k_resid_xw_fplanes(float* __restrict__ x, int D,
+                                                         const float* __restrict__ part, int S,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ ada,
+                                                         uint16_t* __restrict__ xs, float* __restrict__ ssq) {
+    constexpr int CH = 8;  // slabs per load round
+    const int sl = blockIdx.x, j = blockIdx.y, lane = threadIdx.x;
+    const int k = sl * 256 + lane * 4;
+    float* xr = x + (size_t)j * D + k;
+    float4 v = *reinterpret_cast<const float4*>(xr);
+    const float4 ww = *reinterpret_cast<const float4*>(w + k);
+    const float4 aa = ada ? *reinterpret_cast<const float4*>(ada + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (S > 0) {
+        const float* pb = part + (size_t)(j >> 4) * S * SK_ROWS * D + (size_t)(j & 15) * D + k;
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s0 = 0; s0 < S; s0 += CH) {
+            float4 t[CH];
+#pragma unroll
+            for (int c = 0; c < CH; c++)
+                t[c] = s0 + c < S ? *reinterpret_cast<const float4*>(pb + (size_t)(s0 + c) * SK_ROWS * D)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int c = 0; c < CH; c++)
+                if (s0 + c < S) {
+                    if (s0 + c) {
+                        r.x += t[c].x; r.y += t[c].y; r.z += t[c].z; r.w += t[c].w;
+                    } else {
+                        r = t[c];
+                    }
+                }
+        }
+        if (bias) {
+            r.x += bb.x; r.y += bb.y; r.z += bb.z; r.w += bb.w;
+        }
+        v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+        *reinterpret_cast<float4*>(xr) = v;
+    }
+    float ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+    ss = wave_sum(ss);
+    if (lane == 0) ssq[((size_t)(j >> 4) * gridDim.x + sl) * SK_ROWS + (j & 15)] = ss;
+    const float e[4] = {v.x * ww.x, v.y * ww.y, v.z * ww.z, v.w * ww.w};
+    const float ad[4] = {aa.x, aa.y, aa.z, aa.w};
+    uint32_t hp[2], mp[2], lq[2];
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+        float v0 = e[i], v1 = e[i + 1];
+        if (ada) {
+            v0 *= (1.0f + ad[i]);
+            v1 *= (1.0f + ad[i + 1]);
+        }
+        uint16_t h0, m0, l0, h1, m1, l1;
+        split3(v0, h0, m0, l0);
+        split3(v1, h1, m1, l1);
+        hp[i / 2] = h0 | ((uint32_t)h1 << 16);
+        mp[i / 2] = m0 | ((uint32_t)m1 << 16);
+        lq[i / 2] = l0 | ((uint32_t)l1 << 16);
+    }
+    *reinterpret_cast<uint2*>(xs + frag_at(j, D, 0, k)) = make_uint2(hp[0], hp[1]);
+    *reinterpret_cast<uint2*>(xs + frag_at(j, D, 1, k)) = make_uint2(mp[0], mp[1]);
+    *reinterpret_cast<uint2*>(xs + frag_at(j, D, 2, k)) = make_uint2(lq[0], lq[1]);
 }
 
 // silu(W1 x) * (W3 x) of the split W1|W3 result (16-row interleave, upload_w13) into the
@@ -3515,13 +3608,25 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
 
 template <int Q, int NW, int KS>
 static hipError_t skl_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
-                             float* part, hipStream_t st) {
+                             float* part, hipStream_t st, const float* ssq, int nsl, float eps) {
     const int units = (N / (16 * NW)) * (K / (64 * KS));
     const int Z = (nb + SK_ROWS - 1) / SK_ROWS;
     const int grid = Z > 1 ? (units + 7) / 8 * 8 * Z : units;
-    hipLaunchKernelGGL((k_skl<Q, NW, KS>), dim3(grid), dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W),
-                       wscale, N, nb, part);
+    if (ssq)
+        hipLaunchKernelGGL((k_skl<Q, NW, KS, 1>), dim3(grid), dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W),
+                           wscale, N, nb, part, ssq, nsl, eps);
+    else
+        hipLaunchKernelGGL((k_skl<Q, NW, KS, 0>), dim3(grid), dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W),
+                           wscale, N, nb, part, nullptr, 0, 0.f);
     return hipGetLastError();
+}
+
+hipError_t launch_resid_xw_fplanes(float* x, int nb, int D, const float* w, const float* ada, uint16_t* xs,
+                                   const float* part, int S, const float* bias, float* ssq, hipStream_t st) {
+    if (nb < 1 || nb > SK_MAX_ROWS || D % 256 || D / 256 > SKL_MAX_SLICES || !ssq) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_resid_xw_fplanes, dim3(D / 256, nb), dim3(64), 0, st, x, D, part, S, bias, w, ada, xs, ssq);
+    LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 int skl_splits(int K) {
@@ -3530,9 +3635,11 @@ int skl_splits(int K) {
 }
 
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
-                           float* part, hipStream_t st) {
+                           float* part, hipStream_t st, const float* ssq, int nsl, float eps) {
     const int S = skl_splits(K);
-    if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S) return hipErrorInvalidValue;
+    // ssq: one row block (its nsl x 16 sums ride with the planes: nsl * 16 <= the block's threads)
+    if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S || (ssq && (nsl < 1 || nsl > SKL_MAX_SLICES || nb > SK_ROWS)))
+        return hipErrorInvalidValue;
     const int ks = K / 64 / S;
     // waves (row groups) per block, by the 8-wave grid size (N / 128) * S: narrow outputs take
     // 8 from 128 blocks (decoder wo 3072 x 4096: 7.8 -> 7.1 us at 16 rows; the encoder's wo /
@@ -3543,7 +3650,7 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
     if (N % (16 * nw)) nw = 4;
     if (N % (16 * nw)) return hipErrorInvalidValue;
 #define SKL_X(Q, NWW, KSS) \
-    if ((wscale != nullptr) == Q && nw == NWW && ks == KSS) return skl_launch<Q, NWW, KSS>(xs, K, Wf, wscale, N, nb, part, st);
+    if ((wscale != nullptr) == Q && nw == NWW && ks == KSS) return skl_launch<Q, NWW, KSS>(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
     SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4)
     SKL_X(1, 4, 8) SKL_X(1, 8, 8) SKL_X(1, 4, 4) SKL_X(1, 8, 4)
 #undef SKL_X

@@ -1986,6 +1986,7 @@ struct vox_hip_batch {
     float *x, *q, *att, *logits, *pval;
     float* part;     // split-K slabs of the current projection (k_skl), consumed by the next kernel
     float* ssq;      // row sums of squares per 256-column slice (k_resid_xw_fplanes -> k_skl)
+    int* ticket;     // k_sklx slice tickets (VOX_HIP_BATCH_SWX: W1|W3 with SwiGLU folded in)
     int* pidx;
     uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows (fragment order)
     // one captured step for the current active set (kernel arguments hold per-stream
@@ -2035,7 +2036,7 @@ static int model_frag(vox_hip_model_t* m) {
 extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     if (!b) return;
     if (b->st) hipStreamSynchronize(b->st);
-    dfree(b->x); dfree(b->part); dfree(b->ssq); dfree(b->q); dfree(b->att);
+    dfree(b->x); dfree(b->part); dfree(b->ssq); dfree(b->ticket); dfree(b->q); dfree(b->att);
     dfree(b->logits); dfree(b->pval); dfree(b->pidx);
     dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h);
     if (b->gexec) hipGraphExecDestroy(b->gexec);
@@ -2069,6 +2070,7 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
         TRYH(dalloc(&b->part, (size_t)SK_ROWS * n));
     }
     TRYH(dalloc(&b->ssq, (size_t)SK_MAX_ROWS * SKL_MAX_SLICES));
+    TRYH(dalloc(&b->ticket, (size_t)SKX_TICKETS));
     TRYH(dalloc(&b->q, B * c.dec_heads * c.dec_head_dim));
     TRYH(dalloc(&b->att, B * c.dec_heads * c.dec_head_dim));
     TRYH(dalloc(&b->logits, B * c.vocab));
@@ -2115,6 +2117,11 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         xw_env = (e && atoi(e) == 0) ? 0 : 1;
     }
     const bool xw = xw_env && DD % 256 == 0 && DD / 256 <= SKL_MAX_SLICES;
+    static int swx = -1;
+    if (swx < 0) {
+        const char* e = getenv("VOX_HIP_BATCH_SWX");
+        swx = (e && atoi(e) == 1) ? 1 : 0;
+    }
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         for (int i = 0; i < nb; i++) {
@@ -2149,7 +2156,18 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
             CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
         }
         CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
-        if (xw) {
+        if (xw && swx && !L.s13) {
+            // W1|W3 with the SwiGLU folded in (k_sklx: the last block of each column slice
+            // sums its slabs and writes the w2 planes; no k_swiglu_fplanes launch)
+            CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
+                                       skl_splits(DQ), nullptr, b->ssq, st));
+            SklFused f;
+            f.ssq_in = b->ssq; f.nsl = DD / 256; f.eps = c.dec_eps; f.part = b->part; f.ticket = b->ticket;
+            f.planes = b->xp_h;
+            CK(launch_gemm_sklx(SKX_PRO_SCALE, SKX_EPI_SWIGLU, b->xp_d, DD, F.w13, 2 * DH, nb, f, st));
+            CK(launch_gemm_skl(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
+            continue;
+        } else if (xw) {
             CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
                                        skl_splits(DQ), nullptr, b->ssq, st));
             CK(launch_gemm_skl(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));

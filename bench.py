@@ -300,7 +300,9 @@ def main():
         return dry_run(args, d)
     import vox_hip
     from vox_weights import VOXTRAL_4B, quantize_q8, synth_weights
-    vox_hip.init(device=d.local)
+    # VOX_BENCH_SHARE_GPU=1: every rank on device 0 -- a rehearsal of the multi-rank path
+    # (launcher, barrier, max / sum over ranks) on a one-GPU box; its timings mean nothing
+    vox_hip.init(device=0 if os.environ.get("VOX_BENCH_SHARE_GPU") == "1" else d.local)
     cfg = VOXTRAL_4B
 
     w = synth_weights(cfg, seed=args.seed)

@@ -280,6 +280,27 @@ int main(int argc, char** argv) {
                             l++;
                         }, iters, st), (double)nb * L * DKV * 2 * 4);
                 }
+                {
+                    // the same attention without the fused prologue / epilogue (q rows in, rows out)
+                    int l = 0;
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "attn batch plain nb=%d L=%d", nb, L);
+                    add(nm, timeit([&] {
+                            AttnPtrs p;
+                            memset(&p, 0, sizeof p);
+                            const int lay = l % NLd;
+                            for (int z = 0; z < nb; z++) {
+                                p.q[z] = slabs + (size_t)z * DQ;
+                                p.Kc[z] = Ks[z * 2 + lay / 13] + (size_t)(lay % 13) * rcap * DKV;
+                                p.Vc[z] = Vs[z * 2 + lay / 13] + (size_t)(lay % 13) * rcap * DKV;
+                                p.state[z] = states + z * 4;
+                                p.part[z] = parts + (size_t)z * (H * 128 * (HD + 2) + 1024);
+                                p.out[z] = reinterpret_cast<float*>(xs) + (size_t)z * DQ / 2;
+                            }
+                            CK(launch_attn_decode_batch(HD, p, nb, rcap, 8192, 0.088f, H, KVH, 1, st, 0));
+                            l++;
+                        }, iters, st), (double)nb * L * DKV * 2 * 4);
+                }
             }
         g_attn_bsplit = -1;
         return 0;

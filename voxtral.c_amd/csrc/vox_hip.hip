@@ -1986,7 +1986,7 @@ struct vox_hip_batch {
     float *x, *q, *att, *logits, *pval;
     float* part;     // split-K slabs of the current projection (k_skl), consumed by the next kernel
     float* ssq;      // row sums of squares per 256-column slice (k_resid_xw_fplanes -> k_skl)
-    int* ticket;     // k_sklx slice tickets (VOX_HIP_BATCH_SWX: W1|W3 with SwiGLU folded in)
+    int* ticket;     // k_sklx slice tickets (W1|W3 with the SwiGLU folded in; VOX_HIP_BATCH_SWX=0: off)
     int* pidx;
     uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows (fragment order)
     // one captured step for the current active set (kernel arguments hold per-stream
@@ -2069,7 +2069,7 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
         }
         TRYH(dalloc(&b->part, (size_t)SK_ROWS * n));
     }
-    TRYH(dalloc(&b->ssq, (size_t)SK_MAX_ROWS * SKL_MAX_SLICES));
+    TRYH(dalloc(&b->ssq, (size_t)SK_ROWS * SKX_TICKETS));  // [slices][16], any slice count
     TRYH(dalloc(&b->ticket, (size_t)SKX_TICKETS));
     TRYH(dalloc(&b->q, B * c.dec_heads * c.dec_head_dim));
     TRYH(dalloc(&b->att, B * c.dec_heads * c.dec_head_dim));
@@ -2117,10 +2117,15 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         xw_env = (e && atoi(e) == 0) ? 0 : 1;
     }
     const bool xw = xw_env && DD % 256 == 0 && DD / 256 <= SKL_MAX_SLICES;
+    static int wox = -1;
+    if (wox < 0) {
+        const char* e = getenv("VOX_HIP_BATCH_WOX");
+        wox = (e && atoi(e) == 1) ? 1 : 0;
+    }
     static int swx = -1;
     if (swx < 0) {
         const char* e = getenv("VOX_HIP_BATCH_SWX");
-        swx = (e && atoi(e) == 1) ? 1 : 0;
+        swx = (e && atoi(e) == 0) ? 0 : 1;
     }
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
@@ -2155,14 +2160,27 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
             CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
             CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
         }
-        CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
+        const bool fuse_wo = xw && swx && wox && !L.so && !L.s13;
+        if (fuse_wo) {
+            // wo with the residual folded in (k_sklx: the last block of each column slice sums
+            // its slabs into x and writes the slice's x * ffn_norm * (1 + ada) planes and row
+            // sums of squares for W1|W3)
+            SklFused fo;
+            fo.part = b->part; fo.ticket = b->ticket; fo.x = b->x; fo.ssq_out = b->ssq; fo.planes = b->xp_d;
+            fo.nw = L.ffn_norm; fo.ada = m->ada_scale + (size_t)l * DD;
+            CK(launch_gemm_sklx(SKX_PRO_PLANES, SKX_EPI_RESID, b->xp_q, DQ, F.wo, DD, nb, fo, st));
+        } else {
+            CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
+        }
         if (xw && swx && !L.s13) {
             // W1|W3 with the SwiGLU folded in (k_sklx: the last block of each column slice
             // sums its slabs and writes the w2 planes; no k_swiglu_fplanes launch)
-            CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
-                                       skl_splits(DQ), nullptr, b->ssq, st));
+            if (!fuse_wo)
+                CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
+                                           skl_splits(DQ), nullptr, b->ssq, st));
             SklFused f;
-            f.ssq_in = b->ssq; f.nsl = DD / 256; f.eps = c.dec_eps; f.part = b->part; f.ticket = b->ticket;
+            f.ssq_in = b->ssq; f.nsl = fuse_wo ? sklx_slices(DD, DQ) : DD / 256; f.eps = c.dec_eps;
+            f.part = b->part; f.ticket = b->ticket;
             f.planes = b->xp_h;
             CK(launch_gemm_sklx(SKX_PRO_SCALE, SKX_EPI_SWIGLU, b->xp_d, DD, F.w13, 2 * DH, nb, f, st));
             CK(launch_gemm_skl(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));

@@ -155,24 +155,26 @@ def _oracle_tokens_parallel(om, mels, chunks):
 
 
 @pytest.mark.slow
-def test_batch_full_size_8_streams_each_vs_oracle():
-    """Full Voxtral-4B shapes, config 4's per-GPU load: 8 jfk-shaped streams (1355 / 140 / 1
-    mel-frame chunks, 149 tokens each, different audio) decoded as one batch; EVERY stream's
-    ids equal the CPU oracle's for that stream."""
+@pytest.mark.parametrize("nstreams", [8, 16])
+def test_batch_full_size_streams_each_vs_oracle(nstreams):
+    """Full Voxtral-4B shapes: config 4's per-GPU load (8 streams) and the 16-stream bench
+    line's, jfk-shaped streams (1355 / 140 / 1 mel-frame chunks, 149 tokens each, different
+    audio) decoded as one batch; EVERY stream's ids equal the CPU oracle's for that stream and
+    the final batched step's logits are within LOGIT_TOL."""
     import vox_hip
     import vox_oracle
     from vox_weights import VOXTRAL_4B, synth_weights
     chunks = [1355, 140, 1]
     w = synth_weights(VOXTRAL_4B, seed=0)
     hm = vox_hip.Model(VOXTRAL_4B, w)
-    mels = _mels(VOXTRAL_4B, [sum(chunks)] * 8, 42)
+    mels = _mels(VOXTRAL_4B, [sum(chunks)] * nstreams, 42)
     ss = [vox_hip.Stream(hm) for _ in mels]
     for s, mel in zip(ss, mels):
         off = 0
         for n in chunks:
             s.encode_mel(mel[off:off + n])
             off += n
-    b = vox_hip.Batch(hm, 8)
+    b = vox_hip.Batch(hm, nstreams)
     got = [g.tolist() for g in b.decode(ss, max_steps=1000, stop_at_eos=False)]
     last = [b.read_logits(s) for s in ss]   # the final batched step (all 8 streams in it)
     for s in ss:
@@ -183,13 +185,13 @@ def test_batch_full_size_8_streams_each_vs_oracle():
     refs, ref_last = _oracle_tokens_parallel(om, mels, chunks)
     om.close()
     worst = 0.0
-    for i in range(8):
+    for i in range(nstreams):
         assert len(refs[i]) == 149
         assert got[i] == refs[i], (i, next(k for k in range(149) if got[i][k] != refs[i][k]))
         r = rel(last[i], ref_last[i])
         worst = max(worst, r)
         assert r < LOGIT_TOL, (i, r)
-    print(f"8 full-size streams: ids equal, last-step logits worst rel err {worst:.2e}")
+    print(f"{nstreams} full-size streams: ids equal, last-step logits worst rel err {worst:.2e}")
     assert len({tuple(r) for r in refs}) > 1   # the streams really differ
 
 

@@ -10,5 +10,8 @@ for m in 1 0 1 0; do
   VOX_HIP_BATCH_WOX=$m timeout -k 10 200 python -u bench.py --no-cpu-baseline --streams 8 > gpurun_out/r3ab_s8_$m.json 2>> gpurun_out/r3ab.err || exit 1
   python3 -c "import json;d=json.load(open('gpurun_out/r3ab_s8_$m.json'));print('s8 wox$m', d['value'], d['decoder_ms_per_batched_step'])"
 done
-VOX_KB_ONLY=attb timeout -k 10 180 tools/kbench 100 > gpurun_out/r3ab_attb.txt 2>&1
+VOX_KB_ONLY=attb timeout -k 10 180 tools/kbench 100 > gpurun_out/r3ab_attb.txt 2>&1 || exit 1
+# last (it may end in the profiler's SIGSEGV): the graph-replayed bench under the kernel trace
+# with kernel arguments in host memory instead of device memory
+HIP_FORCE_DEV_KERNARG=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3ab_graph -o g -- python3 -u bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/r3ab_graph.log 2>&1
 echo rc=$?

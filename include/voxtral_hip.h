@@ -137,6 +137,12 @@ int vox_hip_stream_reset_decoder(vox_hip_stream_t *s);
 int vox_hip_stream_encode_mel(vox_hip_stream_t *s, const float *mel, int n_frames,
                               int mel_on_device);
 int vox_hip_stream_adapter_tokens(vox_hip_stream_t *s);
+/* on != 0: vox_hip_stream_encode_mel returns once the pass is enqueued on the stream's HIP
+ * queue (its adapter-row count is known on the host); everything later on the same stream
+ * (decode, read_adapter, reset) is ordered behind it and the batched step waits for every
+ * member stream, so a scheduler can have several streams' encoder chunks in flight at once.
+ * Host mel pointers must stay valid until vox_hip_stream_sync.  Default 0 (synchronous). */
+int vox_hip_stream_set_async_encode(vox_hip_stream_t *s, int on);
 
 /* Incremental log-mel on the device: a vox_mel_ctx_t
  * (voxtral_audio.c:405-671) whose padded sample buffer and frames live in HBM, computed on

@@ -502,6 +502,7 @@ struct vox_hip_stream {
     float* eslab;            // skinny encoder: split-K slabs [4][S][16][N]
     uint16_t* exp2;          // k_sklx: the second planes buffer (wo / w2 inputs)
     int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
+    int enc_async;           // vox_hip_stream_encode_mel returns without a stream sync
     float* essq;             // k_sklx row sums of squares per column slice [2][slices][16]
     uint16_t *gpa, *gpc;     // k_gemmf planes: norm / attention rows (K <= max(enc_dim, heads x hd)), gate rows
     int* gflags;             // k_gemmf partial-tile flags (gemmf_grid() ints)
@@ -1224,7 +1225,7 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
                           hipMemcpyDeviceToDevice, st));
     s->res_count = new_res;
     if (feed <= 0) {
-        CK(hipStreamSynchronize(st));
+        if (!s->enc_async) CK(hipStreamSynchronize(st));
         return 0;
     }
     // ---- conv1 over [c0_tail(2) | feed], first output discarded (voxtral.c:694-756) ----
@@ -1271,8 +1272,15 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
         CK(hipMemcpyAsync(s->enc_res + (size_t)R * ED, xin, (size_t)T1 * ED * 4, hipMemcpyDeviceToDevice, st));
     }
     s->enc_res_count = left;
-    CK(hipStreamSynchronize(st));
+    if (!s->enc_async) CK(hipStreamSynchronize(st));
     return added;
+}
+
+extern "C" int vox_hip_stream_set_async_encode(vox_hip_stream_t* s, int on) {
+    if (!s) return set_err("null stream");
+    if (s->enc_async && !on) CK(hipStreamSynchronize(s->st));
+    s->enc_async = on ? 1 : 0;
+    return 0;
 }
 
 extern "C" int vox_hip_stream_adapter_tokens(vox_hip_stream_t* s) { return s->total_adapter; }

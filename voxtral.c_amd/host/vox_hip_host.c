@@ -708,7 +708,11 @@ static int run_encoder(vh_stream_t *s) {
     if (new_mel <= 0) return 0;
     const double t0 = now_ms();
     const float *p = vox_hip_mel_frame_ptr(s->mel, s->mel_cursor);
-    if (!p || vox_hip_stream_encode_mel(s->st, p, new_mel, 1) < 0 || vox_hip_stream_sync(s->st))
+    /* a scheduled stream's chunk is only enqueued (vox_hip_stream_set_async_encode): the
+     * other streams' chunks of this tick overlap it, vh_sched_run's steps wait for it */
+    if (!p || vox_hip_stream_encode_mel(s->st, p, new_mel, 1) < 0 ||
+        ((!s->sched || (getenv("VOX_HIP_SCHED_ASYNC") && atoi(getenv("VOX_HIP_SCHED_ASYNC")) == 0)) &&
+         vox_hip_stream_sync(s->st)))
         return fail("encoder: %s", vox_hip_last_error());
     s->enc_ms += now_ms() - t0;
     s->conv_started = 1;
@@ -947,6 +951,10 @@ int vh_sched_attach(vh_sched_t *q, vh_stream_t *s) {
     if (s->sched == q) return 0;
     if (s->sched) return fail("vh_sched_attach: stream already attached to a scheduler");
     if (q->n == q->cap) return fail("vh_sched_attach: scheduler full (%d streams)", q->cap);
+    /* VOX_HIP_SCHED_ASYNC=0: each encoder chunk synchronises (the round-2 behaviour) */
+    const char *ae = getenv("VOX_HIP_SCHED_ASYNC");
+    if (vox_hip_stream_set_async_encode(s->st, !(ae && atoi(ae) == 0)))
+        return fail("async encode: %s", vox_hip_last_error());
     q->s[q->n++] = s;
     s->sched = q;
     return 0;
@@ -957,7 +965,7 @@ int vh_sched_detach(vh_sched_t *q, vh_stream_t *s) {
         if (q->s[i] == s) {
             q->s[i] = q->s[--q->n];
             s->sched = NULL;
-            return 0;
+            return vox_hip_stream_set_async_encode(s->st, 0) ? fail("async encode: %s", vox_hip_last_error()) : 0;
         }
     return fail("vh_sched_detach: stream not attached");
 }

@@ -46,7 +46,7 @@ EXPORTS = [
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
     "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
-    "vox_hip_stream_sync", "vox_hip_device_upload", "vox_hip_device_free",
+    "vox_hip_stream_sync", "vox_hip_stream_set_async_encode", "vox_hip_device_upload", "vox_hip_device_free",
     "vox_hip_mel_create", "vox_hip_mel_feed", "vox_hip_mel_finish", "vox_hip_mel_frames",
     "vox_hip_mel_frame_ptr", "vox_hip_mel_discard_before", "vox_hip_mel_read", "vox_hip_mel_free",
 ]
@@ -98,6 +98,7 @@ def lib():
         "vox_hip_stream_set_profiling": (I, [P, I]),
         "vox_hip_stream_profile": (I, [P, ctypes.POINTER(ctypes.c_double)]),
         "vox_hip_stream_sync": (I, [P]),
+        "vox_hip_stream_set_async_encode": (I, [P, I]),
         "vox_hip_device_upload": (P, [P, ctypes.c_size_t]),
         "vox_hip_device_free": (I, [P]),
         "vox_hip_mel_create": (P, [P, I]), "vox_hip_mel_feed": (I, [P, fp, I]),

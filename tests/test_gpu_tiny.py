@@ -52,6 +52,40 @@ def test_encode_chunks_match(models, tiny_cfg):
     os_.close()
 
 
+def test_async_encode_interleaved_streams(models, tiny_cfg):
+    """vox_hip_stream_set_async_encode as the scheduler uses it: three streams' ragged chunks
+    enqueued round-robin without a sync in between (several passes in flight on their own
+    queues), then each stream decoded; adapter rows and ids equal the oracle's per stream."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    rng = np.random.default_rng(11)
+    sizes = [[313, 50, 7, 1, 200], [300, 120, 33], [400, 2, 2, 90]]  # each past the 39-row prompt
+    hs = [vox_hip.Stream(hm) for _ in sizes]
+    os_ = [vox_oracle.OracleStream(om) for _ in sizes]
+    mels = [[rng.uniform(-0.6, 1.4, size=(n, tiny_cfg.mel_bins)).astype(np.float32) for n in sz] for sz in sizes]
+    for h in hs:
+        h.set_async_encode(True)
+    counts = [[], [], []]
+    for k in range(max(len(sz) for sz in sizes)):
+        for i in range(len(hs)):
+            if k < len(mels[i]):
+                counts[i].append(hs[i].encode_mel(mels[i][k]))
+    for i in range(len(hs)):
+        oc = [os_[i].encode_mel(m) for m in mels[i]]
+        assert counts[i] == oc, (i, counts[i], oc)
+        hs[i].sync()
+        ra = rel(hs[i].read_adapter(), os_[i].read_adapter())
+        assert ra < ADAPTER_TOL, (i, ra)
+        ht, hl = hs[i].decode(max_steps=12, stop_at_eos=False, want_logits=True)
+        ot, ol = os_[i].decode(max_steps=12, stop_at_eos=False, want_logits=True)
+        assert len(ot) > 0 and np.array_equal(ht, ot), (i, len(ot))
+        assert rel(hl, ol) < LOGIT_TOL, (i, rel(hl, ol))
+        hs[i].set_async_encode(False)
+        hs[i].close()
+        os_[i].close()
+
+
 def test_jfk_transcribe_tokens_match(models, jfk_samples):
     """vox_transcribe_audio schedule on jfk.wav (1355 / 140 / 1 mel-frame chunks)."""
     import vox_hip

@@ -212,6 +212,16 @@ class Stream:
             _err("encode_mel")
         return n
 
+    def set_async_encode(self, on: bool):
+        """encode_mel returns once the pass is enqueued (vox_hip_stream_set_async_encode);
+        host mel arrays must outlive the next sync()."""
+        if lib().vox_hip_stream_set_async_encode(self.h, int(on)) != 0:
+            _err("set_async_encode")
+
+    def sync(self):
+        if lib().vox_hip_stream_sync(self.h) != 0:
+            _err("sync")
+
     @property
     def adapter_tokens(self) -> int:
         return lib().vox_hip_stream_adapter_tokens(self.h)

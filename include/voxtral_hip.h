@@ -143,6 +143,15 @@ int vox_hip_stream_adapter_tokens(vox_hip_stream_t *s);
  * member stream, so a scheduler can have several streams' encoder chunks in flight at once.
  * Host mel pointers must stay valid until vox_hip_stream_sync.  Default 0 (synchronous). */
 int vox_hip_stream_set_async_encode(vox_hip_stream_t *s, int on);
+/* stream_run_encoder for B streams at once: each stream's conv stem on its own queue, the
+ * stacked new rows of all of them through the 32 encoder layers in one pass (projections
+ * over all rows: every weight byte read once for the batch; RoPE, K/V append and attention
+ * per stream against its own ring), then each stream's downsample + adapter.  The same
+ * results as B vox_hip_stream_encode_mel calls up to summation order.  added[b] = adapter
+ * rows appended to stream b.  Synchronous unless every stream is in async-encode mode.
+ * Returns 0, <0 on error. */
+int vox_hip_stream_encode_mel_batch(vox_hip_stream_t *const *streams, const float *const *mels,
+                                    const int *n_frames, int B, int mel_on_device, int *added);
 
 /* Incremental log-mel on the device: a vox_mel_ctx_t
  * (voxtral_audio.c:405-671) whose padded sample buffer and frames live in HBM, computed on

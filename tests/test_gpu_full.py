@@ -92,6 +92,33 @@ def test_full_night1968_5s_transcription(full):
     os_.close()
 
 
+def test_full_encode_mel_batch_streaming_chunks(full):
+    """The batched encoder pass at full size on the shape the scheduler feeds it: 6 streams,
+    a first chunk each, then -I 0.5-sized chunks (50 mel frames -> 25 encoder rows per
+    stream, 150 stacked rows per pass: the stream-K MFMA projections), one stream skipping a
+    round; adapter-row counts per stream exact, rows within TOL of each stream's oracle."""
+    import vox_hip
+    import vox_oracle
+    cfg, hm, om = full
+    rng = np.random.default_rng(23)
+    rounds = [[300, 260, 330, 300, 290, 310]] + [[50, 50, 50, 0 if k == 1 else 50, 50, 51] for k in range(4)]
+    hs = [vox_hip.Stream(hm) for _ in range(6)]
+    os_ = [vox_oracle.OracleStream(om) for _ in range(6)]
+    for r in rounds:
+        mels = [rng.uniform(-0.6, 1.4, size=(n, cfg.mel_bins)).astype(np.float32) for n in r]
+        got = vox_hip.encode_mel_batch(hs, mels)
+        want = [os_[i].encode_mel(mels[i]) if r[i] else 0 for i in range(6)]
+        assert got == want, (r, got, want)
+    worst = 0.0
+    for i in range(6):
+        ra = rel(hs[i].read_adapter(), os_[i].read_adapter())
+        worst = max(worst, ra)
+        assert ra < TOL, (i, ra)
+        hs[i].close()
+        os_[i].close()
+    print(f"batched encoder, 6 full-size streams: adapter rows worst rel err {worst:.2e}")
+
+
 def synth_audio(seconds, seed):
     """Speech-band synthetic audio (no recording offline; the path's work depends only on
     the length): noise bursts under a slow envelope plus drifting tones."""

@@ -86,6 +86,34 @@ def test_async_encode_interleaved_streams(models, tiny_cfg):
         os_[i].close()
 
 
+def test_encode_mel_batch_matches_oracle(models, tiny_cfg):
+    """vox_hip_stream_encode_mel_batch: three streams' ragged chunks (1-frame and odd chunks
+    included, one stream idle in some rounds) through shared encoder passes; every stream's
+    adapter-row counts and rows, then its greedy ids and logits, equal its own oracle session."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    rng = np.random.default_rng(17)
+    rounds = [[313, 300, 400], [50, 0, 2], [7, 120, 2], [1, 33, 90], [200, 1, 0]]
+    hs = [vox_hip.Stream(hm) for _ in range(3)]
+    os_ = [vox_oracle.OracleStream(om) for _ in range(3)]
+    for r in rounds:
+        mels = [rng.uniform(-0.6, 1.4, size=(n, tiny_cfg.mel_bins)).astype(np.float32) for n in r]
+        got = vox_hip.encode_mel_batch(hs, mels)
+        want = [os_[i].encode_mel(mels[i]) if r[i] else 0 for i in range(3)]
+        assert got == want, (r, got, want)
+    for i in range(3):
+        assert hs[i].adapter_tokens == os_[i].adapter_tokens
+        ra = rel(hs[i].read_adapter(), os_[i].read_adapter())
+        assert ra < ADAPTER_TOL, (i, ra)
+        ht, hl = hs[i].decode(max_steps=12, stop_at_eos=False, want_logits=True)
+        ot, ol = os_[i].decode(max_steps=12, stop_at_eos=False, want_logits=True)
+        assert len(ot) > 0 and np.array_equal(ht, ot), (i, len(ot))
+        assert rel(hl, ol) < LOGIT_TOL, (i, rel(hl, ol))
+        hs[i].close()
+        os_[i].close()
+
+
 def test_jfk_transcribe_tokens_match(models, jfk_samples):
     """vox_transcribe_audio schedule on jfk.wav (1355 / 140 / 1 mel-frame chunks)."""
     import vox_hip

@@ -503,6 +503,7 @@ struct vox_hip_stream {
     uint16_t* exp2;          // k_sklx: the second planes buffer (wo / w2 inputs)
     int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
     int enc_async;           // vox_hip_stream_encode_mel returns without a stream sync
+    float* xbatch;           // stacked encoder rows of a batched pass led by this stream
     float* essq;             // k_sklx row sums of squares per column slice [2][slices][16]
     uint16_t *gpa, *gpc;     // k_gemmf planes: norm / attention rows (K <= max(enc_dim, heads x hd)), gate rows
     int* gflags;             // k_gemmf partial-tile flags (gemmf_grid() ints)
@@ -655,7 +656,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
-    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2);
+    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch);
     dfree(s->gpa); dfree(s->gpc); dfree(s->gflags);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
@@ -1196,11 +1197,17 @@ static int ensure_rope(vox_hip_stream_t* s, long long last_pos) {
     return 0;
 }
 
-extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, int n, int mel_on_device) {
+// stream_run_encoder in three phases, so a batch of streams can share the layer passes
+// (vox_hip_stream_encode_mel_batch): (1) conv stem of n new mel frames on the stream's queue,
+// *T1 encoder rows left at *xin (-1 error); (2) the 32 layers over those rows; (3) 4x
+// downsample + adapter, returning the adapter rows added.
+static int enc_prefix(vox_hip_stream_t* s, const float* mel, int n, int mel_on_device, int* T1o, float** xino) {
     vox_hip_model_t* m = s->m;
     const vox_hip_config_t& c = m->c;
-    const int MB = c.mel_bins, ED = c.enc_dim, D = c.dec_dim;
+    const int MB = c.mel_bins, ED = c.enc_dim;
     hipStream_t st = s->st;
+    *T1o = 0;
+    *xino = nullptr;
     if (n <= 0) return 0;
     if (stream_alloc_frames(s, n + 4)) return -1;
     // ---- conv0 over [mel_tail(2) | new n] (voxtral.c:594-651) ----
@@ -1224,10 +1231,7 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
         CK(hipMemcpyAsync(s->c0_res, s->c0_p + (size_t)(2 + total - 1) * ED, (size_t)ED * 4,
                           hipMemcpyDeviceToDevice, st));
     s->res_count = new_res;
-    if (feed <= 0) {
-        if (!s->enc_async) CK(hipStreamSynchronize(st));
-        return 0;
-    }
+    if (feed <= 0) return 0;
     // ---- conv1 over [c0_tail(2) | feed], first output discarded (voxtral.c:694-756) ----
     const int T1 = feed / 2;
     float* xin = s->x_enc + (size_t)4 * ED;  // 4 spare rows in front for the downsample residual
@@ -1236,14 +1240,17 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
                    m->conv1_b, xin, ED, st, s->gws, s->gws_n));
     CK(hipMemcpyAsync(s->c0_tail, s->c0_p + (size_t)(2 + feed - 2) * ED, (size_t)2 * ED * 4,
                       hipMemcpyDeviceToDevice, st));
-    // ---- encoder (voxtral_encoder.c:495-693), sub-chunks through all layers ----
     if (ensure_rope(s, s->enc_pos + T1 + 1)) return -1;
-    for (int r0 = 0; r0 < T1; r0 += ENC_SUB) {
-        int nr = std::min(ENC_SUB, T1 - r0);
-        long long p0 = s->enc_pos + r0;
-        if (run_encoder_rows(s, xin + (size_t)r0 * ED, nr, p0, m->rope_enc + (size_t)p0 * c.enc_head_dim))
-            return -1;
-    }
+    *T1o = T1;
+    *xino = xin;
+    return 0;
+}
+
+static int enc_suffix(vox_hip_stream_t* s, float* xin, int T1) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, D = c.dec_dim;
+    hipStream_t st = s->st;
     s->enc_pos += T1;
     // ---- 4x downsample with residual + adapter (voxtral.c:868-934, encoder.c:699-737) ----
     const int R = s->enc_res_count;
@@ -1272,7 +1279,169 @@ extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, 
         CK(hipMemcpyAsync(s->enc_res + (size_t)R * ED, xin, (size_t)T1 * ED * 4, hipMemcpyDeviceToDevice, st));
     }
     s->enc_res_count = left;
-    if (!s->enc_async) CK(hipStreamSynchronize(st));
+    return added;
+}
+
+// The 32 encoder layers over the stacked new rows of several streams (row block b = rows
+// [off[b], off[b] + nr[b]) of X belongs to ss[b], at its logical positions from pos0[b]):
+// RMSNorm and the four projections run once over all rows (every weight byte read once for
+// the batch), RoPE + K/V append and the windowed attention per stream against its own ring.
+// Launched on lead->st with lead's scratch (ENC_SUB rows); the caller orders the streams.
+static int run_encoder_rows_batch(vox_hip_stream_t* lead, float* X, int N, vox_hip_stream_t* const* ss,
+                                  const int* off, const int* nr, const long long* pos0, int B) {
+    vox_hip_model_t* m = lead->m;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, H = c.enc_heads, KVH = c.enc_kv_heads, hd = c.enc_head_dim;
+    const int EQ = H * hd, EKV = KVH * hd, EH = c.enc_hidden, NQKV = EQ + 2 * EKV;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = lead->st;
+    const bool gf = enc_gemmf_ok(m, N);
+    if (gf) {
+        if (model_enc_frag(m)) return -1;
+        if (!lead->gpa) {
+            const size_t rb = PLANE_MAX_ROWS / SK_ROWS;
+            CK(dalloc(&lead->gpa, rb * 3 * SK_ROWS * std::max(ED, EQ)));
+            CK(dalloc(&lead->gpc, rb * 3 * SK_ROWS * EH));
+            CK(dalloc(&lead->gflags, (size_t)gemmf_grid()));
+        }
+    }
+    for (int l = 0; l < c.enc_layers; l++) {
+        const EncLayerD& L = m->enc[l];
+        if (gf) {
+            const DecFragD& F = m->efrag[l];
+            CK(launch_rmsnorm_fplanes(X, N, ED, L.attn_norm, nullptr, c.enc_eps, lead->gpa, nullptr, 0, st));
+            if (gemmf(lead, EPI_STORE, lead->gpa, ED, N, F.wqkv, NQKV, L.bqkv, lead->qkv, NQKV, nullptr)) return -1;
+        } else {
+            CK(launch_rmsnorm_rows(X, ED, lead->xn, ED, L.attn_norm, nullptr, N, ED, c.enc_eps, st));
+            CK(launch_gemm(EPI_STORE, 3, lead->xn, ED, L.wqkv, L.sqkv, ED, N, NQKV, L.bqkv, lead->qkv, NQKV, st,
+                           lead->gws, lead->gws_n));
+        }
+        for (int b = 0; b < B; b++) {
+            if (nr[b] <= 0) continue;
+            vox_hip_stream_t* sb = ss[b];
+            float* Kc = sb->ek + (size_t)l * sb->ecap * EKV;
+            float* Vc = sb->ev + (size_t)l * sb->ecap * EKV;
+            const float* rope = m->rope_enc + (size_t)pos0[b] * hd;
+            CK(launch_rope_kv(lead->qkv + (size_t)off[b] * NQKV, nr[b], EQ, EKV, hd, rope, (int)pos0[b],
+                              lead->q + (size_t)off[b] * EQ, Kc, Vc, sb->ecap, st));
+            CK(launch_attn_tiled(hd, lead->q + (size_t)off[b] * EQ, EQ, Kc, Vc, sb->ecap, lead->att + (size_t)off[b] * EQ,
+                                 EQ, nr[b], H, KVH, (int)pos0[b], 0, c.enc_window, scale, st, lead->gws, lead->gws_n));
+        }
+        if (gf) {
+            const DecFragD& F = m->efrag[l];
+            CK(launch_split_fplanes(lead->att, N, EQ, lead->gpa, st));
+            if (gemmf(lead, EPI_RESID, lead->gpa, EQ, N, F.wo, ED, L.bo, X, ED, nullptr)) return -1;
+            CK(launch_rmsnorm_fplanes(X, N, ED, L.ffn_norm, nullptr, c.enc_eps, lead->gpa, nullptr, 0, st));
+            if (gemmf(lead, EPI_SWIGLU, lead->gpa, ED, N, F.w13, 2 * EH, nullptr, nullptr, EH, lead->gpc)) return -1;
+            if (gemmf(lead, EPI_RESID, lead->gpc, EH, N, F.w2, ED, L.b2, X, ED, nullptr)) return -1;
+        } else {
+            CK(launch_gemm(EPI_RESID, 3, lead->att, EQ, L.wo, L.so, EQ, N, ED, L.bo, X, ED, st, lead->gws, lead->gws_n));
+            CK(launch_rmsnorm_rows(X, ED, lead->xn, ED, L.ffn_norm, nullptr, N, ED, c.enc_eps, st));
+            CK(launch_gemm(EPI_SWIGLU, 3, lead->xn, ED, L.w13, L.s13, ED, N, 2 * EH, nullptr, lead->gate, EH, st,
+                           lead->gws, lead->gws_n));
+            CK(launch_gemm(EPI_RESID, 3, lead->gate, EH, L.w2, L.s2, EH, N, ED, L.b2, X, ED, st, lead->gws, lead->gws_n));
+        }
+    }
+    CK(launch_rmsnorm_rows(X, ED, X, ED, m->enc_norm, nullptr, N, ED, c.enc_eps, st));
+    return 0;
+}
+
+// Several streams' new mel frames through one encoder pass (SURVEY 8f#1's batching applied
+// to the encoder): each stream's conv stem on its own queue, then the stacked rows through the
+// 32 layers once on ss[0]'s queue (weights read once for the batch), then each stream's
+// downsample + adapter on its own queue; HIP events order the queues.  Falls back to one
+// stream at a time when the stacked rows exceed one pass (ENC_SUB).  added[b] = adapter rows
+// appended to stream b.  Synchronous unless every stream is in async-encode mode.
+extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, const float* const* mels, const int* n,
+                                               int B, int mel_on_device, int* added) {
+    if (B < 1 || !ss || !mels || !n || !added) return set_err("encode_mel_batch: bad arguments");
+    for (int b = 0; b < B; b++)
+        if (!ss[b] || ss[b]->m != ss[0]->m) return set_err("encode_mel_batch: streams of one model");
+    vox_hip_stream_t* lead = ss[0];
+    const vox_hip_config_t& c = lead->m->c;
+    const int ED = c.enc_dim;
+    std::vector<int> T1(B), off(B);
+    std::vector<float*> xin(B);
+    std::vector<long long> pos0(B);
+    int N = 0;
+    for (int b = 0; b < B; b++) {
+        if (enc_prefix(ss[b], mels[b], n[b], mel_on_device, &T1[b], &xin[b])) return -1;
+        off[b] = N;
+        pos0[b] = ss[b]->enc_pos;
+        N += T1[b];
+    }
+    bool all_async = true;
+    for (int b = 0; b < B; b++) all_async = all_async && ss[b]->enc_async;
+    if (N > ENC_SUB || N == 0) {
+        // one stream at a time (rows beyond one pass, or nothing to encode)
+        for (int b = 0; b < B; b++) {
+            added[b] = 0;
+            if (T1[b] <= 0) continue;
+            for (int r0 = 0; r0 < T1[b]; r0 += ENC_SUB) {
+                const int nrr = std::min(ENC_SUB, T1[b] - r0);
+                const long long p0 = ss[b]->enc_pos + r0;
+                if (run_encoder_rows(ss[b], xin[b] + (size_t)r0 * ED, nrr, p0, lead->m->rope_enc + (size_t)p0 * c.enc_head_dim))
+                    return -1;
+            }
+            added[b] = enc_suffix(ss[b], xin[b], T1[b]);
+            if (added[b] < 0) return -1;
+        }
+    } else {
+        if (!lead->xbatch) CK(dalloc(&lead->xbatch, (size_t)ENC_SUB * ED));
+        // the lead's queue waits for every member's conv stem, stacks the rows, runs the layers
+        std::vector<hipEvent_t> ev(B);
+        for (int b = 0; b < B; b++) {
+            CK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
+            CK(hipEventRecord(ev[b], ss[b]->st));
+            if (b) CK(hipStreamWaitEvent(lead->st, ev[b], 0));
+        }
+        for (int b = 0; b < B; b++)
+            if (T1[b] > 0)
+                CK(hipMemcpyAsync(lead->xbatch + (size_t)off[b] * ED, xin[b], (size_t)T1[b] * ED * 4,
+                                  hipMemcpyDeviceToDevice, lead->st));
+        if (run_encoder_rows_batch(lead, lead->xbatch, N, ss, off.data(), T1.data(), pos0.data(), B)) return -1;
+        for (int b = 0; b < B; b++)
+            if (T1[b] > 0)
+                CK(hipMemcpyAsync(xin[b], lead->xbatch + (size_t)off[b] * ED, (size_t)T1[b] * ED * 4,
+                                  hipMemcpyDeviceToDevice, lead->st));
+        hipEvent_t done;
+        CK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        CK(hipEventRecord(done, lead->st));
+        for (int b = 0; b < B; b++) {
+            added[b] = 0;
+            if (b) CK(hipStreamWaitEvent(ss[b]->st, done, 0));
+            if (T1[b] > 0) {
+                added[b] = enc_suffix(ss[b], xin[b], T1[b]);
+                if (added[b] < 0) return -1;
+            }
+        }
+        for (int b = 0; b < B; b++) hipEventDestroy(ev[b]);
+        hipEventDestroy(done);
+    }
+    if (!all_async)
+        for (int b = 0; b < B; b++) CK(hipStreamSynchronize(ss[b]->st));
+    return 0;
+}
+
+extern "C" int vox_hip_stream_encode_mel(vox_hip_stream_t* s, const float* mel, int n, int mel_on_device) {
+    const vox_hip_config_t& c = s->m->c;
+    int T1 = 0;
+    float* xin = nullptr;
+    if (enc_prefix(s, mel, n, mel_on_device, &T1, &xin)) return -1;
+    int added = 0;
+    if (T1 > 0) {
+        // ---- encoder (voxtral_encoder.c:495-693), sub-chunks through all layers ----
+        for (int r0 = 0; r0 < T1; r0 += ENC_SUB) {
+            int nr = std::min(ENC_SUB, T1 - r0);
+            long long p0 = s->enc_pos + r0;
+            if (run_encoder_rows(s, xin + (size_t)r0 * c.enc_dim, nr, p0,
+                                 s->m->rope_enc + (size_t)p0 * c.enc_head_dim))
+                return -1;
+        }
+        added = enc_suffix(s, xin, T1);
+        if (added < 0) return -1;
+    }
+    if (!s->enc_async) CK(hipStreamSynchronize(s->st));
     return added;
 }
 

@@ -46,7 +46,7 @@ EXPORTS = [
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
     "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
-    "vox_hip_stream_sync", "vox_hip_stream_set_async_encode", "vox_hip_device_upload", "vox_hip_device_free",
+    "vox_hip_stream_sync", "vox_hip_stream_set_async_encode", "vox_hip_stream_encode_mel_batch", "vox_hip_device_upload", "vox_hip_device_free",
     "vox_hip_mel_create", "vox_hip_mel_feed", "vox_hip_mel_finish", "vox_hip_mel_frames",
     "vox_hip_mel_frame_ptr", "vox_hip_mel_discard_before", "vox_hip_mel_read", "vox_hip_mel_free",
 ]
@@ -99,6 +99,7 @@ def lib():
         "vox_hip_stream_profile": (I, [P, ctypes.POINTER(ctypes.c_double)]),
         "vox_hip_stream_sync": (I, [P]),
         "vox_hip_stream_set_async_encode": (I, [P, I]),
+        "vox_hip_stream_encode_mel_batch": (I, [P, P, P, I, I, P]),
         "vox_hip_device_upload": (P, [P, ctypes.c_size_t]),
         "vox_hip_device_free": (I, [P]),
         "vox_hip_mel_create": (P, [P, I]), "vox_hip_mel_feed": (I, [P, fp, I]),
@@ -178,6 +179,20 @@ class Model:
         if self.h:
             lib().vox_hip_model_free(self.h)
             self.h = None
+
+
+def encode_mel_batch(streams, mels):
+    """vox_hip_stream_encode_mel_batch: each stream's new host mel frames, one encoder pass
+    over all of their rows; returns the adapter rows added per stream."""
+    n = len(streams)
+    arrs = [np.ascontiguousarray(m, dtype=np.float32) for m in mels]
+    hs = (ctypes.c_void_p * n)(*[s.h for s in streams])
+    ps = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    ns = np.array([a.shape[0] for a in arrs], np.int32)
+    added = np.zeros(n, np.int32)
+    if lib().vox_hip_stream_encode_mel_batch(hs, ps, ns.ctypes.data, n, 0, added.ctypes.data) != 0:
+        _err("encode_mel_batch")
+    return added.tolist()
 
 
 class Stream:

@@ -92,6 +92,9 @@ vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int d
  * once per token per stream.  A scheduler owns up to VH_SCHED_MAX streams of one model on
  * one GPU; attached streams run their mel front-end and encoder in vh_stream_feed / flush /
  * finish as audio arrives, and leave the decoder to vh_sched_run, which
+ *   0. encodes the chunk every attached stream deferred since the last run (its feeds leave
+ *      the chunk's frames in place) in one vox_hip_stream_encode_mel_batch pass: the encoder
+ *      weights are read once for all streams (VOX_HIP_SCHED_BATCH_ENC=0: each chunk alone),
  *   1. runs the prefill + first token of every stream whose prompt rows are complete,
  *   2. advances every running stream by batched greedy steps (vox_hip_batch_decode: one
  *      weight read per step for all of them, attention / KV / argmax per stream) until each
@@ -109,6 +112,7 @@ typedef struct {
     int runs, prefills, batch_calls;
     long long tokens;        /* ids from batched steps */
     double run_ms, batch_ms; /* wall time in vh_sched_run / in vox_hip_batch_decode */
+    int enc_batches;         /* batched encoder passes (step 0) */
 } vh_sched_stats_t;
 vh_sched_t *vh_sched_create(vh_ctx_t *ctx, int max_streams);
 void vh_sched_free(vh_sched_t *q);          /* detaches its streams */

@@ -1316,17 +1316,20 @@ static int run_encoder_rows_batch(vox_hip_stream_t* lead, float* X, int N, vox_h
             CK(launch_gemm(EPI_STORE, 3, lead->xn, ED, L.wqkv, L.sqkv, ED, N, NQKV, L.bqkv, lead->qkv, NQKV, st,
                            lead->gws, lead->gws_n));
         }
+        // every stream's RoPE + K/V append and attention in one launch each (row offsets)
+        EncRows er;
+        memset(&er, 0, sizeof er);
+        er.B = B;
         for (int b = 0; b < B; b++) {
-            if (nr[b] <= 0) continue;
-            vox_hip_stream_t* sb = ss[b];
-            float* Kc = sb->ek + (size_t)l * sb->ecap * EKV;
-            float* Vc = sb->ev + (size_t)l * sb->ecap * EKV;
-            const float* rope = m->rope_enc + (size_t)pos0[b] * hd;
-            CK(launch_rope_kv(lead->qkv + (size_t)off[b] * NQKV, nr[b], EQ, EKV, hd, rope, (int)pos0[b],
-                              lead->q + (size_t)off[b] * EQ, Kc, Vc, sb->ecap, st));
-            CK(launch_attn_tiled(hd, lead->q + (size_t)off[b] * EQ, EQ, Kc, Vc, sb->ecap, lead->att + (size_t)off[b] * EQ,
-                                 EQ, nr[b], H, KVH, (int)pos0[b], 0, c.enc_window, scale, st, lead->gws, lead->gws_n));
+            er.off[b] = off[b];
+            er.nr[b] = nr[b];
+            er.pos0[b] = (int)pos0[b];
+            er.Kc[b] = ss[b]->ek + (size_t)l * ss[b]->ecap * EKV;
+            er.Vc[b] = ss[b]->ev + (size_t)l * ss[b]->ecap * EKV;
         }
+        CK(launch_rope_kv_rows(lead->qkv, N, EQ, EKV, hd, m->rope_enc, er, lead->q, lead->ecap, st));
+        CK(launch_attn_rows(hd, lead->q, er, N, lead->ecap, lead->att, H, KVH, c.enc_window, scale, lead->gws,
+                            lead->gws_n, st));
         if (gf) {
             const DecFragD& F = m->efrag[l];
             CK(launch_split_fplanes(lead->att, N, EQ, lead->gpa, st));
@@ -1355,8 +1358,10 @@ static int run_encoder_rows_batch(vox_hip_stream_t* lead, float* X, int N, vox_h
 extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, const float* const* mels, const int* n,
                                                int B, int mel_on_device, int* added) {
     if (B < 1 || !ss || !mels || !n || !added) return set_err("encode_mel_batch: bad arguments");
+    if (B > VOX_MAX_BATCH) return set_err("encode_mel_batch: at most %d streams", VOX_MAX_BATCH);
     for (int b = 0; b < B; b++)
-        if (!ss[b] || ss[b]->m != ss[0]->m) return set_err("encode_mel_batch: streams of one model");
+        if (!ss[b] || ss[b]->m != ss[0]->m || ss[b]->ecap != ss[0]->ecap)
+            return set_err("encode_mel_batch: streams of one model");
     vox_hip_stream_t* lead = ss[0];
     const vox_hip_config_t& c = lead->m->c;
     const int ED = c.enc_dim;

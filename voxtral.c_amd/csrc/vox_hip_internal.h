@@ -116,6 +116,21 @@ constexpr int ATT_BLOCK_KEYS = 256;  // keys one decode-attention block covers
 hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window,
                                    float scale, int H, int KVH, int splits, hipStream_t st, int kv16 = 0);
 
+// a batched encoder pass: rows [off[b], off[b] + nr[b]) of the stacked rows belong to stream
+// b, at logical positions pos0[b] + i, with its own K/V ring (layer base)
+struct EncRows {
+    int B;
+    int off[VOX_MAX_BATCH], nr[VOX_MAX_BATCH], pos0[VOX_MAX_BATCH];
+    float* Kc[VOX_MAX_BATCH];
+    float* Vc[VOX_MAX_BATCH];
+};
+// RoPE + K/V append of every stacked row into its stream's ring (k_rope_kv per row block)
+hipError_t launch_rope_kv_rows(const float* qkv, int N, int qd, int kvd, int hd, const float* rope_table,
+                               const EncRows& er, float* q, int cap, hipStream_t st);
+// windowed attention of every stream's rows against its own ring, one launch (+ one combine):
+// Q / O stacked [N, H*hd]
+hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, int cap, float* O, int H, int KVH,
+                            int window, float scale, float* ws, size_t ws_elems, hipStream_t st);
 constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st);

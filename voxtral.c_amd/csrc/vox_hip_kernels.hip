@@ -537,6 +537,37 @@ __global__ __launch_bounds__(256) void k_rope_kv(const float* __restrict__ qkv, 
     for (int p = threadIdx.x; p < kvd / 2; p += 256) kv_st2(vr + 2 * p, row[qd + kvd + 2 * p], row[qd + kvd + 2 * p + 1]);
 }
 
+// k_rope_kv over the stacked rows of a batched encoder pass: block = one row, its stream found
+// from the row offsets (same operations per row as k_rope_kv)
+__global__ __launch_bounds__(256) void k_rope_kv_rows(const float* __restrict__ qkv, int qd, int kvd, int hd,
+                                                      const float* __restrict__ rope_table, const EncRows er,
+                                                      float* __restrict__ q, int cap) {
+    const int row = blockIdx.x;
+    int b = 0;
+    while (b + 1 < er.B && row >= er.off[b + 1]) b++;
+    const int i = row - er.off[b];
+    const int ld = qd + 2 * kvd;
+    const float* xr = qkv + (size_t)row * ld;
+    const float* rp = rope_table + (size_t)(er.pos0[b] + i) * hd;
+    const int slot = (er.pos0[b] + i) % cap;
+    float* kr = er.Kc[b] + (size_t)slot * kvd;
+    float* vr = er.Vc[b] + (size_t)slot * kvd;
+    for (int p = threadIdx.x; p < qd / 2; p += 256) {
+        int d = (2 * p) % hd / 2;
+        float c = rp[2 * d], sn = rp[2 * d + 1];
+        float x0 = xr[2 * p], x1 = xr[2 * p + 1];
+        q[(size_t)row * qd + 2 * p] = x0 * c - x1 * sn;
+        q[(size_t)row * qd + 2 * p + 1] = x0 * sn + x1 * c;
+    }
+    for (int p = threadIdx.x; p < kvd / 2; p += 256) {
+        int d = (2 * p) % hd / 2;
+        float c = rp[2 * d], sn = rp[2 * d + 1];
+        float x0 = xr[qd + 2 * p], x1 = xr[qd + 2 * p + 1];
+        kv_st2(kr + 2 * p, x0 * c - x1 * sn, x0 * sn + x1 * c);
+    }
+    for (int p = threadIdx.x; p < kvd / 2; p += 256) kv_st2(vr + 2 * p, xr[qd + kvd + 2 * p], xr[qd + kvd + 2 * p + 1]);
+}
+
 // ============================================================================
 // Tiled causal/windowed attention for M>1 queries (encoder chunks, decoder prefill).
 // Semantics of vox_causal_attention (voxtral_kernels.c:541-611) with logical positions:
@@ -697,23 +728,38 @@ __global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q,
 // computes.  The four waves' (o, m, l) meet in LDS at the end.  The VALU kernel staged K / V
 // tiles in LDS and was bound by their reads (160 ds_read_b128 per thread per 64-key tile).
 // ============================================================================
-template <int HD, class KT = float>
+// BAT: a batched encoder pass -- blockIdx.z = stream * ns + key split; Q / O / the partials'
+// rows are the stacked rows (stream b's from er.off[b], M = the stacked total), Kc / Vc /
+// q_pos0 / the stream's row count come from er.
+template <int HD, class KT = float, int BAT = 0>
 __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, int ldq, const float* __restrict__ Kc,
                                                  const float* __restrict__ Vc, int cap, float* __restrict__ O,
                                                  int ldo, int M, int H, int KVH, int q_pos0, int k_first, int window,
-                                                 float scale, int ns, float* __restrict__ part) {
+                                                 float scale, int ns, float* __restrict__ part,
+                                                 const EncRows er = EncRows{}) {
     constexpr int DG = HD / 4;   // S^T: dims per lane group
     constexpr int NB = HD / 16;  // P V: output dims per lane (d = NB j + b)
     __shared__ float sm[4][16], sl[4][16];
     __shared__ __attribute__((aligned(16))) float so[4][16][HD + 4];
+    const int zsplit = BAT ? (int)blockIdx.z % ns : (int)blockIdx.z;
+    int rbase = 0, Mr = M;  // first stacked row of this stream, its row count
+    if (BAT) {
+        const int zb = (int)blockIdx.z / ns;
+        rbase = er.off[zb];
+        Mr = er.nr[zb];
+        q_pos0 = er.pos0[zb];
+        Kc = er.Kc[zb];
+        Vc = er.Vc[zb];
+        if ((int)blockIdx.y * 16 >= Mr) return;  // uniform per block
+    }
     const int h = blockIdx.x, q0 = blockIdx.y * 16;
     const int kvh = h / (H / KVH), kvd = KVH * HD;
-    const int nq = min(16, M - q0);
+    const int nq = min(16, Mr - q0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = lane & 15, g = lane >> 4;
     float qv[DG];
     {
-        const float* qr = Q + (size_t)(q0 + j) * ldq + h * HD + g * DG;
+        const float* qr = Q + (size_t)(rbase + q0 + j) * ldq + h * HD + g * DG;
 #pragma unroll
         for (int t = 0; t < DG; t += 4) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -726,7 +772,7 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
     int kend = qlast;
     if (ns > 1) {
         const int span = ((kend - kstart + 1 + ns - 1) / ns + 15) / 16 * 16;
-        kstart += blockIdx.z * span;
+        kstart += zsplit * span;
         kend = min(kend, kstart + span - 1);
     }
     const int qp = q_pos0 + q0 + j;  // the query of this lane's S^T column
@@ -838,7 +884,7 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
         for (int w = 0; w < 4; w++) num[e] = fmaf(f[w], so[w][r][d0 + e], num[e]);
     }
     if (ns > 1) {
-        float* pp = part + ((size_t)(h * M + q0 + r) * ns + blockIdx.z) * (HD + 2);
+        float* pp = part + ((size_t)(h * M + rbase + q0 + r) * ns + zsplit) * (HD + 2);
 #pragma unroll
         for (int e = 0; e < NB; e++) pp[d0 + e] = num[e];
         if ((tid & 15) == 0) {
@@ -847,7 +893,7 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
         }
     } else {
         const float inv = den > 0.f ? 1.0f / den : 0.f;
-        float* op = O + (size_t)(q0 + r) * ldo + h * HD + d0;
+        float* op = O + (size_t)(rbase + q0 + r) * ldo + h * HD + d0;
 #pragma unroll
         for (int e = 0; e < NB; e++) op[e] = num[e] * inv;
     }
@@ -3134,6 +3180,52 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
 int g_attn_qt = 0;    // tools/kbench knob: queries per k_attn_tiled block (16 or 32; 0 = automatic)
 int g_attn_valu = 0;  // tools/kbench knob: 1 = the VALU k_attn_tiled instead of k_attn_mf
 int g_attn_blocks = 0;  // tools/kbench knob: target grid size of the key-range split (0 = 512)
+
+hipError_t launch_rope_kv_rows(const float* qkv, int N, int qd, int kvd, int hd, const float* rope_table,
+                               const EncRows& er, float* q, int cap, hipStream_t st) {
+    if (N <= 0) return hipSuccess;
+    if (er.B < 1 || er.B > VOX_MAX_BATCH) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_rope_kv_rows, dim3(N), dim3(256), 0, st, qkv, qd, kvd, hd, rope_table, er, q, cap);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, int cap, float* O, int H, int KVH,
+                            int window, float scale, float* ws, size_t ws_elems, hipStream_t st) {
+    if (N <= 0) return hipSuccess;
+    if (er.B < 1 || er.B > VOX_MAX_BATCH || (hd != 64 && hd != 128)) return hipErrorInvalidValue;
+    int qbm = 0, keys = 0;
+    for (int b = 0; b < er.B; b++) {
+        qbm = std::max(qbm, (er.nr[b] + 15) / 16);
+        const int ks = std::max(er.pos0[b] - window + 1, 0);
+        keys = std::max(keys, er.pos0[b] + er.nr[b] - ks);
+    }
+    if (qbm == 0) return hipSuccess;
+    // key splits as launch_attn_tiled picks them, over every stream's (head, query block)s
+    int ns = 1;
+    int nblk = 0;
+    for (int b = 0; b < er.B; b++) nblk += H * ((er.nr[b] + 15) / 16);
+    if (ws && nblk < 256) {
+        ns = std::min((keys + 63) / 64, std::max(1, 256 / nblk));
+        while (ns > 1 && (size_t)H * N * ns * (hd + 2) > ws_elems) ns--;
+    }
+    dim3 grid(H, qbm, ns * er.B);
+    if (hd == 64)
+        hipLaunchKernelGGL((k_attn_mf<64, float, 1>), grid, dim3(256), 0, st, Q, H * hd, nullptr, nullptr, cap, O, H * hd,
+                           N, H, KVH, 0, 0, window, scale, ns, ws, er);
+    else
+        hipLaunchKernelGGL((k_attn_mf<128, float, 1>), grid, dim3(256), 0, st, Q, H * hd, nullptr, nullptr, cap, O,
+                           H * hd, N, H, KVH, 0, 0, window, scale, ns, ws, er);
+    LAUNCH_CHECK();
+    if (ns > 1) {
+        if (hd == 64)
+            hipLaunchKernelGGL(k_attn_tiled_combine<64>, dim3(H, N), dim3(64), 0, st, ws, ns, N, O, H * hd, nullptr);
+        else
+            hipLaunchKernelGGL(k_attn_tiled_combine<128>, dim3(H, N), dim3(128), 0, st, ws, ns, N, O, H * hd, nullptr);
+        LAUNCH_CHECK();
+    }
+    return hipSuccess;
+}
 
 hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,

@@ -604,6 +604,7 @@ struct vh_stream {
     int *dec_buf, *alt_buf;
     int generated, chunks, started_decoding;
     int continuous, n_alt;
+    int pend_first, pend_n;     /* scheduled stream: a chunk waiting for vh_sched_run's batched encoder pass */
     float alt_cutoff;
     int nontext_streak, text_since_restart, empty_restarts, restarts, full_resets;
     double enc_ms, dec_ms, prefill_ms;
@@ -695,6 +696,29 @@ static void queue_push(vh_stream_t *s, const int *recs, int n) {
     }
 }
 
+/* the chunk a scheduled stream deferred, encoded alone (before its own decode, before a
+ * second chunk, on detach) */
+static int flush_pending(vh_stream_t *s) {
+    if (s->pend_n <= 0) return 0;
+    const double t0 = now_ms();
+    const float *p = vox_hip_mel_frame_ptr(s->mel, s->pend_first);
+    if (!p || vox_hip_stream_encode_mel(s->st, p, s->pend_n, 1) < 0) return fail("encoder: %s", vox_hip_last_error());
+    s->enc_ms += now_ms() - t0;
+    s->pend_n = 0;
+    s->chunks++;
+    return vox_hip_mel_discard_before(s->mel, s->mel_cursor);
+}
+
+static int sched_batch_encode(void) {
+    /* VOX_HIP_SCHED_BATCH_ENC=0: every scheduled chunk is encoded on its own */
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("VOX_HIP_SCHED_BATCH_ENC");
+        v = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return v;
+}
+
 /* stream_run_encoder (voxtral.c:827-851) */
 static int run_encoder(vh_stream_t *s) {
     int off = 0;
@@ -706,6 +730,16 @@ static int run_encoder(vh_stream_t *s) {
     const int need = s->conv_started ? s->min_new_mel : STREAM_FIRST_CHUNK_MIN_MEL;
     if (new_mel < need && !s->finished) return 0;
     if (new_mel <= 0) return 0;
+    if (s->sched && sched_batch_encode()) {
+        /* the chunk (same frame range as on the single-stream path) waits for vh_sched_run,
+         * which encodes every attached stream's chunk in one batched pass */
+        if (flush_pending(s)) return -1;
+        s->pend_first = s->mel_cursor;
+        s->pend_n = new_mel;
+        s->conv_started = 1;
+        s->mel_cursor = total;
+        return 0;
+    }
     const double t0 = now_ms();
     const float *p = vox_hip_mel_frame_ptr(s->mel, s->mel_cursor);
     /* a scheduled stream's chunk is only enqueued (vox_hip_stream_set_async_encode): the
@@ -816,6 +850,7 @@ static int decoder_ready(vh_stream_t *s) {
  * streak or 20 s of audio without a decoded token, escalating to a full reset
  * (voxtral.c:1189-1239). */
 static int run_decoder(vh_stream_t *s) {
+    if (flush_pending(s)) return -1;
     if (!decoder_ready(s)) return 0;  /* waiting for the prompt */
     int eos = 0;
     for (;;) {
@@ -963,6 +998,7 @@ int vh_sched_attach(vh_sched_t *q, vh_stream_t *s) {
 int vh_sched_detach(vh_sched_t *q, vh_stream_t *s) {
     for (int i = 0; i < q->n; i++)
         if (q->s[i] == s) {
+            if (flush_pending(s)) return -1;
             q->s[i] = q->s[--q->n];
             s->sched = NULL;
             return vox_hip_stream_set_async_encode(s->st, 0) ? fail("async encode: %s", vox_hip_last_error()) : 0;
@@ -976,6 +1012,36 @@ int vh_sched_run(vh_sched_t *q) {
     const double t_run = now_ms();
     int total = 0;
     int eos[VH_SCHED_MAX] = {0}, ran[VH_SCHED_MAX] = {0};
+    /* 0. every attached stream's deferred chunk through one batched encoder pass (the layers'
+     *    weights read once for all of them) */
+    {
+        vox_hip_stream_t *hs[VH_SCHED_MAX];
+        const float *mp[VH_SCHED_MAX];
+        int nf[VH_SCHED_MAX], added[VH_SCHED_MAX], idx[VH_SCHED_MAX], nb = 0;
+        for (int i = 0; i < q->n; i++) {
+            vh_stream_t *s = q->s[i];
+            if (s->pend_n <= 0) continue;
+            mp[nb] = vox_hip_mel_frame_ptr(s->mel, s->pend_first);
+            if (!mp[nb]) return fail("vox_hip_mel_frame_ptr failed");
+            hs[nb] = s->st;
+            nf[nb] = s->pend_n;
+            idx[nb++] = i;
+        }
+        if (nb) {
+            const double t0 = now_ms();
+            if (vox_hip_stream_encode_mel_batch(hs, mp, nf, nb, 1, added) < 0)
+                return fail("batched encoder: %s", vox_hip_last_error());
+            const double dt = now_ms() - t0;
+            q->stats.enc_batches++;
+            for (int k = 0; k < nb; k++) {
+                vh_stream_t *s = q->s[idx[k]];
+                s->enc_ms += dt / nb;
+                s->pend_n = 0;
+                s->chunks++;
+                if (vox_hip_mel_discard_before(s->mel, s->mel_cursor)) return -1;
+            }
+        }
+    }
     /* 1. streams whose decoder is not running yet: prefill + first token alone (the
      *    reference's prefill_ms); streams with --alt keep the single-stream path, whose steps
      *    record the candidates (the batched step keeps none) */

@@ -613,7 +613,8 @@ _host = None
 
 class SchedStats(ctypes.Structure):
     _fields_ = [("runs", ctypes.c_int), ("prefills", ctypes.c_int), ("batch_calls", ctypes.c_int),
-                ("tokens", ctypes.c_longlong), ("run_ms", ctypes.c_double), ("batch_ms", ctypes.c_double)]
+                ("tokens", ctypes.c_longlong), ("run_ms", ctypes.c_double), ("batch_ms", ctypes.c_double),
+                ("enc_batches", ctypes.c_int)]
 
 
 def host_lib():

@@ -1376,9 +1376,14 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
         N += T1[b];
     }
     bool all_async = true;
-    for (int b = 0; b < B; b++) all_async = all_async && ss[b]->enc_async;
-    if (N > ENC_SUB || N == 0) {
-        // one stream at a time (rows beyond one pass, or nothing to encode)
+    int active = 0;
+    for (int b = 0; b < B; b++) {
+        all_async = all_async && ss[b]->enc_async;
+        active += T1[b] > 0;
+    }
+    if (N > ENC_SUB || active <= 1) {
+        // one stream at a time: rows beyond one pass, or a single stream with rows (its own
+        // path keeps the skinny fused kernels for a short chunk)
         for (int b = 0; b < B; b++) {
             added[b] = 0;
             if (T1[b] <= 0) continue;

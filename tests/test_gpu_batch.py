@@ -155,16 +155,18 @@ def _oracle_tokens_parallel(om, mels, chunks):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("nstreams", [8, 16])
-def test_batch_full_size_streams_each_vs_oracle(nstreams):
-    """Full Voxtral-4B shapes: config 4's per-GPU load (8 streams) and the 16-stream bench
-    line's, jfk-shaped streams (1355 / 140 / 1 mel-frame chunks, 149 tokens each, different
+def test_batch_full_size_streams_each_vs_oracle():
+    """Full Voxtral-4B shapes at the 16-stream bench line's load (config 4's 8 streams per GPU
+    run the same kernels: below 256 (stream, kv head) blocks the attention takes the same
+    path): 16 streams of 7 s one-shot schedules (700 / 70 / 1 mel-frame chunks, different
     audio) decoded as one batch; EVERY stream's ids equal the CPU oracle's for that stream and
-    the final batched step's logits are within LOGIT_TOL."""
+    the final batched step's logits are within LOGIT_TOL.  (A full jfk length per stream
+    doubled the oracle's share of the GPU suite's wall time.)"""
     import vox_hip
     import vox_oracle
     from vox_weights import VOXTRAL_4B, synth_weights
-    chunks = [1355, 140, 1]
+    nstreams = 16
+    chunks = [700, 70, 1]
     w = synth_weights(VOXTRAL_4B, seed=0)
     hm = vox_hip.Model(VOXTRAL_4B, w)
     mels = _mels(VOXTRAL_4B, [sum(chunks)] * nstreams, 42)
@@ -185,9 +187,11 @@ def test_batch_full_size_streams_each_vs_oracle(nstreams):
     refs, ref_last = _oracle_tokens_parallel(om, mels, chunks)
     om.close()
     worst = 0.0
+    nt = len(refs[0])
+    assert nt > 40
     for i in range(nstreams):
-        assert len(refs[i]) == 149
-        assert got[i] == refs[i], (i, next(k for k in range(149) if got[i][k] != refs[i][k]))
+        assert len(refs[i]) == nt
+        assert got[i] == refs[i], (i, next(k for k in range(nt) if got[i][k] != refs[i][k]))
         r = rel(last[i], ref_last[i])
         worst = max(worst, r)
         assert r < LOGIT_TOL, (i, r)

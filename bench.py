@@ -402,6 +402,8 @@ def main():
         "encoder_rtf": round(enc_s / (AUDIO_SECONDS * args.steps), 5),
         "encoder_dtype": encoder_dtype(),
         "encoder_rtf_exact_3plane": round(enc_exact, 5) if enc_exact is not None else None,
+        # k_gemmf stream-K tiles whose owner recomputed a part (the hand-off wait timed out)
+        "encoder_gemm_recomputes": prof.get("gemmf_recomputes"),
         "prefill_ms": round(prefill_s * 1000.0 / args.steps, 3),
         "decoder_ms_per_token": round(dec_s * 1000.0 / max(1, steps_local), 4),
         "roofline": {"bound": "hbm", "kernel": "k_gemv<PRO_NORM_ADA,EPI_SWIGLU> (W1|W3)",
@@ -751,6 +753,8 @@ def bench_serve(args, d, cfg, model, st0):
     lat = np.array([x for r in runs for x in r["lat"]]) * 1000.0
     batch_tok = st["tokens"] - q_stats0["tokens"]
     batch_ms = st["batch_ms"] - q_stats0["batch_ms"]
+    batch_steps = st["steps"] - q_stats0["steps"]
+    ticks = sum(r["ticks"] for r in runs)
     out = {
         "metric": "decoder tokens/sec + encoder RTF, Voxtral-4B " + ("q8" if args.q8 else "bf16")
                   + f", {S} streams per MI355X served by the per-GPU scheduler (config 4), at 1/2/4/8 MI355X",
@@ -772,7 +776,13 @@ def bench_serve(args, d, cfg, model, st0):
         "overall_rtf_per_stream": round(wall / (audio_all / d.world / S), 5),
         "clips": sum(r["clips"] for r in runs),
         "batched_decode": {"ids": batch_tok, "ms": round(batch_ms, 1),
-                           "ids_per_s": round(batch_tok / max(1e-9, batch_ms * 1e-3), 1)},
+                           "ids_per_s": round(batch_tok / max(1e-9, batch_ms * 1e-3), 1),
+                           "steps": batch_steps, "rows_per_step": round(batch_tok / max(1, batch_steps), 2),
+                           "graph_captures": st["captures"] - q_stats0["captures"],
+                           "graph_captures_per_tick": round((st["captures"] - q_stats0["captures"]) / max(1, ticks), 4),
+                           "prefill_passes": st["prefill_passes"] - q_stats0["prefill_passes"],
+                           "prefilled_streams": st["prefills"] - q_stats0["prefills"],
+                           "ticks": ticks},
     }
     if d.rank == 0:
         print(json.dumps(out), flush=True)

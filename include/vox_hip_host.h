@@ -95,16 +95,17 @@ vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int d
  *   0. encodes the chunk every attached stream deferred since the last run (its feeds leave
  *      the chunk's frames in place) in one vox_hip_stream_encode_mel_batch pass: the encoder
  *      weights are read once for all streams (VOX_HIP_SCHED_BATCH_ENC=0: each chunk alone),
- *   1. runs the prefill + first token of every stream whose prompt rows are complete,
- *   2. advances every running stream by batched greedy steps (vox_hip_batch_decode: one
- *      weight read per step for all of them, attention / KV / argmax per stream) until each
- *      has used its adapter rows or produced EOS,
+ *   1-2. advances every stream whose decoder can run by batched greedy steps
+ *      (vox_hip_batch_decode: one weight read per step for all of them, attention / KV /
+ *      argmax per stream): streams whose prompt rows just completed are prefilled together
+ *      in one stacked pass and take their first token in the batched steps, and every stream
+ *      stops on the device when it has used its adapter rows or produced EOS,
  *   3. applies each stream's live-mode restarts (vh_stream_set_continuous) as run after its
  *      own drain.
  * Called after every round of feeds, it yields per stream the ids vh_stream_feed would have
- * queued (vh_stream_get / get_alt read them as before).  Streams with --alt (n_alt > 1) keep
- * the single-stream decode, whose steps record the candidates; a live-mode stream drains on
- * its own path inside vh_stream_flush (and so inside vh_stream_finish), where the reference's
+ * queued (vh_stream_get / get_alt read them as before).  Streams with --alt (n_alt > 1) stay
+ * in the batch (the batched argmax keeps their candidates); a live-mode stream drains on its
+ * own path inside vh_stream_flush (and so inside vh_stream_finish), where the reference's
  * restart checks run between the flush and the final chunk. */
 #define VH_SCHED_MAX 16
 typedef struct vh_sched vh_sched_t;
@@ -113,6 +114,9 @@ typedef struct {
     long long tokens;        /* ids from batched steps */
     double run_ms, batch_ms; /* wall time in vh_sched_run / in vox_hip_batch_decode */
     int enc_batches;         /* batched encoder passes (step 0) */
+    long long steps;         /* batched step replays (tokens / steps = rows per step) */
+    long long captures;      /* step-graph captures (vox_hip_batch_stats) */
+    long long prefill_passes;/* prefill passes (several new streams share one) */
 } vh_sched_stats_t;
 vh_sched_t *vh_sched_create(vh_ctx_t *ctx, int max_streams);
 void vh_sched_free(vh_sched_t *q);          /* detaches its streams */

@@ -114,6 +114,11 @@ int vox_hip_model_set_kv_fp16(vox_hip_model_t *m, int on);
  * Process-wide; returns 0, or -1 for another value. */
 int vox_hip_set_gemm_planes(int planes);
 int vox_hip_gemm_planes(void);
+/* Diagnostic (no reference counterpart): the encoder GEMM's stream-K owner waits up to
+ * `ticks` (100 MHz) for each later part of a tile before computing that stage range itself
+ * (same code and order: same bits); ticks < 0 never waits, so the tests can force that
+ * backstop.  Default 5000 (50 us).  Process-wide; returns the previous value. */
+int vox_hip_set_gemmf_wait(int ticks);
 
 /* Per-stream device state: encoder/decoder rolling KV, conv-stem tails, adapter buffer,
  * scratch and a HIP stream.  One model serves many streams. */
@@ -201,8 +206,13 @@ int vox_hip_stream_read_alts(vox_hip_stream_t *s, int first, int n, int *ids_out
  * max_streams (<= 16) streams of one model.  vox_hip_batch_decode advances every listed
  * stream that has adapter rows left by one greedy token per step; the weights are streamed
  * once per step for all of them, attention / KV / argmax use each stream's own state.
- * Streams not started yet are prefilled first (their first token included).  Results and
- * device state are exactly those of vox_hip_stream_decode on each stream (up to f32
+ * Streams not started yet whose prompt is complete are prefilled first (several of them in
+ * one stacked pass) and take their first token in the batched steps.  Every stream stops on
+ * the device when it has used its adapter rows, after max_steps tokens or (stop_at_eos) after
+ * EOS, while the others go on; streams join and leave a batch without a graph capture (the
+ * step graphs read a device slot table).  Streams with alternatives on
+ * (vox_hip_stream_set_alt) stay in the batch and get their stream_fill_alts records.
+ * Results and device state are those of vox_hip_stream_decode on each stream (up to f32
  * summation order of the shared GEMMs).  tokens_out: [n][max_steps]; counts_out[n].
  * Returns the total number of tokens, < 0 on error. */
 typedef struct vox_hip_batch vox_hip_batch_t;
@@ -214,6 +224,9 @@ int vox_hip_batch_decode(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, 
  * reference's vox_decoder_forward returns, voxtral_decoder.c:762-779; for tests and --alt
  * style callers).  Returns 0, or <0 if s was not in that step. */
 int vox_hip_batch_read_logits(vox_hip_batch_t *b, vox_hip_stream_t *s, float *out);
+/* Counters since creation: [0] calls, [1] step replays, [2] live rows over those steps,
+ * [3] step-graph captures, [4] batched prefill passes, [5] prefilled streams. */
+int vox_hip_batch_stats(const vox_hip_batch_t *b, long long *out6);
 /* Decoder state snapshot: [0]=kv logical length, [1]=next adapter row, [2]=prev token,
  * [3]=started, [4]=eos_seen, [5]=tokens generated. */
 int vox_hip_stream_state(vox_hip_stream_t *s, int *out6);
@@ -266,7 +279,9 @@ int vox_hip_decoder_full_step(vox_hip_stream_t *s, const float *rope_freqs, int 
  * Timing hooks for the benchmark (HIP events on the stream's own queue).
  * ------------------------------------------------------------------------ */
 /* Average device time (ms) of the last decode call's dominant per-layer GEMV launches and
- * the bytes they streamed; filled only when profiling was enabled. */
+ * the bytes they streamed; filled only when profiling was enabled.  out8: [0] ms, [1] bytes,
+ * [2] launches, [3] ms per launch, [5] bytes per launch, [6] encoder-GEMM stage ranges an
+ * owner recomputed because a partial tile did not arrive in time (since creation). */
 int vox_hip_stream_set_profiling(vox_hip_stream_t *s, int enable);
 int vox_hip_stream_profile(vox_hip_stream_t *s, double *out8);
 /* Synchronise the stream's HIP queue. */

@@ -64,9 +64,9 @@ def test_batch_matches_single_and_oracle(models, tiny_cfg, nstreams):
 
 
 def test_batch_logits_per_step_vs_oracle(models, tiny_cfg):
-    """The batched path's logit bar: 3 TINY streams advanced one batched step per call; every
-    step's logits (after the first token, which each stream takes on its own prefill path)
-    within LOGIT_TOL of the oracle's, ids identical."""
+    """The batched path's logit bar: 3 TINY streams advanced one batched step per call (the
+    first call prefills all three in one stacked pass and takes their first token in the
+    batched step); every step's logits within LOGIT_TOL of the oracle's, ids identical."""
     import vox_hip
     import vox_oracle
     hm, om = models
@@ -81,8 +81,7 @@ def test_batch_logits_per_step_vs_oracle(models, tiny_cfg):
     for step in range(n):
         for i, t in enumerate(b.decode(ss, max_steps=1, stop_at_eos=False)):
             got[i] += t.tolist()
-            if step:
-                lg[i].append(b.read_logits(ss[i]))
+            lg[i].append(b.read_logits(ss[i]))
     worst = 0.0
     for i, mel in enumerate(mels):
         o = vox_oracle.OracleStream(om)
@@ -90,7 +89,7 @@ def test_batch_logits_per_step_vs_oracle(models, tiny_cfg):
         t, ol = o.decode(max_steps=n, stop_at_eos=False, want_logits=True)
         o.close()
         assert got[i] == t.tolist(), i
-        r = rel(np.stack(lg[i]), ol[1:])
+        r = rel(np.stack(lg[i]), ol)
         worst = max(worst, r)
         assert r < LOGIT_TOL, (i, r)
     print(f"batched logits vs oracle: worst rel err {worst:.2e}")
@@ -252,6 +251,78 @@ def test_batch_graph_not_reused_after_stream_churn(models, tiny_cfg):
     assert out[0] + got[0] == refs[0]
     assert got[1] == refs[3], reused
     assert out[2] + got[2] == refs[2]
+    for s in ss:
+        s.close()
+    b.close()
+
+
+def test_batch_churn_device_slots(models, tiny_cfg):
+    """Serving churn on one Batch: every call lists a different set of streams -- new ones
+    (prefilled together in one stacked pass, first token in the batched step), running ones,
+    ones that run out of adapter rows in the middle of a call (they stop on the device while
+    the others go on) -- and the step graphs are captured once per slot bucket, not per set.
+    Every stream's ids equal the CPU oracle's."""
+    import vox_hip
+    hm, om = models
+    sizes = [430, 520, 470, 610, 400, 560, 505]
+    mels = _mels(tiny_cfg, sizes, 77)
+    refs = [_reference_tokens(om, m) for m in mels]
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 8)
+    out = [[] for _ in ss]
+    # (streams, max_steps) per call: joins, leaves, re-joins, drop-outs mid-call
+    plan = [([0, 1, 2], 5), ([1, 2, 3, 4], 7), ([0, 4, 5], 3), ([6, 3, 0, 2, 5], 11), ([1, 6], 2),
+            ([0, 1, 2, 3, 4, 5, 6], 9), ([4, 2], 1000), ([0, 1, 3, 5, 6], 1000)]
+    for idx, ms in plan:
+        toks = b.decode([ss[i] for i in idx], max_steps=ms, stop_at_eos=False)
+        for i, t in zip(idx, toks):
+            assert len(t) <= ms
+            out[i] += t.tolist()
+    st = b.stats()
+    for i in range(len(ss)):
+        assert out[i] == refs[i], (i, len(out[i]), len(refs[i]))
+    # buckets 4 and 8 slots (1-2 streams: 2), one attention split bucket (48-key window)
+    assert st["captures"] <= 3, st
+    assert st["prefilled"] == len(ss) and st["prefill_passes"] <= 4, st
+    assert st["rows"] == sum(len(o) for o in out), st
+    print(f"churn: {st}")
+    for s in ss:
+        s.close()
+    b.close()
+
+
+def test_batch_alternatives_match_stream_fill_alts(models, tiny_cfg):
+    """--alt streams stay in the batch (VERDICT r3 missing 1): the batched argmax keeps the
+    softmax partials and the top-4 text candidates per row, and each alt stream's records agree
+    with the reference rule (stream_fill_alts, voxtral.c:955-1010) on the oracle's logits; a
+    stream without alternatives in the same batch is unaffected."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    mels = _mels(tiny_cfg, [640, 700, 580], 91)
+    settings = [(3, 1.0), (1, 1.0), (4, 0.5)]
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel, (na, co) in zip(ss, mels, settings):
+        s.set_alt(na, co)
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, 4)
+    got = [g.tolist() for g in b.decode(ss, max_steps=1000, stop_at_eos=False)]
+    n_with = 0
+    for i, (mel, (na, co)) in enumerate(zip(mels, settings)):
+        o = vox_oracle.OracleStream(om)
+        o.encode_mel(mel)
+        t, ol = o.decode(stop_at_eos=False, want_logits=True)
+        o.close()
+        assert got[i] == t.tolist(), i
+        ids, pr = ss[i].read_alts(0, len(got[i]))
+        for k, tok in enumerate(got[i]):
+            rid, rpr = vox_oracle.fill_alts(ol[k], tok, na, co)
+            assert ids[k].tolist() == rid, (i, k, ids[k], rid)
+            np.testing.assert_allclose(pr[k], rpr, rtol=2 * LOGIT_TOL * float(np.max(np.abs(ol[k]))), atol=1e-9)
+            n_with += ids[k][1] >= 0
+    assert n_with > 0
     for s in ss:
         s.close()
     b.close()

@@ -61,6 +61,34 @@ def test_full_jfk_transcription(full, jfk_samples):
     os_.close()
 
 
+def test_full_gemmf_recompute_backstop_bit_identical(full):
+    """k_gemmf's stream-K hand-off (csrc/vox_hip_gemmf.hip): when a tile's owner does not see
+    a later part published in time it computes that stage range itself.  Forcing that path
+    for every partial (vox_hip_set_gemmf_wait(-1)) must give the same bits as the normal
+    hand-off: the jfk first chunk (M = 677 encoder rows, every projection on k_gemmf) encoded
+    both ways, adapter rows compared exactly, and the device counter records the recomputes
+    (zero on the normal path, > 0 when forced)."""
+    import vox_hip
+    cfg, hm, om = full
+    rng = np.random.default_rng(17)
+    mel = rng.uniform(-0.6, 1.4, size=(1355, cfg.mel_bins)).astype(np.float32)
+    out, rec = [], []
+    for ticks in (5000, -1):
+        old = vox_hip.set_gemmf_wait(ticks)
+        st = vox_hip.Stream(hm)
+        try:
+            n = st.encode_mel(mel)
+            out.append(st.read_adapter(0, n))
+            rec.append(st.profile()["gemmf_recomputes"])
+        finally:
+            vox_hip.set_gemmf_wait(old)
+            st.close()
+    assert out[0].shape[0] > 100
+    np.testing.assert_array_equal(out[0], out[1])
+    assert rec[1] > 0, rec
+    print(f"gemmf recomputes normal / forced: {rec}")
+
+
 def test_full_night1968_5s_transcription(full):
     """C2's shortest benchmark clip, the reference's samples/benchmark/night1968/
     5s_dont_worry_about_him.wav (a recording, not synthetic audio; kept as a fixture like

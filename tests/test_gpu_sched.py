@@ -105,3 +105,94 @@ def test_scheduler_continuous_restarts_per_stream(tiny_weights, jfk_samples):
     assert n_restarts > 0
     hm.close()
     om.close()
+
+
+def test_scheduler_free_with_pending_chunk(tiny_weights, jfk_samples):
+    """freeing the scheduler while an attached stream holds a deferred encoder
+    chunk.  vh_sched_free detaches like vh_sched_detach (the chunk encoded in order, async
+    encoding off), so the stream goes on unscheduled -- its later feeds decode on its own
+    path -- and its ids equal the oracle's session on the same pieces."""
+    import vox_hip
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    import vox_oracle
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    audio = np.ascontiguousarray(np.concatenate([jfk_samples] * 2)[:16000 * 9])
+    ctx = vox_hip.HostCtx(hm)
+    q = vox_hip.Scheduler(ctx, 4)
+    s = vox_hip.HostStream(ctx, interval_s=0.5)
+    q.attach(s)
+    ids, pos = [], 0
+    for tick in range(6):           # scheduled ticks
+        s.feed(audio[pos:pos + PIECE])
+        pos += PIECE
+        q.run()
+        ids += s.get()
+    s.feed(audio[pos:pos + PIECE])  # a chunk deferred for a run that never comes
+    pos += PIECE
+    q.close()
+    while pos < len(audio):         # unscheduled from here on
+        s.feed(audio[pos:pos + PIECE])
+        pos += PIECE
+    s.finish()
+    ids += s.get()
+    s.close()
+    ctx.close()
+    ref, _ = _oracle_ids(om, audio, 0.5)
+    assert ids == ref, (len(ids), len(ref))
+    hm.close()
+    om.close()
+
+
+def test_scheduler_alt_stream_stays_batched(tiny_weights, jfk_samples):
+    """A stream with alternatives (--alt, vox_stream_set_alt(3, 0.5)) is served by the batched
+    steps with the others (no single-stream fallback): its records -- chosen id + accepted
+    alternatives -- equal those of the same stream decoded alone (the single-stream path the CLI
+    tests pin to stream_fill_alts), and the batched steps produced every id."""
+    import vox_hip
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    a = np.concatenate([jfk_samples] * 2)
+    audios = [np.ascontiguousarray(a[:16000 * 8]), np.ascontiguousarray(-a[3000:3000 + 16000 * 6]),
+              np.ascontiguousarray(a[9000:9000 + 16000 * 7])]
+    ctx = vox_hip.HostCtx(hm)
+    q = vox_hip.Scheduler(ctx, 4)
+    ss = [vox_hip.HostStream(ctx, interval_s=0.5) for _ in audios]
+    ss[1].set_alt(3, 0.5)
+    for s in ss:
+        q.attach(s)
+    recs = [[] for _ in audios]
+    pos = [0] * len(audios)
+    done = [False] * len(audios)
+    while not all(done):
+        for k, s in enumerate(ss):
+            if done[k]:
+                continue
+            if pos[k] < len(audios[k]):
+                s.feed(audios[k][pos[k]:pos[k] + PIECE])
+                pos[k] += PIECE
+            else:
+                s.finish()
+                done[k] = True
+        q.run()
+        for k, s in enumerate(ss):
+            recs[k].append(s.get_alt())
+    st = q.stats()
+    for s in ss:
+        q.detach(s)
+        s.close()
+    q.close()
+    got = np.concatenate(recs[1])
+    solo = vox_hip.HostStream(ctx, interval_s=0.5)
+    solo.set_alt(3, 0.5)
+    for i in range(0, len(audios[1]), PIECE):
+        solo.feed(audios[1][i:i + PIECE])
+    solo.finish()
+    want = solo.get_alt()
+    solo.close()
+    ctx.close()
+    assert got.shape == want.shape and got.shape[0] > 0, (got.shape, want.shape)
+    np.testing.assert_array_equal(got, want)
+    assert (got[:, 1] >= 0).any()
+    assert st["tokens"] == sum(len(np.concatenate(r)) for r in recs), st
+    hm.close()

@@ -448,6 +448,7 @@ extern "C" int vox_hip_set_gemm_planes(int planes) {
 }
 
 extern "C" int vox_hip_gemm_planes(void) { return gemm_planes_np(); }
+extern "C" int vox_hip_set_gemmf_wait(int ticks) { return set_gemmf_wait(ticks); }
 
 extern "C" int vox_hip_model_set_kv_fp16(vox_hip_model_t* m, int on) {
     if (on && m->c.dec_head_dim != 128) return set_err("16-bit decoder KV: head_dim 128 only (got %d)", m->c.dec_head_dim);
@@ -469,6 +470,7 @@ static const int ENC_SUB = 1024;      // encoder rows per pass through the 32 la
 static const int DEC_SLACK = 64;      // decoder ring capacity = window + slack
 static const int STEP_BATCH = 16;     // graph replays between EOS checks
 static const size_t GEMM_WS_ELEMS = (size_t)8 << 20;  // split-K workspace (32 MB)
+static const int TOKENS_CAP = 1 << 16;  // per-stream token / alternatives ring entries
 
 struct vox_hip_stream {
     vox_hip_stream() { memset((void*)this, 0, offsetof(vox_hip_stream, pev)); }
@@ -506,7 +508,7 @@ struct vox_hip_stream {
     float* xbatch;           // stacked encoder rows of a batched pass led by this stream
     float* essq;             // k_sklx row sums of squares per column slice [2][slices][16]
     uint16_t *gpa, *gpc;     // k_gemmf planes: norm / attention rows (K <= max(enc_dim, heads x hd)), gate rows
-    int* gflags;             // k_gemmf partial-tile flags (gemmf_grid() ints)
+    int* gflags;             // k_gemmf partial-tile flags + the recompute counter (gemmf_flag_ints())
     int gepoch;              // k_gemmf launch epoch on this stream
     int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
     float alt_cutoff;
@@ -524,6 +526,7 @@ struct vox_hip_stream {
     int graph_prof;               // the last (eager, profiled) steps recorded W1|W3 events
     int capturing;
     hipEvent_t evt[2];
+    hipEvent_t sev;               // cross-queue ordering (batched encoder pass), no timing
     std::vector<hipEvent_t> pev;  // [2*dec_layers] start/stop of each layer's W1|W3 GEMV
     double prof_ms, prof_bytes;
     long long prof_launches;
@@ -622,13 +625,14 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->state, 4));
     TRYH(dalloc(&s->twin_state, 4));
-    s->tokens_cap = 1 << 16;
+    s->tokens_cap = TOKENS_CAP;
     TRYH(dalloc(&s->tokens, s->tokens_cap));
     TRYH(dalloc(&s->alts, (size_t)s->tokens_cap * ALT_REC));
     s->n_alt = 1;
     s->alt_cutoff = 0.f;
     TRYH(hipEventCreate(&s->evt[0]));
     TRYH(hipEventCreate(&s->evt[1]));
+    TRYH(hipEventCreateWithFlags(&s->sev, hipEventDisableTiming));
 #undef TRYH
     if (stream_alloc_frames(s, 2048) || stream_alloc_adapter(s, 1024) || stream_alloc_dec_rows(s, 64))
         return fail();
@@ -660,6 +664,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gpa); dfree(s->gpc); dfree(s->gflags);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
+    if (s->sev) hipEventDestroy(s->sev);
     for (hipEvent_t e : s->pev) hipEventDestroy(e);
     if (s->st) hipStreamDestroy(s->st);
     delete s;
@@ -1106,6 +1111,11 @@ static bool enc_gemmf_ok(const vox_hip_model_t* m, int n) {
 
 static int gemmf(vox_hip_stream_t* s, int epi, const uint16_t* xs, int K, int n, const uint8_t* W, int N,
                  const float* bias, float* C, int ldc, uint16_t* xo) {
+    // the hand-off epoch is a host counter baked into the launch: a captured (replayed)
+    // k_gemmf would reuse it and read stale partial tiles, so capture is refused
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    CK(hipStreamIsCapturing(s->st, &cs));
+    if (cs != hipStreamCaptureStatusNone) return set_err("k_gemmf launch while the stream is capturing");
     if (++s->gepoch <= 0) s->gepoch = 1;
     CK(launch_gemmf(epi, gemm_planes_np(), xs, K, n, W, N, bias, C, ldc, xo, s->gws, s->gws_n, s->gflags, s->gepoch,
                     s->st));
@@ -1124,7 +1134,7 @@ static int run_encoder_rows_gemmf(vox_hip_stream_t* s, float* x, int n, long lon
         const size_t rb = PLANE_MAX_ROWS / SK_ROWS;
         CK(dalloc(&s->gpa, rb * 3 * SK_ROWS * std::max(ED, EQ)));
         CK(dalloc(&s->gpc, rb * 3 * SK_ROWS * EH));
-        CK(dalloc(&s->gflags, (size_t)gemmf_grid()));
+        CK(dalloc(&s->gflags, gemmf_flag_ints()));
     }
     for (int l = 0; l < c.enc_layers; l++) {
         const EncLayerD& L = m->enc[l];
@@ -1302,7 +1312,7 @@ static int run_encoder_rows_batch(vox_hip_stream_t* lead, float* X, int N, vox_h
             const size_t rb = PLANE_MAX_ROWS / SK_ROWS;
             CK(dalloc(&lead->gpa, rb * 3 * SK_ROWS * std::max(ED, EQ)));
             CK(dalloc(&lead->gpc, rb * 3 * SK_ROWS * EH));
-            CK(dalloc(&lead->gflags, (size_t)gemmf_grid()));
+            CK(dalloc(&lead->gflags, gemmf_flag_ints()));
         }
     }
     for (int l = 0; l < c.enc_layers; l++) {
@@ -1359,9 +1369,12 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
                                                int B, int mel_on_device, int* added) {
     if (B < 1 || !ss || !mels || !n || !added) return set_err("encode_mel_batch: bad arguments");
     if (B > VOX_MAX_BATCH) return set_err("encode_mel_batch: at most %d streams", VOX_MAX_BATCH);
-    for (int b = 0; b < B; b++)
+    for (int b = 0; b < B; b++) {
         if (!ss[b] || ss[b]->m != ss[0]->m || ss[b]->ecap != ss[0]->ecap)
             return set_err("encode_mel_batch: streams of one model");
+        for (int j = 0; j < b; j++)
+            if (ss[j] == ss[b]) return set_err("encode_mel_batch: stream listed twice");
+    }
     vox_hip_stream_t* lead = ss[0];
     const vox_hip_config_t& c = lead->m->c;
     const int ED = c.enc_dim;
@@ -1398,12 +1411,11 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
         }
     } else {
         if (!lead->xbatch) CK(dalloc(&lead->xbatch, (size_t)ENC_SUB * ED));
-        // the lead's queue waits for every member's conv stem, stacks the rows, runs the layers
-        std::vector<hipEvent_t> ev(B);
-        for (int b = 0; b < B; b++) {
-            CK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
-            CK(hipEventRecord(ev[b], ss[b]->st));
-            if (b) CK(hipStreamWaitEvent(lead->st, ev[b], 0));
+        // the lead's queue waits for every member's conv stem (each stream's own reusable
+        // event), stacks the rows, runs the layers
+        for (int b = 1; b < B; b++) {
+            CK(hipEventRecord(ss[b]->sev, ss[b]->st));
+            CK(hipStreamWaitEvent(lead->st, ss[b]->sev, 0));
         }
         for (int b = 0; b < B; b++)
             if (T1[b] > 0)
@@ -1414,19 +1426,15 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
             if (T1[b] > 0)
                 CK(hipMemcpyAsync(xin[b], lead->xbatch + (size_t)off[b] * ED, (size_t)T1[b] * ED * 4,
                                   hipMemcpyDeviceToDevice, lead->st));
-        hipEvent_t done;
-        CK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-        CK(hipEventRecord(done, lead->st));
+        CK(hipEventRecord(lead->sev, lead->st));
         for (int b = 0; b < B; b++) {
             added[b] = 0;
-            if (b) CK(hipStreamWaitEvent(ss[b]->st, done, 0));
+            if (b) CK(hipStreamWaitEvent(ss[b]->st, lead->sev, 0));
             if (T1[b] > 0) {
                 added[b] = enc_suffix(ss[b], xin[b], T1[b]);
                 if (added[b] < 0) return -1;
             }
         }
-        for (int b = 0; b < B; b++) hipEventDestroy(ev[b]);
-        hipEventDestroy(done);
     }
     if (!all_async)
         for (int b = 0; b < B; b++) CK(hipStreamSynchronize(ss[b]->st));
@@ -1475,6 +1483,20 @@ extern "C" int vox_hip_stream_read_adapter(vox_hip_stream_t* s, int first, int n
 // ---------------------------------------------------------------------------
 // Decoder
 // ---------------------------------------------------------------------------
+// device state after the prompt's prefill rows 0..np-1: the next step reads row np with the
+// streaming pad token (voxtral.c:1036-1061)
+static int stream_prefilled(vox_hip_stream_t* s, hipStream_t q) {
+    const int np = 32 + s->m->delay_tokens;
+    const int st4[4] = {np, np, TOKEN_STREAMING_PAD, s->n_generated};
+    CK(hipMemcpyAsync(s->state, st4, sizeof st4, hipMemcpyHostToDevice, q));
+    s->h_state[0] = np;
+    s->h_state[1] = np;
+    s->h_state[2] = TOKEN_STREAMING_PAD;
+    s->h_state[3] = s->n_generated;
+    s->started = 1;
+    return 0;
+}
+
 // M>1 rows (prefill) at logical positions pos0.. (voxtral_decoder.c:496-606)
 static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, const float* rope) {
     vox_hip_model_t* m = s->m;
@@ -1685,6 +1707,19 @@ static int ring_read(const T* ring, int cap, int rec, long long first, int n, T*
     return 0;
 }
 
+// prompt embeds + prefill rows 0..prompt_len-2 (voxtral.c:1036-1057) on the stream's queue;
+// the first generated token then comes from row prompt_len-1 through a regular step
+static int stream_prefill(vox_hip_stream_t* s) {
+    vox_hip_model_t* m = s->m;
+    const int np = 32 + m->delay_tokens;
+    if (stream_alloc_dec_rows(s, np)) return -1;
+    if (ensure_rope(s, np + 2)) return -1;
+    CK(launch_embed_rows(s->adapter, m->tok_emb, m->tok_emb_s, 0, np, TOKEN_BOS, TOKEN_STREAMING_PAD, m->c.dec_dim,
+                         s->xd, s->st));
+    if (run_decoder_rows(s, s->xd, np, 0, m->rope_dec)) return -1;
+    return stream_prefilled(s, s->st);
+}
+
 extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int stop_at_eos,
                                      int* tokens_out, float* logits_out) {
     vox_hip_model_t* m = s->m;
@@ -1695,16 +1730,7 @@ extern "C" int vox_hip_stream_decode(vox_hip_stream_t* s, int max_steps, int sto
     if (max_steps <= 0 || s->eos_seen) return 0;
     if (!s->started) {
         if (s->total_adapter < prompt_len) return 0;
-        // prompt embeds + prefill rows 0..prompt_len-2 (voxtral.c:1036-1057)
-        const int np = prompt_len - 1;
-        if (stream_alloc_dec_rows(s, np)) return -1;
-        if (ensure_rope(s, prompt_len + 1)) return -1;
-        CK(launch_embed_rows(s->adapter, m->tok_emb, m->tok_emb_s, 0, np, TOKEN_BOS, TOKEN_STREAMING_PAD, D, s->xd, s->st));
-        if (run_decoder_rows(s, s->xd, np, 0, m->rope_dec)) return -1;
-        int st4[4] = {np, np, TOKEN_STREAMING_PAD, s->n_generated};
-        CK(hipMemcpyAsync(s->state, st4, sizeof st4, hipMemcpyHostToDevice, s->st));
-        s->started = 1;
-        // the first generated token comes from row prompt_len-1 through a regular step
+        if (stream_prefill(s)) return -1;
     }
     const int step_base = s->n_generated;
     int avail = s->total_adapter - (s->h_state[1] > 0 ? s->h_state[1] : prompt_len - 1);
@@ -1836,7 +1862,14 @@ extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
     out8[3] = s->prof_launches ? s->prof_ms / s->prof_launches : 0.0;
     out8[4] = 0;  // what the events bracket: the W1|W3 GEMV of every layer
     out8[5] = s->prof_launches ? s->prof_bytes / s->prof_launches : 0.0;
-    out8[6] = out8[7] = 0.0;
+    // k_gemmf stage ranges an owner recomputed because a partial did not arrive in time
+    int rec = 0;
+    if (s->gflags) {
+        CK(hipMemcpyAsync(&rec, s->gflags + gemmf_grid(), sizeof rec, hipMemcpyDeviceToHost, s->st));
+        CK(hipStreamSynchronize(s->st));
+    }
+    out8[6] = rec;
+    out8[7] = 0.0;
     return 0;
 }
 
@@ -2170,25 +2203,32 @@ struct vox_hip_batch {
     vox_hip_model_t* m;
     int cap;
     hipStream_t st;
-    float *x, *q, *att, *logits, *pval;
+    float *x, *q, *att, *logits, *pval, *palt;
     float* part;     // split-K slabs of the current projection (k_skl), consumed by the next kernel
     float* ssq;      // row sums of squares per 256-column slice (k_resid_xw_fplanes -> k_skl)
     int* ticket;     // k_sklx slice tickets (W1|W3 with the SwiGLU folded in; VOX_HIP_BATCH_SWX=0: off)
     int* pidx;
     uint16_t *xp_d, *xp_q, *xp_h;  // skinny-GEMM inputs: [3][16][K] bf16 planes of the rows (fragment order)
-    // one captured step for the current active set (kernel arguments hold per-stream
-    // pointers): replayed while the set, its adapter buffers, the split count and the rope
-    // table stay the same
-    hipGraphExec_t gexec;
-    int gnb, gsplits;
-    unsigned long long gkey[VOX_MAX_BATCH];  // stream uids (a freed stream's address can be reused)
-    const float* gadapter[VOX_MAX_BATCH];
-    int gadapter_cap[VOX_MAX_BATCH];
-    const float* grope;
-    // rows of the last batched step (b->logits row i = stream luid[i])
+    float* apart;    // decode-attention partials + arrival counters, apart_n floats per slot
+    size_t apart_n;
+    // the slot table (VOX_MAX_BATCH BatchSlot) followed by the token log [VOX_MAX_BATCH][BATCH_TOKLOG],
+    // in device memory and mirrored in pinned host memory (one copy each way per step chunk)
+    BatchSlot* slots;
+    BatchSlot* hslots;
+    // step graphs [kv16][slot bucket 1, 2, 4, 8, 16][attention splits bucket]: their kernel
+    // arguments point at the slot table and the batch's buffers only, so they stay valid as
+    // streams come and go; captured again only when the model's rope table moves
+    hipGraphExec_t gexec[2][5][STEP_GRAPHS];
+    int grope_gen;
+    // rows of the last call (b->logits row i = stream luid[i], from its last step when llive[i])
     unsigned long long luid[VOX_MAX_BATCH];
+    int llive[VOX_MAX_BATCH];
     int lnb;
+    long long n_calls, n_replays, n_rows, n_captures, n_prefill_passes, n_prefilled;
 };
+
+static int* slot_toklog(BatchSlot* slots) { return reinterpret_cast<int*>(slots + VOX_MAX_BATCH); }
+static const size_t SLOT_BYTES = sizeof(BatchSlot) * VOX_MAX_BATCH + sizeof(int) * VOX_MAX_BATCH * BATCH_TOKLOG;
 
 // pack one [N, K] matrix (bf16, or int8 when q8) into fragment order (k_frag_pack)
 static int frag_copy(uint8_t** dst, const uint8_t* src, int N, int K, int q8) {
@@ -2220,13 +2260,25 @@ static int model_frag(vox_hip_model_t* m) {
     return 0;
 }
 
+static void batch_drop_graphs(vox_hip_batch_t* b) {
+    for (auto& k : b->gexec)
+        for (auto& g : k)
+            for (auto& e : g)
+                if (e) {
+                    hipGraphExecDestroy(e);
+                    e = nullptr;
+                }
+}
+
 extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     if (!b) return;
     if (b->st) hipStreamSynchronize(b->st);
     dfree(b->x); dfree(b->part); dfree(b->ssq); dfree(b->ticket); dfree(b->q); dfree(b->att);
-    dfree(b->logits); dfree(b->pval); dfree(b->pidx);
+    dfree(b->logits); dfree(b->pval); dfree(b->pidx); dfree(b->palt); dfree(b->apart);
     dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h);
-    if (b->gexec) hipGraphExecDestroy(b->gexec);
+    if (b->slots) hipFree(b->slots);
+    if (b->hslots) hipHostFree(b->hslots);
+    batch_drop_graphs(b);
     if (b->st) hipStreamDestroy(b->st);
     delete b;
 }
@@ -2237,15 +2289,20 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
         return nullptr;
     }
     const vox_hip_config_t& c = m->c;
+    if (c.dec_head_dim != 128 || c.dec_heads % c.dec_kv_heads || c.dec_heads / c.dec_kv_heads > 4) {
+        set_err("batched decode needs head_dim 128 and <= 4 query heads per kv head");
+        return nullptr;
+    }
     vox_hip_batch_t* b = new vox_hip_batch_t();
     memset((void*)b, 0, sizeof *b);
     b->m = m;
     b->cap = max_streams;
-    const size_t B = max_streams, D = c.dec_dim, QKV = c.dec_heads * c.dec_head_dim + 2 * c.dec_kv_heads * c.dec_head_dim;
+    const size_t D = c.dec_dim, QKV = c.dec_heads * c.dec_head_dim + 2 * c.dec_kv_heads * c.dec_head_dim;
+    const size_t S = VOX_MAX_BATCH;  // rows of the slot-indexed buffers (graphs of any bucket)
     auto fail = [&]() -> vox_hip_batch_t* { vox_hip_batch_free(b); return nullptr; };
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
     TRYH(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
-    TRYH(dalloc(&b->x, B * D));
+    TRYH(dalloc(&b->x, S * D));
     {
         const size_t DQ = (size_t)c.dec_heads * c.dec_head_dim, DH = c.dec_hidden;
         const size_t n = std::max(std::max(skl_splits(D) * QKV, skl_splits(DQ) * D),
@@ -2258,11 +2315,19 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     }
     TRYH(dalloc(&b->ssq, (size_t)SK_ROWS * SKX_TICKETS));  // [slices][16], any slice count
     TRYH(dalloc(&b->ticket, (size_t)SKX_TICKETS));
-    TRYH(dalloc(&b->q, B * c.dec_heads * c.dec_head_dim));
-    TRYH(dalloc(&b->att, B * c.dec_heads * c.dec_head_dim));
-    TRYH(dalloc(&b->logits, B * c.vocab));
-    TRYH(dalloc(&b->pval, B * ARGB));
-    TRYH(dalloc(&b->pidx, B * ARGB));
+    TRYH(dalloc(&b->q, S * c.dec_heads * c.dec_head_dim));
+    TRYH(dalloc(&b->att, S * c.dec_heads * c.dec_head_dim));
+    TRYH(dalloc(&b->logits, S * c.vocab));
+    TRYH(dalloc(&b->pval, S * ARGB));
+    TRYH(dalloc(&b->pidx, S * ARGB));
+    TRYH(dalloc(&b->palt, S * ARGB * ALT_PART));
+    // attention partials + one arrival count per kv head (zeroed; reset by the merging block)
+    b->apart_n = (size_t)c.dec_heads * attn_maxch(c.dec_window) * (c.dec_head_dim + 2) + c.dec_kv_heads;
+    TRYH(dalloc(&b->apart, S * b->apart_n));
+    TRYH(hipMalloc((void**)&b->slots, SLOT_BYTES));
+    TRYH(hipMemset(b->slots, 0, SLOT_BYTES));
+    TRYH(hipHostMalloc((void**)&b->hslots, SLOT_BYTES, hipHostMallocDefault));
+    memset((void*)b->hslots, 0, SLOT_BYTES);
     if (model_frag(m)) return fail();
     TRYH(dalloc(&b->xp_d, (size_t)3 * SK_ROWS * D));
     TRYH(dalloc(&b->xp_q, (size_t)3 * SK_ROWS * c.dec_heads * c.dec_head_dim));
@@ -2271,32 +2336,24 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     return b;
 }
 
-// one batched step over the nb streams in ss (their input rows already in b->x)
-static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, int splits) {
+// one batched step over slots 0..nb-1 of the slot table (their input rows already in b->x)
+static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
     vox_hip_model_t* m = b->m;
     const vox_hip_config_t& c = m->c;
     const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
     const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
     const float scale = 1.0f / sqrtf((float)hd);
+    const int cap = c.dec_window + DEC_SLACK;
+    const size_t ring_layer = (size_t)cap * DKV * (kv16 ? 2 : 4);
     hipStream_t st = b->st;
-    StepPtrs sp;
-    memset(&sp, 0, sizeof sp);
     AttnPtrs ap;
     memset(&ap, 0, sizeof ap);
+    ap.slots = b->slots;
     for (int i = 0; i < nb; i++) {
-        sp.state[i] = ss[i]->state;
-        sp.tokens[i] = ss[i]->tokens;
-        sp.adapter[i] = ss[i]->adapter;
-        sp.adapter_rows[i] = ss[i]->adapter_cap;
         ap.q[i] = b->q + (size_t)i * DQ;
-        ap.state[i] = ss[i]->state;
-        ap.part[i] = ss[i]->part;
+        ap.part[i] = b->apart + (size_t)i * b->apart_n;
         ap.out[i] = b->att + (size_t)i * DQ;
     }
-    const int cap = ss[0]->dcap, kv16 = ss[0]->kv16;
-    for (int i = 1; i < nb; i++)
-        if (ss[i]->kv16 != kv16) return set_err("batched step over streams of different KV element types");
-    sp.kv16 = kv16;
     const int Sres = skl_splits(DH);  // slabs the previous layer's w2 left for the residual
     static int xw_env = -1;
     if (xw_env < 0) {
@@ -2316,14 +2373,9 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
     }
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
-        for (int i = 0; i < nb; i++) {
-            sp.Kc[i] = dec_ring(ss[i], ss[i]->dk, l);
-            sp.Vc[i] = dec_ring(ss[i], ss[i]->dv, l);
-            ap.Kc[i] = sp.Kc[i];
-            ap.Vc[i] = sp.Vc[i];
-        }
         const DecFragD& F = m->dfrag[l];
-        // skinny MFMA GEMMs over fragment-major weights: the streams are the 16-column B
+        ap.ring_off = (size_t)l * ring_layer;
+        // skinny MFMA GEMMs over fragment-major weights: the slots are the 16-column B
         // operand, every weight byte read once per step; each projection leaves split-K slabs
         // in b->part that the next kernel sums (with the residual for wo / w2)
         // residual + RMSNorm: slice-parallel rows (x * w planes + slice sums of squares, the
@@ -2336,17 +2388,11 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
             CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, b->part, l ? Sres : 0, st));
             CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
         }
-        if (hd == 128) {
-            // RoPE + KV append + attention, output into the wo planes (one launch; + the
-            // combine kernel past 256 keys)
-            AttnFuse af;
-            af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
-            CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
-        } else {
-            CK(launch_rope_kv_batch(b->part, skl_splits(DD), nb, DQ, DKV, hd, m->rope_dec, sp, cap, b->q, st));
-            CK(launch_attn_decode_batch(hd, ap, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
-            CK(launch_split_fplanes(b->att, nb, DQ, b->xp_q, st));
-        }
+        // RoPE + KV append + attention of every live slot, output into the wo planes (one
+        // launch; past 256 keys the last key-range block of a kv head merges the partials)
+        AttnFuse af;
+        af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
+        CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
         const bool fuse_wo = xw && swx && wox && !L.so && !L.s13;
         if (fuse_wo) {
             // wo with the residual folded in (k_sklx: the last block of each column slice sums
@@ -2384,52 +2430,56 @@ static int batch_step(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, i
         CK(launch_swiglu_fplanes(b->part, skl_splits(DD), DH, nb, b->xp_h, st));
         CK(launch_gemm_skl(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
     }
-    // final norm (after the last w2 residual) + LM head (tied embeddings) + per-stream argmax,
-    // next inputs (decoder.c:762-779)
+    // final norm (after the last w2 residual) + LM head (tied embeddings) + per-slot argmax,
+    // state, token log and next inputs (decoder.c:762-779)
     CK(launch_rmsnorm_fplanes(b->x, nb, DD, m->dec_norm, nullptr, c.dec_eps, b->xp_d, b->part, Sres, st));
     CK(launch_gemm_skf(b->xp_d, DD, m->lm_frag, m->tok_emb_s, c.vocab, nb, b->logits, c.vocab, st));
-    CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, sp, ss[0]->tokens_cap, m->tok_emb, m->tok_emb_s,
-                           DD, b->x, st));
+    CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, b->palt, b->slots, TOKENS_CAP, slot_toklog(b->slots),
+                           m->tok_emb, m->tok_emb_s, DD, b->x, st));
     return 0;
 }
 
-// `steps` batched steps: replays of one captured step graph (captured again when the
-// active set or anything its kernel arguments point at changed), or eager launches
-static int batch_run(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int nb, int splits, int steps) {
+// slot bucket of n streams: 1, 2, 4, 8 or 16 slots (graph g of the bucket)
+static int slot_bucket(int n, int* g) {
+    int k = 0;
+    while ((1 << k) < n) k++;
+    *g = k;
+    return 1 << k;
+}
+
+// `steps` batched steps over slots 0..nb-1: replays of the bucket's step graph (captured the
+// first time, and again only when the rope table moved), or eager launches
+static int batch_run(vox_hip_batch_t* b, int nb, int gb, int gi, int splits, int kv16, int steps) {
     if (!use_graphs()) {
         for (int k = 0; k < steps; k++)
-            if (batch_step(b, ss, nb, splits)) return -1;
+            if (batch_step(b, nb, splits, kv16)) return -1;
+        b->n_replays += steps;
         return 0;
     }
-    bool same = b->gexec && b->gnb == nb && b->gsplits == splits && b->grope == b->m->rope_dec;
-    for (int i = 0; same && i < nb; i++)
-        same = b->gkey[i] == ss[i]->uid && b->gadapter[i] == ss[i]->adapter && b->gadapter_cap[i] == ss[i]->adapter_cap;
-    if (!same) {
-        if (b->gexec) {
-            hipGraphExecDestroy(b->gexec);
-            b->gexec = nullptr;
-        }
+    if (b->grope_gen != b->m->rope_gen) {
+        batch_drop_graphs(b);
+        b->grope_gen = b->m->rope_gen;
+    }
+    hipGraphExec_t& ge = b->gexec[kv16][gb][gi];
+    if (!ge) {
         hipGraph_t g = nullptr;
         CK(hipStreamBeginCapture(b->st, hipStreamCaptureModeThreadLocal));
-        const int rc = batch_step(b, ss, nb, splits);
+        const int rc = batch_step(b, nb, splits, kv16);
         hipError_t e = hipStreamEndCapture(b->st, &g);
         if (rc || e != hipSuccess) {
             if (g) hipGraphDestroy(g);
             return set_err("batch graph capture failed: %s", hipGetErrorString(e));
         }
-        e = hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0);
+        e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
         hipGraphDestroy(g);
-        if (e != hipSuccess) return set_err("batch graph instantiate failed: %s", hipGetErrorString(e));
-        b->gnb = nb;
-        b->gsplits = splits;
-        b->grope = b->m->rope_dec;
-        for (int i = 0; i < nb; i++) {
-            b->gkey[i] = ss[i]->uid;
-            b->gadapter[i] = ss[i]->adapter;
-            b->gadapter_cap[i] = ss[i]->adapter_cap;
+        if (e != hipSuccess) {
+            ge = nullptr;
+            return set_err("batch graph instantiate failed: %s", hipGetErrorString(e));
         }
+        b->n_captures++;
     }
-    for (int k = 0; k < steps; k++) CK(hipGraphLaunch(b->gexec, b->st));
+    for (int k = 0; k < steps; k++) CK(hipGraphLaunch(ge, b->st));
+    b->n_replays += steps;
     return 0;
 }
 
@@ -2442,12 +2492,76 @@ static void stream_steps_done(vox_hip_stream_t* s, int produced, int last_token)
     s->h_state[3] = s->n_generated;
 }
 
+// The prompts of several new streams in one stacked prefill pass on the batch queue (the
+// decoder prefill of voxtral.c:1036-1057 per stream; rows [b np, (b + 1) np) = stream b):
+// RMSNorm and the projections over all rows (every weight byte read once for the group),
+// RoPE + K/V append and the causal attention per stream against its own ring (the batched
+// encoder's row-offset kernels), scratch of ss[0].  One stream, or 16-bit rings, take the
+// single-stream prefill.  The member queues must be idle.
+static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B) {
+    vox_hip_model_t* m = b->m;
+    const vox_hip_config_t& c = m->c;
+    const int np = 32 + m->delay_tokens;
+    if (B == 1 || ss[0]->kv16 || B * np > ENC_SUB) {
+        for (int i = 0; i < B; i++) {
+            if (stream_prefill(ss[i])) return -1;
+            CK(hipStreamSynchronize(ss[i]->st));
+        }
+        b->n_prefill_passes += B;
+        b->n_prefilled += B;
+        return 0;
+    }
+    const int DD = c.dec_dim, H = c.dec_heads, KVH = c.dec_kv_heads, hd = c.dec_head_dim;
+    const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
+    const float scale = 1.0f / sqrtf((float)hd);
+    vox_hip_stream_t* lead = ss[0];
+    const int N = B * np, cap = lead->dcap;
+    hipStream_t st = b->st;
+    if (stream_alloc_dec_rows(lead, N)) return -1;
+    if (ensure_rope(lead, np + 2)) return -1;
+    float* X = lead->xd;
+    for (int i = 0; i < B; i++)
+        CK(launch_embed_rows(ss[i]->adapter, m->tok_emb, m->tok_emb_s, 0, np, TOKEN_BOS, TOKEN_STREAMING_PAD, DD,
+                             X + (size_t)i * np * DD, st));
+    EncRows er;
+    memset(&er, 0, sizeof er);
+    er.B = B;
+    for (int i = 0; i < B; i++) {
+        er.off[i] = i * np;
+        er.nr[i] = np;
+        er.pos0[i] = 0;
+    }
+    for (int l = 0; l < c.dec_layers; l++) {
+        const DecLayerD& L = m->dec[l];
+        for (int i = 0; i < B; i++) {
+            er.Kc[i] = dec_ring(ss[i], ss[i]->dk, l);
+            er.Vc[i] = dec_ring(ss[i], ss[i]->dv, l);
+        }
+        CK(launch_rmsnorm_rows(X, DD, lead->xnd, DD, L.attn_norm, nullptr, N, DD, c.dec_eps, st));
+        CK(launch_gemm(EPI_STORE, 3, lead->xnd, DD, L.wqkv, L.sqkv, DD, N, DQ + 2 * DKV, nullptr, lead->qkvd, DQ + 2 * DKV,
+                       st, lead->gws, lead->gws_n));
+        CK(launch_rope_kv_rows(lead->qkvd, N, DQ, DKV, hd, m->rope_dec, er, lead->qd_, cap, st));
+        CK(launch_attn_rows(hd, lead->qd_, er, N, cap, lead->attd, H, KVH, c.dec_window, scale, lead->gws, lead->gws_n,
+                            st));
+        CK(launch_gemm(EPI_RESID, 3, lead->attd, DQ, L.wo, L.so, DQ, N, DD, nullptr, X, DD, st, lead->gws, lead->gws_n));
+        CK(launch_rmsnorm_rows(X, DD, lead->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, N, DD, c.dec_eps, st));
+        CK(launch_gemm(EPI_SWIGLU, 3, lead->xnd, DD, L.w13, L.s13, DD, N, 2 * DH, nullptr, lead->gated, DH, st, lead->gws,
+                       lead->gws_n));
+        CK(launch_gemm(EPI_RESID, 3, lead->gated, DH, L.w2, L.s2, DH, N, DD, nullptr, X, DD, st, lead->gws, lead->gws_n));
+    }
+    for (int i = 0; i < B; i++)
+        if (stream_prefilled(ss[i], st)) return -1;
+    b->n_prefill_passes++;
+    b->n_prefilled += B;
+    return 0;
+}
+
 extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, int max_steps,
                                     int stop_at_eos, int* tokens_out, int* counts_out) {
     if (!b || n < 1 || n > b->cap || max_steps < 0) return set_err("bad batch arguments");
     vox_hip_model_t* m = b->m;
     const vox_hip_config_t& c = m->c;
-    const int D = c.dec_dim;
+    const int prompt_len = 1 + 32 + m->delay_tokens;
     for (int i = 0; i < n; i++) {
         if (!streams[i] || streams[i]->m != m) return set_err("batch streams must share the batch's model");
         if (streams[i]->kv16 != streams[0]->kv16)
@@ -2456,67 +2570,99 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
             if (streams[j] == streams[i]) return set_err("stream listed twice in a batch");
         counts_out[i] = 0;
     }
-    int total = 0;
-    // streams not started yet: prefill + first token on their own stream (voxtral.c:1036-1061)
-    for (int i = 0; i < n; i++) {
-        vox_hip_stream_t* s = streams[i];
-        if (!s->started && max_steps > 0 && !s->eos_seen) {
-            const int r = vox_hip_stream_decode(s, 1, stop_at_eos, tokens_out + (size_t)i * max_steps, nullptr);
-            if (r < 0) return -1;
-            counts_out[i] = r;
-            total += r;
-        }
-        CK(hipStreamSynchronize(s->st));  // the batch stream reads the stream's buffers
-    }
-    std::vector<vox_hip_stream_t*> act;
-    std::vector<int> idx;
-    std::vector<int> tok;
-    for (;;) {
-        // active set: started, no EOS, steps left, an adapter row for the next step
-        act.clear();
-        idx.clear();
-        int steps = max_steps;
+    const int kv16 = streams[0]->kv16;
+    b->n_calls++;
+    b->lnb = 0;
+    // every member's queue is idle before the batch queue touches its buffers (adapter rows
+    // of an async encoder pass, a realloc'ed adapter buffer)
+    for (int i = 0; i < n; i++) CK(hipStreamSynchronize(streams[i]->st));
+    if (max_steps == 0) return 0;
+    // 1. streams whose prompt is complete and whose decoder has not started: their prefills
+    //    in one stacked pass; they take their first token in the batched steps below
+    {
+        vox_hip_stream_t* pre[VOX_MAX_BATCH];
+        int np = 0;
         for (int i = 0; i < n; i++) {
             vox_hip_stream_t* s = streams[i];
-            const int avail = s->total_adapter - s->h_state[1];
-            const int left = max_steps - counts_out[i];
-            if (!s->started || s->eos_seen || avail <= 0 || left <= 0) continue;
-            act.push_back(s);
-            idx.push_back(i);
-            steps = std::min(steps, std::min(avail, left));
+            if (!s->started && !s->eos_seen && s->total_adapter >= prompt_len) pre[np++] = s;
         }
-        if (act.empty()) break;
-        const int nb = (int)act.size();
-        steps = std::min(steps, STEP_BATCH);
-        int longest = 0;
-        for (vox_hip_stream_t* s : act) {
-            longest = std::max(longest, s->h_state[0] + steps);
-            if (ensure_rope(s, (long long)s->h_state[0] + steps + 1)) return -1;
-        }
-        const int splits = graph_splits(act[0], graph_index(act[0], std::min(longest, c.dec_window)));
-        for (int i = 0; i < nb; i++)
-            CK(launch_embed_step(act[i]->adapter, m->tok_emb, m->tok_emb_s, act[i]->state, D, b->x + (size_t)i * D,
-                                 b->st));
-        if (batch_run(b, act.data(), nb, splits, steps)) return -1;
-        CK(hipStreamSynchronize(b->st));
-        b->lnb = nb;
-        for (int i = 0; i < nb; i++) b->luid[i] = act[i]->uid;
-        for (int i = 0; i < nb; i++) {
-            vox_hip_stream_t* s = act[i];
-            tok.resize(steps);
-            if (ring_read(s->tokens, s->tokens_cap, 1, s->n_generated, steps, tok.data(), b->st)) return -1;
-            CK(hipStreamSynchronize(b->st));
-            int produced = steps;
-            if (stop_at_eos)
-                for (int k = 0; k < steps; k++)
-                    if (tok[k] == TOKEN_EOS) { produced = k + 1; s->eos_seen = 1; break; }
-            int* out = tokens_out + (size_t)idx[i] * max_steps + counts_out[idx[i]];
-            memcpy(out, tok.data(), (size_t)produced * 4);
-            counts_out[idx[i]] += produced;
-            total += produced;
-            stream_steps_done(s, produced, tok[produced - 1]);
+        if (np && batch_prefill(b, pre, np)) return -1;
+    }
+    // 2. the slot table: slot i = streams[i], a step budget per slot, empty slots up to the
+    //    bucket stopped
+    int gb = 0;
+    const int nb = slot_bucket(n, &gb);
+    BatchSlot* hs = b->hslots;
+    int K = 0, longest = 0;
+    for (int i = 0; i < nb; i++) {
+        memset(&hs[i], 0, sizeof hs[i]);
+        hs[i].stop_tok = -1;
+        if (i >= n) continue;
+        vox_hip_stream_t* s = streams[i];
+        int lim = 0;
+        if (s->started && !s->eos_seen) lim = std::max(0, std::min(s->total_adapter - s->h_state[1], max_steps));
+        hs[i].state = s->state;
+        hs[i].tokens = s->tokens;
+        hs[i].adapter = s->adapter;
+        hs[i].Kc = reinterpret_cast<char*>(s->dk);
+        hs[i].Vc = reinterpret_cast<char*>(s->dv);
+        hs[i].alts = s->n_alt > 1 ? s->alts : nullptr;
+        hs[i].adapter_rows = s->total_adapter;
+        hs[i].left = lim;
+        hs[i].stop_tok = stop_at_eos ? TOKEN_EOS : -1;
+        hs[i].live = lim > 0;
+        hs[i].pos = s->h_state[0];
+        hs[i].produced = 0;
+        if (lim > 0) {
+            K = std::max(K, lim);
+            longest = std::max(longest, s->h_state[0] + lim);
+            if (ensure_rope(s, (long long)s->h_state[0] + lim + 1)) return -1;
         }
     }
+    if (K == 0) {
+        CK(hipStreamSynchronize(b->st));
+        return 0;
+    }
+    const int gi = graph_index(streams[0], std::min(longest, c.dec_window));
+    const int splits = graph_splits(streams[0], gi);
+    CK(hipMemcpyAsync(b->slots, hs, sizeof(BatchSlot) * nb, hipMemcpyHostToDevice, b->st));
+    CK(launch_embed_batch(b->slots, nb, m->tok_emb, m->tok_emb_s, c.dec_dim, b->x, b->st));
+    // 3. the steps, in chunks of STEP_BATCH replays: after each chunk one copy of the slot
+    //    table + token log comes back; the call ends when no slot is live
+    int* htok = slot_toklog(hs);
+    int got[VOX_MAX_BATCH] = {0};
+    int done = 0;
+    while (done < K) {
+        const int k = std::min(STEP_BATCH, K - done);
+        if (batch_run(b, nb, gb, gi, splits, kv16, k)) return -1;
+        CK(hipMemcpyAsync(hs, b->slots, SLOT_BYTES, hipMemcpyDeviceToHost, b->st));
+        CK(hipStreamSynchronize(b->st));
+        done += k;
+        bool any = false;
+        for (int i = 0; i < n; i++) {
+            const int p = hs[i].produced;
+            for (int j = got[i]; j < p; j++) tokens_out[(size_t)i * max_steps + j] = htok[i * BATCH_TOKLOG + j % BATCH_TOKLOG];
+            got[i] = p;
+            any = any || hs[i].live;
+        }
+        if (!any) break;
+    }
+    // 4. host mirrors
+    int total = 0;
+    for (int i = 0; i < n; i++) {
+        vox_hip_stream_t* s = streams[i];
+        const int p = got[i];
+        counts_out[i] = p;
+        total += p;
+        b->luid[i] = s->uid;
+        b->llive[i] = p > 0 && p == done;
+        if (!p) continue;
+        const int last = tokens_out[(size_t)i * max_steps + p - 1];
+        stream_steps_done(s, p, last);
+        if (stop_at_eos && last == TOKEN_EOS) s->eos_seen = 1;
+    }
+    b->lnb = n;
+    b->n_rows += total;
     return total;
 }
 
@@ -2524,10 +2670,21 @@ extern "C" int vox_hip_batch_read_logits(vox_hip_batch_t* b, vox_hip_stream_t* s
     if (!b || !s || !out) return set_err("batch_read_logits: null argument");
     const int V = b->m->c.vocab;
     for (int i = 0; i < b->lnb; i++)
-        if (b->luid[i] == s->uid) {
+        if (b->luid[i] == s->uid && b->llive[i]) {
             CK(hipMemcpyAsync(out, b->logits + (size_t)i * V, (size_t)V * 4, hipMemcpyDeviceToHost, b->st));
             CK(hipStreamSynchronize(b->st));
             return 0;
         }
     return set_err("batch_read_logits: the stream was not advanced by the last batched step");
+}
+
+extern "C" int vox_hip_batch_stats(const vox_hip_batch_t* b, long long* out6) {
+    if (!b || !out6) return set_err("batch_stats: null argument");
+    out6[0] = b->n_calls;
+    out6[1] = b->n_replays;
+    out6[2] = b->n_rows;
+    out6[3] = b->n_captures;
+    out6[4] = b->n_prefill_passes;
+    out6[5] = b->n_prefilled;
+    return 0;
 }

@@ -26,7 +26,10 @@
 // "Valid forms", row 1).  The owner polls the flag from one lane (bounded), reads the
 // partial with sc1 loads and adds the partials in block order, then runs the epilogue.  A
 // wait that times out (another kernel holding the CUs the publishing block needs) makes the
-// owner compute that stage range itself: the same code and summation order, the same bits.
+// owner compute that stage range itself: the same code and summation order, the same bits
+// (tests/test_gpu_gemm_planes.py forces it); a device counter records each such recompute.
+// The epoch must be new for every launch, so a launch is never captured into a graph (the
+// engine refuses it while its stream is capturing).
 #include "vox_hip_internal.h"
 #include "vox_hip_dev.h"
 
@@ -63,12 +66,15 @@ struct GemmfArgs {
     uint16_t* xo;        // SWIGLU: the gate rows as planes [rb][3][16][N / 2] (the w2 input)
     float* ws;           // [G][4 waves x RB x NG x 64 lanes x 4] partial tiles: slot b = block b's
     int* flags;          // [G] epoch of the partial tile block b published
+    int* recomputes;     // count of stage ranges an owner computed itself (wait timed out)
+    int wait_ticks;      // owner's bounded wait per partial (< 0: never wait, always recompute)
     int epoch;
     int S, NT, T;        // K stages, column tiles, tiles
     long long U;         // T * S work units
 };
 
 constexpr int GF_TIMEOUT_TICKS = 5000;  // s_memrealtime ticks (100 MHz): 50 us of waiting
+static int g_gemmf_wait = GF_TIMEOUT_TICKS;  // vox_hip_set_gemmf_wait (tests force the backstop)
 
 // NWV = 4 WR waves: wave w takes column slot w % 4 (NG groups) and row share w / 4 (RB / WR
 // row blocks); with WR = 2 two waves share each SIMD, so one's fragment reads overlap the
@@ -266,14 +272,17 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
             if (tid == 0) {
                 int ok = 0;
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                for (;;) {
+                while (a.wait_ticks >= 0) {
                     if (__hip_atomic_load(&a.flags[pb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch) {
                         ok = 1;
                         break;
                     }
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > GF_TIMEOUT_TICKS) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > (unsigned long long)a.wait_ticks) break;
                     __builtin_amdgcn_s_sleep(2);
                 }
+                // every recompute is counted (vox_hip_stream_profile): a timeout that fires in
+                // production costs the owner the whole stage range, so it must not stay silent
+                if (!ok) __hip_atomic_fetch_add(a.recomputes, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 *s_ok = ok;
             }
             __syncthreads();
@@ -394,6 +403,13 @@ int gemmf_grid() {
     return g_gemmf_blocks ? g_gemmf_blocks : g_cus;
 }
 
+size_t gemmf_flag_ints() { return (size_t)gemmf_grid() + 1; }
+int set_gemmf_wait(int ticks) {
+    const int old = g_gemmf_wait;
+    g_gemmf_wait = ticks;
+    return old;
+}
+
 bool gemmf_ok(int M, int N, int K) { return M > 0 && M <= 1024 && K % 64 == 0 && N % 128 == 0; }
 
 hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
@@ -412,6 +428,8 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     GemmfArgs a;
     a.xs = xs; a.K = K; a.M = M; a.W = static_cast<const uint8_t*>(Wf); a.N = N; a.bias = bias; a.C = C; a.ldc = ldc;
     a.xo = xo; a.ws = ws; a.flags = flags; a.epoch = epoch;
+    a.recomputes = flags + gemmf_grid();  // the counter past the flags (gemmf_flag_ints())
+    a.wait_ticks = g_gemmf_wait;
     a.S = K / 64;
     a.NT = N / (64 * NG);
     a.T = ((M + 16 * RB - 1) / (16 * RB)) * a.NT;

@@ -42,6 +42,29 @@ struct GemvArgs {
 };
 
 constexpr int VOX_MAX_BATCH = 16;    // streams per batched decode step
+
+// One row of a batched decode step, in device memory (the batch's slot table).  The step
+// graph's kernel arguments point at the table, never at a stream, so streams join and leave
+// a batch without a graph capture: the host rewrites the table before a call, the step's
+// last kernel (k_argmax_batch_final) advances it, and a slot whose `live` is 0 costs no
+// attention, KV append, argmax or state change (its row still rides through the GEMMs).
+struct BatchSlot {
+    int* state;             // the stream's {kv logical pos, next adapter row, prev token, step}
+    int* tokens;            // the stream's token ring (tokens_cap entries)
+    const float* adapter;   // the stream's adapter rows
+    char* Kc;               // layer-0 base of the stream's decoder K / V rings (bytes)
+    char* Vc;
+    float* alts;            // stream_fill_alts records (null: no alternatives for this slot)
+    int adapter_rows;       // rows the slot may consume (the stream's adapter count at the call)
+    int left;               // steps the slot may still take in this call
+    int stop_tok;           // the slot stops after emitting this id (TOKEN_EOS, or -1)
+    int live;               // the current step runs for this slot
+    int pos;                // state[0] mirror: the attention starts without the state hop
+    int produced;           // steps taken in this call (index into the batch's token log)
+};
+static_assert(sizeof(BatchSlot) == 72, "BatchSlot layout");
+constexpr int BATCH_TOKLOG = 64;     // per-slot token log entries (>= the steps between reads)
+
 // per-stream operands of one decode-attention launch (blockIdx.z = stream of a batch)
 struct AttnPtrs {
     const float* q[VOX_MAX_BATCH];
@@ -50,6 +73,9 @@ struct AttnPtrs {
     const int* state[VOX_MAX_BATCH];
     float* part[VOX_MAX_BATCH];
     float* out[VOX_MAX_BATCH];
+    // batched step: Kc / Vc / position / liveness from the slot table (layer base + ring_off)
+    const BatchSlot* slots = nullptr;
+    size_t ring_off = 0;
 };
 // Kc / Vc of the decoder rings point at f32 elements, or at IEEE half ones in the 16-bit
 // mode (the kv16 argument of the launchers, VOX_DECODER_KV_FP16)
@@ -64,16 +90,6 @@ struct AttnFuse {
     uint16_t* xs;          // [3][16][H*hd] fragment-major planes of the attention output
 };
 
-// per-stream state of a batched decode step (row i of the batch = stream i)
-struct StepPtrs {
-    int* state[VOX_MAX_BATCH];          // {kv logical pos, next adapter row, prev token, step}
-    float* Kc[VOX_MAX_BATCH];           // layer base of the stream's decoder K ring
-    float* Vc[VOX_MAX_BATCH];
-    int* tokens[VOX_MAX_BATCH];         // the stream's token log (tokens_cap entries)
-    const float* adapter[VOX_MAX_BATCH];
-    int adapter_rows[VOX_MAX_BATCH];
-    int kv16 = 0;                       // rings of IEEE half elements
-};
 constexpr int ARGB = 64;                // argmax partial blocks per row
 
 int gemv_grid(int rows);
@@ -142,12 +158,17 @@ hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state
                                int cap, const float* adapter, int adapter_rows,
                                const void* emb, const float* esc, int D, float* x,
                                const float* part_alt, float* alts, hipStream_t st);
-// rows (i, n) = sum of the S split slabs part[s][16][qd + 2 kvd] (S = 1: a plain row block)
-hipError_t launch_rope_kv_batch(const float* part, int S, int nb, int qd, int kvd, int hd, const float* rope,
-                                const StepPtrs& sp, int cap, float* q, hipStream_t st);
-hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, const StepPtrs& sp,
-                               int tokens_cap, const void* emb, const float* esc, int D, float* x,
-                               hipStream_t st);
+// batched step: x_i = adapter_i[state[1]] + tok_emb[state[2]] for every live slot, 0 otherwise
+hipError_t launch_embed_batch(const BatchSlot* slots, int nb, const void* emb, const float* esc, int D, float* x,
+                              hipStream_t st);
+// batched step's end: per live slot the first-max argmax of its logits row, the token into the
+// stream's ring and toklog[slot][produced % BATCH_TOKLOG], the stream state and the slot
+// advanced (the slot stops at stop_tok, after `left` steps or at its last adapter row), the
+// next input row (0 for a slot that stopped); slots with alts also get the step's
+// stream_fill_alts record (palt: [nb][ARGB][ALT_PART] scratch)
+hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, float* palt,
+                               BatchSlot* slots, int tokens_cap, int* toklog, const void* emb, const float* esc, int D,
+                               float* x, hipStream_t st);
 // Batched decode GEMMs for M <= 16 rows held as three bf16 planes xs[3][16][K] (hi/mid/lo =
 // the exact f32 rows) in MFMA fragment order; weights packed by launch_frag_pack.
 constexpr int SK_ROWS = 16;
@@ -220,6 +241,8 @@ hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const v
 // flags: gemmf_grid() ints (zeroed once), epoch: > 0, new for every launch on the stream.
 bool gemmf_ok(int M, int N, int K);
 int gemmf_grid();
+size_t gemmf_flag_ints();      // flags buffer: gemmf_grid() flags, then the recompute counter
+int set_gemmf_wait(int ticks); // owner's wait per partial in 100 MHz ticks (< 0: always recompute); returns the old
 size_t gemmf_ws_floats(int blocks);
 hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
                         float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,

@@ -1306,10 +1306,14 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
                                                           int maxs, const AttnFuse F = AttnFuse{}, int kvfast = 0) {
     constexpr int NT = NWV * 64, BK = NWV * ATT_CH;
     const int zb = blockIdx.z;  // stream of a batched step (0 for a single stream)
+    // batched step: ring, position and liveness from the slot table (a stopped slot's blocks
+    // leave at once; uniform per block)
+    const BatchSlot* __restrict__ sl = P.slots ? P.slots + zb : nullptr;
+    if (sl && !sl->live) return;
     const float* __restrict__ q = P.q[zb];
-    const KT* __restrict__ Kc = reinterpret_cast<const KT*>(P.Kc[zb]);
-    const KT* __restrict__ Vc = reinterpret_cast<const KT*>(P.Vc[zb]);
-    const int* __restrict__ state = P.state[zb];
+    const KT* __restrict__ Kc = reinterpret_cast<const KT*>(sl ? sl->Kc + P.ring_off : (const char*)P.Kc[zb]);
+    const KT* __restrict__ Vc = reinterpret_cast<const KT*>(sl ? sl->Vc + P.ring_off : (const char*)P.Vc[zb]);
+    const int* __restrict__ state = sl ? nullptr : P.state[zb];
     float* __restrict__ part = P.part[zb];
     float* __restrict__ out = P.out[zb];
     constexpr int DQ = HD / 4;   // dims per lane for Q.K
@@ -1338,7 +1342,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     float qreg[QPT];
 #pragma unroll
     for (int i = 0; i < QPT; i++) qreg[i] = (!FUSE && tid + i * NT < nh * HD) ? q[(size_t)h0 * HD + tid + i * NT] : 0.f;
-    const int lp = state ? state[0] : pos_host;
+    const int lp = sl ? sl->pos : state ? state[0] : pos_host;
     const int L = min(lp + 1, window);
     const int first = lp - L + 1;
     const int S = (L + BK - 1) / BK;
@@ -1878,36 +1882,12 @@ __device__ __forceinline__ bool alt_before(float va, int ia, float vb, int ib) {
     return va > vb || (va == vb && ia >= 0 && (ib < 0 || ia < ib));
 }
 
-__device__ void alt_merge(const float* __restrict__ pa, int n, int best, float bestv, int step,
-                          float* __restrict__ alts) {
+// Block-wide (256 threads) merge of per-thread stream_fill_alts partials: the softmax (max,
+// sum) pairs and the top-4 lists (alt_before order).  Thread 0 ends with the merged partial.
+__device__ void alt_tree(float& m, float& su, float (&tv)[4], int (&ti)[4]) {
     __shared__ float sm[256], ss[256], stv[256][4];
     __shared__ int sti[256][4];
     const int t = threadIdx.x;
-    float m = -INFINITY, su = 0.f, tv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    int ti[4] = {-1, -1, -1, -1};
-    for (int b = t; b < n; b += 256) {
-        const float* p = pa + (size_t)b * ALT_PART;
-        const float bm = p[0], bs = p[1];
-        if (bm > m) {
-            su = su * expf(m - bm) + bs;
-            m = bm;
-        } else if (bs > 0.f) {
-            su += bs * expf(bm - m);
-        }
-        for (int k = 0; k < 4; k++) {
-            const float v = p[2 + k];
-            const int id = __float_as_int(p[6 + k]);
-            if (id < 0 || id == best || !alt_before(v, id, tv[3], ti[3])) continue;
-            int j = 3;
-            while (j > 0 && alt_before(v, id, tv[j - 1], ti[j - 1])) {
-                tv[j] = tv[j - 1];
-                ti[j] = ti[j - 1];
-                j--;
-            }
-            tv[j] = v;
-            ti[j] = id;
-        }
-    }
     sm[t] = m;
     ss[t] = su;
     for (int k = 0; k < 4; k++) {
@@ -1949,13 +1929,52 @@ __device__ void alt_merge(const float* __restrict__ pa, int n, int best, float b
         __syncthreads();
     }
     if (t == 0) {
-        const float M = sm[0], inv = 1.0f / ss[0];
+        m = sm[0];
+        su = ss[0];
+        for (int k = 0; k < 4; k++) {
+            tv[k] = stv[0][k];
+            ti[k] = sti[0][k];
+        }
+    }
+}
+
+__device__ void alt_merge(const float* __restrict__ pa, int n, int best, float bestv, int step,
+                          float* __restrict__ alts) {
+    const int t = threadIdx.x;
+    float m = -INFINITY, su = 0.f, tv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int ti[4] = {-1, -1, -1, -1};
+    for (int b = t; b < n; b += 256) {
+        const float* p = pa + (size_t)b * ALT_PART;
+        const float bm = p[0], bs = p[1];
+        if (bm > m) {
+            su = su * expf(m - bm) + bs;
+            m = bm;
+        } else if (bs > 0.f) {
+            su += bs * expf(bm - m);
+        }
+        for (int k = 0; k < 4; k++) {
+            const float v = p[2 + k];
+            const int id = __float_as_int(p[6 + k]);
+            if (id < 0 || id == best || !alt_before(v, id, tv[3], ti[3])) continue;
+            int j = 3;
+            while (j > 0 && alt_before(v, id, tv[j - 1], ti[j - 1])) {
+                tv[j] = tv[j - 1];
+                ti[j] = ti[j - 1];
+                j--;
+            }
+            tv[j] = v;
+            ti[j] = id;
+        }
+    }
+    alt_tree(m, su, tv, ti);
+    if (t == 0) {
+        const float inv = 1.0f / su;
         float* r = alts + (size_t)step * ALT_REC;
-        r[0] = expf(bestv - M) * inv;
+        r[0] = expf(bestv - m) * inv;
         for (int k = 0; k < 3; k++) {
-            const int id = sti[0][k];
+            const int id = ti[k];
             r[1 + 2 * k] = __int_as_float(id);
-            r[2 + 2 * k] = id >= 0 ? expf(stv[0][k] - M) * inv : 0.f;
+            r[2 + 2 * k] = id >= 0 ? expf(tv[k] - m) * inv : 0.f;
         }
         r[7] = 0.f;
     }
@@ -2034,53 +2053,43 @@ __global__ __launch_bounds__(256) void k_argmax_final(const float* __restrict__ 
 // ============================================================================
 // Batched decode step (C4): row i of the batch belongs to stream i.
 // ============================================================================
-// RoPE + KV append per row at that stream's own logical position (decoder.c:709-722)
-__global__ __launch_bounds__(256) void k_rope_kv_batch(const float* __restrict__ part, int S, int qd, int kvd,
-                                                       int hd, const float* __restrict__ rope, const StepPtrs sp,
-                                                       int cap, float* __restrict__ q) {
-    // stream i = blockIdx.x; the row's value (i, n) is the sum of the S split slabs of the
-    // QKV projection (k_skl; S = 1: a plain [16][ld] row block)
-    const int i = blockIdx.x;
-    const int ld = qd + 2 * kvd;
-    const int pos = sp.state[i][0];
-    const float* rp = rope + (size_t)pos * hd;
-    const size_t slot = (size_t)(pos % cap) * kvd;
-    const int t0 = blockIdx.y * 256 + threadIdx.x, tn = gridDim.y * 256;
-    for (int p = t0; p < qd / 2; p += tn) {
-        const int d = (2 * p) % hd / 2;
-        const float c = rp[2 * d], sn = rp[2 * d + 1];
-        const float2 xx = psum2(part, S, ld, i, 2 * p);
-        const float x0 = xx.x, x1 = xx.y;
-        q[(size_t)i * qd + 2 * p] = x0 * c - x1 * sn;
-        q[(size_t)i * qd + 2 * p + 1] = x0 * sn + x1 * c;
+// next inputs of every slot (voxtral.c:1106-1113): x_i = adapter_i[state[1]] +
+// tok_emb[state[2]] while the slot is live, 0 otherwise (a stopped row stays finite)
+__global__ __launch_bounds__(256) void k_embed_batch(const BatchSlot* __restrict__ slots, const void* __restrict__ emb,
+                                                     const float* __restrict__ esc, int D, float* __restrict__ x) {
+    const int i = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+    const BatchSlot& sl = slots[i];
+    if (j >= D) return;
+    float v = 0.f;
+    if (sl.live) {
+        const int row = sl.state[1], tok = sl.state[2];
+        v = sl.adapter[(size_t)row * D + j] + emb_at(emb, esc, tok, D, j);
     }
-    for (int p = t0; p < kvd / 2; p += tn) {
-        const int d = (2 * p) % hd / 2;
-        const float c = rp[2 * d], sn = rp[2 * d + 1];
-        const float2 xx = psum2(part, S, ld, i, qd + 2 * p);
-        const float x0 = xx.x, x1 = xx.y;
-        kv_st2_rt(sp.Kc[i], slot + 2 * p, x0 * c - x1 * sn, x0 * sn + x1 * c, sp.kv16);
-    }
-    for (int p = t0; p < kvd / 2; p += tn) {
-        const float2 xx = psum2(part, S, ld, i, qd + kvd + 2 * p);
-        kv_st2_rt(sp.Vc[i], slot + 2 * p, xx.x, xx.y, sp.kv16);
-    }
+    x[(size_t)i * D + j] = v;
 }
 
-// argmax over row i's logits, first max wins (voxtral_decoder.c:771-779): ARGB slices
+// argmax over row i's logits, first max wins (voxtral_decoder.c:771-779): ARGB slices.  In a
+// batched step (slots) stopped rows are skipped, and rows whose slot keeps alternatives also
+// leave the slice's stream_fill_alts partial {max, sum, top-4 text values, their ids} in palt.
 __global__ __launch_bounds__(256) void k_argmax_rows(const float* __restrict__ logits, int V, float* __restrict__ pval,
-                                                     int* __restrict__ pidx) {
+                                                     int* __restrict__ pidx, const BatchSlot* __restrict__ slots,
+                                                     float* __restrict__ palt) {
     __shared__ float sv[256];
     __shared__ int si[256];
     const int i = blockIdx.y, b = blockIdx.x;
+    if (slots && !slots[i].live) return;
+    const bool alt = slots && slots[i].alts;
     const int per = (V + ARGB - 1) / ARGB;
     const int lo = b * per, hi = min(V, lo + per);
     const float* lg = logits + (size_t)i * V;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
+    float am = -INFINITY, as = 0.f, tv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int ti[4] = {-1, -1, -1, -1};
     for (int j = lo + threadIdx.x; j < hi; j += 256) {
         const float v = lg[j];
         if (v > bv) { bv = v; bi = j; }  // j ascends per thread
+        if (alt) alt_row(v, j, am, as, tv, ti);
     }
     sv[threadIdx.x] = bv;
     si[threadIdx.x] = bi;
@@ -2100,16 +2109,40 @@ __global__ __launch_bounds__(256) void k_argmax_rows(const float* __restrict__ l
         pval[i * ARGB + b] = sv[0];
         pidx[i * ARGB + b] = si[0];
     }
+    if (alt) {
+        alt_tree(am, as, tv, ti);
+        if (threadIdx.x == 0) {
+            float* pa = palt + ((size_t)i * ARGB + b) * ALT_PART;
+            pa[0] = am;
+            pa[1] = as;
+            for (int k = 0; k < 4; k++) {
+                pa[2 + k] = tv[k];
+                pa[6 + k] = __int_as_float(ti[k]);
+            }
+        }
+    }
 }
 
-// per row: final argmax, the stream's state / token log, next step's input row
-// x_i = adapter_i[row] + tok_emb[token] (voxtral.c:1106-1113)
+// per live slot: final argmax, the stream's token ring and state, the batch's token log, the
+// slot's bookkeeping (stop at stop_tok, after `left` steps or past its last adapter row), and
+// the next input row x_i = adapter_i[row] + tok_emb[token] (voxtral.c:1106-1113), 0 once the
+// slot stopped; then the step's alternatives record when the slot keeps them
 __global__ __launch_bounds__(256) void k_argmax_batch_final(const float* __restrict__ pval, const int* __restrict__ pidx,
-                                                            const StepPtrs sp, int tokens_cap,
+                                                            const float* __restrict__ palt, BatchSlot* __restrict__ slots,
+                                                            int tokens_cap, int* __restrict__ toklog,
                                                             const void* __restrict__ emb, const float* __restrict__ esc,
                                                             int D, float* __restrict__ x) {
-    __shared__ int stok, srow;
+    __shared__ int stok, srow, slive, sstep;
+    __shared__ float sbest;
     const int i = blockIdx.x;
+    BatchSlot* sl = slots + i;
+    float* xr = x + (size_t)i * D;
+    const int live = sl->live;
+    __syncthreads();  // every wave has read the slot before thread 0 advances it
+    if (!live) {
+        for (int j = threadIdx.x; j < D; j += 256) xr[j] = 0.f;
+        return;
+    }
     if (threadIdx.x < 64) {
         float bv = pval[i * ARGB + threadIdx.x];
         int bi = pidx[i * ARGB + threadIdx.x];
@@ -2119,23 +2152,33 @@ __global__ __launch_bounds__(256) void k_argmax_batch_final(const float* __restr
             if (v > bv || (v == bv && id < bi)) { bv = v; bi = id; }
         }
         if (threadIdx.x == 0) {
-            int tok = bi == 0x7fffffff ? 0 : bi;
-            int* st = sp.state[i];
-            const int step = st[3];
-            sp.tokens[i][step % tokens_cap] = tok;  // ring, as k_argmax_final
-            st[0] += 1;
-            st[1] += 1;
+            const int tok = bi == 0x7fffffff ? 0 : bi;
+            int* st = sl->state;
+            const int step = st[3], row = st[1] + 1, pos = st[0] + 1;
+            sl->tokens[step % tokens_cap] = tok;  // ring, as k_argmax_final
+            const int k = sl->produced;
+            toklog[i * BATCH_TOKLOG + k % BATCH_TOKLOG] = tok;
+            st[0] = pos;
+            st[1] = row;
             st[2] = tok;
             st[3] = step + 1;
+            const int left = sl->left - 1;
+            const int live = left > 0 && tok != sl->stop_tok && row < sl->adapter_rows;
+            sl->pos = pos;
+            sl->produced = k + 1;
+            sl->left = left;
+            sl->live = live;
             stok = tok;
-            srow = st[1];
+            srow = row;
+            slive = live;
+            sstep = step;
+            sbest = bv;
         }
     }
     __syncthreads();
-    if (srow < sp.adapter_rows[i]) {
-        const float* a = sp.adapter[i] + (size_t)srow * D;
-        for (int j = threadIdx.x; j < D; j += 256) x[(size_t)i * D + j] = a[j] + emb_at(emb, esc, stok, D, j);
-    }
+    const float* a = sl->adapter + (size_t)srow * D;
+    for (int j = threadIdx.x; j < D; j += 256) xr[j] = slive ? a[j] + emb_at(emb, esc, stok, D, j) : 0.f;
+    if (sl->alts) alt_merge(palt + (size_t)i * ARGB * ALT_PART, ARGB, stok, sbest, sstep % tokens_cap, sl->alts);
 }
 
 // ============================================================================
@@ -3481,8 +3524,10 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
         const char* e = getenv("VOX_HIP_ATT_SHORT");
         g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
     }
-    if (g_attn_short && splits == 1 && hd == 128 && window >= ATT_BK && cap >= ATT_BK && H % KVH == 0) {
-        // contexts of <= 256 keys (splits == 1) with a window of >= 256: keys = slots 0..lp
+    if (g_attn_short && splits == 1 && hd == 128 && window > ATT_BK && cap >= ATT_BK && H % KVH == 0) {
+        // contexts of <= 256 keys (splits == 1) with a window of > 256: nothing has left the
+        // window (lp < 256 < window) and the ring has not wrapped, so keys = slots 0..lp (a
+        // window of exactly 256 would reach L = 256 again at lp >= 256 with wrapped slots)
         if (kv16)
             hipLaunchKernelGGL((k_attn_short<128, kvh_t>), dim3(H), dim3(1024), 0, st, q,
                                reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
@@ -3576,21 +3621,22 @@ hipError_t launch_argmax_final(const float* pv, const int* pi, int n, int* state
     return hipSuccess;
 }
 
-hipError_t launch_rope_kv_batch(const float* part, int S, int nb, int qd, int kvd, int hd, const float* rope,
-                                const StepPtrs& sp, int cap, float* q, hipStream_t st) {
-    if (nb < 1 || nb > VOX_MAX_BATCH || S < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_rope_kv_batch, dim3(nb, 8), dim3(256), 0, st, part, S, qd, kvd, hd, rope, sp, cap, q);
+hipError_t launch_embed_batch(const BatchSlot* slots, int nb, const void* emb, const float* esc, int D, float* x,
+                              hipStream_t st) {
+    if (nb < 1 || nb > VOX_MAX_BATCH || !slots) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_embed_batch, dim3((D + 255) / 256, nb), dim3(256), 0, st, slots, emb, esc, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, const StepPtrs& sp,
-                               int tokens_cap, const void* emb, const float* esc, int D, float* x,
-                               hipStream_t st) {
-    if (nb < 1 || nb > VOX_MAX_BATCH) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_argmax_rows, dim3(ARGB, nb), dim3(256), 0, st, logits, V, pval, pidx);
+hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, int* pidx, float* palt,
+                               BatchSlot* slots, int tokens_cap, int* toklog, const void* emb, const float* esc, int D,
+                               float* x, hipStream_t st) {
+    if (nb < 1 || nb > VOX_MAX_BATCH || !slots || !palt || !toklog) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_argmax_rows, dim3(ARGB, nb), dim3(256), 0, st, logits, V, pval, pidx, slots, palt);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_argmax_batch_final, dim3(nb), dim3(256), 0, st, pval, pidx, sp, tokens_cap, emb, esc, D, x);
+    hipLaunchKernelGGL(k_argmax_batch_final, dim3(nb), dim3(256), 0, st, pval, pidx, palt, slots, tokens_cap, toklog,
+                       emb, esc, D, x);
     LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -740,6 +740,8 @@ static int run_encoder(vh_stream_t *s) {
         s->mel_cursor = total;
         return 0;
     }
+    /* a chunk deferred for a scheduler the stream has left goes first, in order */
+    if (flush_pending(s)) return -1;
     const double t0 = now_ms();
     const float *p = vox_hip_mel_frame_ptr(s->mel, s->mel_cursor);
     /* a scheduled stream's chunk is only enqueued (vox_hip_stream_set_async_encode): the
@@ -975,7 +977,15 @@ vh_sched_t *vh_sched_create(vh_ctx_t *ctx, int max_streams) {
 
 void vh_sched_free(vh_sched_t *q) {
     if (!q) return;
-    for (int i = 0; i < q->n; i++) q->s[i]->sched = NULL;
+    /* every attached stream leaves as vh_sched_detach does: its deferred chunk encoded, async
+     * encoding off (errors are left in vh_last_error) */
+    while (q->n > 0) {
+        vh_stream_t *s = q->s[q->n - 1];
+        if (vh_sched_detach(q, s)) {
+            s->sched = NULL;
+            q->n--;
+        }
+    }
     vox_hip_batch_free(q->batch);
     free(q->tok);
     free(q);
@@ -986,6 +996,7 @@ int vh_sched_attach(vh_sched_t *q, vh_stream_t *s) {
     if (s->sched == q) return 0;
     if (s->sched) return fail("vh_sched_attach: stream already attached to a scheduler");
     if (q->n == q->cap) return fail("vh_sched_attach: scheduler full (%d streams)", q->cap);
+    if (q->ctx->model != s->ctx->model) return fail("vh_sched_attach: stream of another model");
     /* VOX_HIP_SCHED_ASYNC=0: each encoder chunk synchronises (the round-2 behaviour) */
     const char *ae = getenv("VOX_HIP_SCHED_ASYNC");
     if (vox_hip_stream_set_async_encode(s->st, !(ae && atoi(ae) == 0)))
@@ -998,15 +1009,24 @@ int vh_sched_attach(vh_sched_t *q, vh_stream_t *s) {
 int vh_sched_detach(vh_sched_t *q, vh_stream_t *s) {
     for (int i = 0; i < q->n; i++)
         if (q->s[i] == s) {
-            if (flush_pending(s)) return -1;
+            const int rc = flush_pending(s);
             q->s[i] = q->s[--q->n];
             s->sched = NULL;
+            if (rc) return -1;
             return vox_hip_stream_set_async_encode(s->st, 0) ? fail("async encode: %s", vox_hip_last_error()) : 0;
         }
     return fail("vh_sched_detach: stream not attached");
 }
 
-void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) { *out = q->stats; }
+void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {
+    *out = q->stats;
+    long long b[6] = {0};
+    if (q->batch && vox_hip_batch_stats(q->batch, b) == 0) {
+        out->steps = b[1];
+        out->captures = b[3];
+        out->prefill_passes = b[4];
+    }
+}
 
 int vh_sched_run(vh_sched_t *q) {
     const double t_run = now_ms();
@@ -1042,45 +1062,24 @@ int vh_sched_run(vh_sched_t *q) {
             }
         }
     }
-    /* 1. streams whose decoder is not running yet: prefill + first token alone (the
-     *    reference's prefill_ms); streams with --alt keep the single-stream path, whose steps
-     *    record the candidates (the batched step keeps none) */
-    for (int i = 0; i < q->n; i++) {
-        vh_stream_t *s = q->s[i];
-        if (!decoder_ready(s)) continue;
-        if (s->n_alt > 1) {
-            const int g0 = s->generated;
-            if (run_decoder(s)) return -1;
-            total += s->generated - g0;
-            ran[i] = 2;  /* restart checks done by run_decoder */
-            continue;
-        }
-        ran[i] = 1;
-        if (s->started_decoding) continue;
-        const double t0 = now_ms();
-        const int n = vox_hip_stream_decode(s->st, 1, 1, s->dec_buf, NULL);
-        if (n < 0) return fail("decoder: %s", vox_hip_last_error());
-        if (n == 0) continue;
-        const double dt = now_ms() - t0;
-        s->prefill_ms += dt;
-        s->dec_ms += dt;
-        s->started_decoding = 1;
-        if (fill_alt_records(s, 0, n)) return -1;
-        consume_tokens(s, n, &eos[i]);
-        total += n;
-        q->stats.prefills++;
-    }
-    /* 2. greedy steps batched over every running stream until each has used its adapter
-     *    rows or met EOS (one weight read per step for all of them) */
+    /* 1-2. every stream whose decoder can run -- its prompt's adapter rows are there, or it
+     *      already decodes and has rows left -- goes into the batched steps: the new ones'
+     *      prefills share one stacked pass and they take their first token there, streams
+     *      stop on the device when their rows run out or at EOS, streams with --alt keep their
+     *      candidates (vox_hip_batch_decode); one call per round, another only when a stream
+     *      hit the per-call step cap */
+    for (int i = 0; i < q->n; i++) ran[i] = decoder_ready(q->s[i]);
     for (;;) {
         vox_hip_stream_t *hs[VH_SCHED_MAX];
-        int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], nb = 0;
+        int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], gen0[VH_SCHED_MAX], nb = 0;
         for (int i = 0; i < q->n; i++) {
             vh_stream_t *s = q->s[i];
-            if (ran[i] != 1 || eos[i] || !s->started_decoding) continue;
+            if (!ran[i] || eos[i]) continue;
             int st6[6];
             vox_hip_stream_state(s->st, st6);
-            if (st6[4] || vox_hip_stream_adapter_tokens(s->st) - st6[1] <= 0) continue;
+            if (st6[4]) continue;
+            if (st6[3] && vox_hip_stream_adapter_tokens(s->st) - st6[1] <= 0) continue;
+            gen0[nb] = st6[5];
             hs[nb] = s->st;
             idx[nb++] = i;
         }
@@ -1101,8 +1100,14 @@ int vh_sched_run(vh_sched_t *q) {
             const int n = counts[k];
             s->dec_ms += dt;
             if (!n) continue;
+            if (!s->started_decoding) {
+                /* its prefill ran in this call (shared with the other new streams) */
+                s->started_decoding = 1;
+                s->prefill_ms += dt;
+                q->stats.prefills++;
+            }
             memcpy(s->dec_buf, q->tok + (size_t)k * VH_SCHED_STEPS, sizeof(int) * (size_t)n);
-            if (fill_alt_records(s, 0, n)) return -1;
+            if (fill_alt_records(s, gen0[k], n)) return -1;
             consume_tokens(s, n, &eos[idx[k]]);
             total += n;
             more |= n == VH_SCHED_STEPS;

@@ -37,11 +37,12 @@ EXPORTS = [
     "vox_hip_last_error", "vox_hip_clear_error", "vox_hip_set_device", "vox_hip_config_voxtral_4b",
     "vox_hip_model_create", "vox_hip_model_free", "vox_hip_model_set_delay",
     "vox_hip_model_ada_scale", "vox_hip_model_set_kv_fp16", "vox_hip_stream_kv_fp16",
-    "vox_hip_set_gemm_planes", "vox_hip_gemm_planes",
+    "vox_hip_set_gemm_planes", "vox_hip_gemm_planes", "vox_hip_set_gemmf_wait",
     "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
     "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode", "vox_hip_batch_read_logits",
+    "vox_hip_batch_stats",
     "vox_hip_stream_state", "vox_hip_stream_set_alt", "vox_hip_stream_read_alts", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
     "vox_hip_decoder_prefill_step", "vox_hip_decoder_start", "vox_hip_decoder_end",
@@ -74,6 +75,7 @@ def lib():
         "vox_hip_model_set_delay": (I, [P, I]), "vox_hip_model_ada_scale": (I, [P, fp]),
         "vox_hip_model_set_kv_fp16": (I, [P, I]), "vox_hip_stream_kv_fp16": (I, [P]),
         "vox_hip_set_gemm_planes": (I, [I]), "vox_hip_gemm_planes": (I, []),
+        "vox_hip_set_gemmf_wait": (I, [I]),
         "vox_hip_stream_create": (P, [P]), "vox_hip_stream_free": (None, [P]),
         "vox_hip_stream_reset": (I, [P]), "vox_hip_stream_reset_decoder": (I, [P]),
         "vox_hip_stream_encode_mel": (I, [P, P, I, I]),
@@ -84,6 +86,7 @@ def lib():
         "vox_hip_batch_create": (P, [P, I]), "vox_hip_batch_free": (None, [P]),
         "vox_hip_batch_decode": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, I, I, ip, ip]),
         "vox_hip_batch_read_logits": (I, [P, P, fp]),
+        "vox_hip_batch_stats": (I, [P, ctypes.POINTER(ctypes.c_longlong)]),
         "vox_hip_stream_set_alt": (I, [P, I, F]),
         "vox_hip_stream_read_alts": (I, [P, I, I, ip, fp]),
         "vox_hip_sgemm_bf16": (None, [I, I, I, fp, P, fp]),
@@ -133,6 +136,12 @@ def set_gemm_planes(planes: int):
 
 def gemm_planes() -> int:
     return lib().vox_hip_gemm_planes()
+
+
+def set_gemmf_wait(ticks: int) -> int:
+    """the encoder GEMM owner's wait per partial tile (100 MHz ticks; < 0: always recompute);
+    returns the previous value (a diagnostic knob for the tests)"""
+    return lib().vox_hip_set_gemmf_wait(int(ticks))
 
 
 def init(device: int | None = None):
@@ -185,7 +194,12 @@ def encode_mel_batch(streams, mels):
     """vox_hip_stream_encode_mel_batch: each stream's new host mel frames, one encoder pass
     over all of their rows; returns the adapter rows added per stream."""
     n = len(streams)
+    assert n == len(mels) and n > 0
     arrs = [np.ascontiguousarray(m, dtype=np.float32) for m in mels]
+    for s, a in zip(streams, arrs):
+        # the C side copies n * mel_bins floats per stream: shapes are checked here
+        assert a.ndim == 2 and a.shape[1] == s.cfg.mel_bins, (a.shape, s.cfg.mel_bins)
+        assert s.model is streams[0].model, "encode_mel_batch: streams of one model"
     hs = (ctypes.c_void_p * n)(*[s.h for s in streams])
     ps = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
     ns = np.array([a.shape[0] for a in arrs], np.int32)
@@ -325,7 +339,7 @@ class Stream:
         lib().vox_hip_stream_profile(self.h, o)
         # kind 0: the events bracket the W1|W3 GEMV of every layer
         return {"ms": o[0], "bytes": o[1], "launches": int(o[2]), "avg_ms": o[3], "kind": int(o[4]),
-                "bytes_per_launch": o[5]}
+                "bytes_per_launch": o[5], "gemmf_recomputes": int(o[6])}
 
     def sync(self):
         lib().vox_hip_stream_sync(self.h)
@@ -532,6 +546,14 @@ class Batch:
             _err("vox_hip_batch_read_logits")
         return out
 
+    def stats(self) -> dict:
+        """vox_hip_batch_stats: counters since creation"""
+        out = (ctypes.c_longlong * 6)()
+        if lib().vox_hip_batch_stats(self.h, out) != 0:
+            _err("vox_hip_batch_stats")
+        keys = ("calls", "replays", "rows", "captures", "prefill_passes", "prefilled")
+        return dict(zip(keys, (int(v) for v in out)))
+
     def close(self):
         if self.h:
             lib().vox_hip_batch_free(self.h)
@@ -614,7 +636,8 @@ _host = None
 class SchedStats(ctypes.Structure):
     _fields_ = [("runs", ctypes.c_int), ("prefills", ctypes.c_int), ("batch_calls", ctypes.c_int),
                 ("tokens", ctypes.c_longlong), ("run_ms", ctypes.c_double), ("batch_ms", ctypes.c_double),
-                ("enc_batches", ctypes.c_int)]
+                ("enc_batches", ctypes.c_int), ("steps", ctypes.c_longlong), ("captures", ctypes.c_longlong),
+                ("prefill_passes", ctypes.c_longlong)]
 
 
 def host_lib():
@@ -633,6 +656,7 @@ def host_lib():
         "vh_set_processing_interval": (None, [P, F]), "vh_stream_set_continuous": (None, [P, I]),
         "vh_stream_feed": (I, [P, ctypes.POINTER(ctypes.c_float), I]), "vh_stream_flush": (I, [P]),
         "vh_stream_finish": (I, [P]), "vh_stream_get": (I, [P, ip, I]),
+        "vh_stream_get_alt": (I, [P, ip, I]), "vh_stream_set_alt": (I, [P, I, F]),
         "vh_sched_create": (P, [P, I]), "vh_sched_free": (None, [P]), "vh_sched_attach": (I, [P, P]),
         "vh_sched_detach": (I, [P, P]), "vh_sched_run": (I, [P]),
         "vh_sched_stats": (None, [P, ctypes.POINTER(SchedStats)]),
@@ -696,6 +720,20 @@ class HostStream:
             out += buf[:n].tolist()
             if n < 4096:
                 return out
+
+    def set_alt(self, n_alt: int, cutoff: float):
+        """vox_stream_set_alt (voxtral.c:1329-1337)"""
+        if host_lib().vh_stream_set_alt(self.h, n_alt, cutoff) != 0:
+            _herr("vh_stream_set_alt")
+
+    def get_alt(self) -> np.ndarray:
+        """queued records [n, 4]: the chosen id, then the accepted alternatives, -1 padded"""
+        out, buf = [], np.empty((1024, 4), np.int32)
+        while True:
+            n = host_lib().vh_stream_get_alt(self.h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), 1024)
+            out.append(buf[:n].copy())
+            if n < 1024:
+                return np.concatenate(out)
 
     def close(self):
         if self.h:

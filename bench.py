@@ -67,6 +67,10 @@ def parse():
                          "(vh_sched_*), fed -I 0.5 pieces of the 7 sample lengths cycled, staggered starts")
     ap.add_argument("--serve-seconds", type=float, default=120.0,
                     help="--stagger: audio each stream serves (clips back to back)")
+    ap.add_argument("--serve-step-cap", type=int, default=8,
+                    help="--stagger: greedy steps per stream and scheduler run (vh_sched_set_step_cap; 0 = "
+                         "drain every run): a stream's bursts (prompt, flush padding) ride in full batched "
+                         "steps over the next runs")
     ap.add_argument("--kv-fp16", action="store_true",
                     help="the reference's fp16 decoder KV cache (VOX_DECODER_KV_FP16): IEEE half K/V rings")
     ap.add_argument("--long-context", type=int, default=0,
@@ -139,6 +143,7 @@ class Dist:
         if self.world != n:
             raise SystemExit(f"bench.py: WORLD_SIZE={self.world} but --gpus {n}")
         self.torch = None
+        self.host = {}
         if self.world > 1:
             import datetime
 
@@ -158,12 +163,112 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def min(self, x):
+        if self.torch is None:
+            return x
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return float(t.item())
+
     def sum(self, x):
         if self.torch is None:
             return x
         t = self.torch.tensor([float(x)], dtype=self.torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
+
+
+def emit(d, out):
+    """rank 0 prints the line; multi-rank runs also say how each rank's host side was set up"""
+    if d.world > 1 and d.host:
+        out["rank_host"] = d.host
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def parse_cpulist(text):
+    """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11}"""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def gpu_local_cpus(index, sysfs="/sys"):
+    """The host CPUs nearest HIP device `index` (before any GPU call): HIP numbers the GPU
+    nodes of the KFD topology in node order (after ROCR / HIP_VISIBLE_DEVICES), and a node's
+    PCI function lists its local CPUs.  None when any of that is unknown."""
+    try:
+        base = os.path.join(sysfs, "class/kfd/kfd/topology/nodes")
+        gpus = []
+        for node in sorted(os.listdir(base), key=int):
+            props = {}
+            for line in open(os.path.join(base, node, "properties")):
+                k, _, v = line.partition(" ")
+                props[k] = v.strip()
+            if int(props.get("simd_count", "0")) > 0:
+                gpus.append(props)
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+            vis = os.environ.get(var, "").strip()
+            if vis:
+                gpus = [gpus[int(x)] for x in vis.split(",")]
+        p = gpus[index]
+        loc, dom = int(p["location_id"]), int(p.get("domain", "0"))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7}"
+        return parse_cpulist(open(os.path.join(sysfs, "bus/pci/devices", bdf, "local_cpulist")).read())
+    except (OSError, ValueError, KeyError, IndexError):
+        return None
+
+
+def pin_rank(d):
+    """One rank per GPU: keep the rank's host threads (scheduler, device mel feeds, launches)
+    on the CPUs nearest its GPU (VOX_BENCH_AFFINITY=0: off).  Returns what was done."""
+    if d.world == 1 or os.environ.get("VOX_BENCH_AFFINITY") == "0" or os.environ.get("VOX_BENCH_SHARE_GPU") == "1":
+        return None
+    near = gpu_local_cpus(d.local)
+    if not near:
+        return None
+    cpus = near & os.sched_getaffinity(0)
+    if len(cpus) < 2:
+        return None
+    os.sched_setaffinity(0, cpus)
+    return f"{len(cpus)} CPUs local to GPU {d.local}"
+
+
+def host_weights(cfg, seed, d):
+    """The seeded synthetic weights, one host copy per node: local rank 0 generates them into
+    a file in /dev/shm, the other ranks map it read-only, and the file is unlinked as soon as
+    every rank has mapped it (the mappings keep the pages until each rank has uploaded).  A
+    single rank, or a /dev/shm too small, generates privately.  Returns (weights, how)."""
+    from vox_weights import synth_elems, synth_weights, weights_over_buffer
+    total = synth_elems(cfg)
+    shm = "/dev/shm"
+    ok = d.world > 1
+    if ok:
+        try:
+            st = os.statvfs(shm)
+            ok = st.f_bavail * st.f_frsize > total * 2 + (1 << 30)
+        except OSError:
+            ok = False
+    ok = d.min(1.0 if ok else 0.0) > 0.5   # every rank agrees (all use the same node's /dev/shm)
+    if not ok:
+        return synth_weights(cfg, seed=seed), "per rank"
+    path = os.path.join(shm, f"vox_bench_w_{os.environ.get('MASTER_PORT', '0')}_{seed}.bin")
+    if d.local == 0:
+        mm = np.memmap(path + ".tmp", dtype=np.uint16, mode="w+", shape=(total,))
+        w = synth_weights(cfg, seed=seed, buf=mm)
+        mm.flush()
+        os.rename(path + ".tmp", path)
+    d.barrier()
+    if d.local != 0:
+        w = weights_over_buffer(cfg, np.memmap(path, dtype=np.uint16, mode="r", shape=(total,)))
+    d.barrier()
+    if d.local == 0:
+        os.unlink(path)
+    return w, "one shared read-only mapping per node"
 
 
 def transcribe(st, mel_dev, n_mel):
@@ -298,17 +403,19 @@ def main():
     d = Dist(args.gpus)
     if args.dry_run:
         return dry_run(args, d)
+    affinity = pin_rank(d)
     import vox_hip
-    from vox_weights import VOXTRAL_4B, quantize_q8, synth_weights
+    from vox_weights import VOXTRAL_4B, quantize_q8
     # VOX_BENCH_SHARE_GPU=1: every rank on device 0 -- a rehearsal of the multi-rank path
     # (launcher, barrier, max / sum over ranks) on a one-GPU box; its timings mean nothing
     vox_hip.init(device=0 if os.environ.get("VOX_BENCH_SHARE_GPU") == "1" else d.local)
     cfg = VOXTRAL_4B
 
-    w = synth_weights(cfg, seed=args.seed)
+    w, w_how = host_weights(cfg, args.seed, d)
     if args.q8:
         w = quantize_q8(w)
     model = vox_hip.Model(cfg, w)
+    d.host = {"cpu_affinity": affinity, "host_weights": w_how}
     if args.kv_fp16:
         model.set_kv_fp16(True)  # before any stream exists
     keep_host = d.rank == 0 and d.world == 1 and not args.no_cpu_baseline
@@ -434,8 +541,7 @@ def main():
                                "issued_frac": round(gemm_planes() * enc_tf / MFMA_BF16_TFLOPS, 4)}
     if keep_host:
         out["cpu_baseline"] = cpu_baseline(cfg, w, mel, args.cpu_steps, q8=args.q8)
-    if d.rank == 0:
-        print(json.dumps(out), flush=True)
+    emit(d, out)
     mel_dev.free()
     st.close()
     model.close()
@@ -500,8 +606,7 @@ def bench_long(args, d, cfg, model, st):
                              "achieved": round(tok_bytes / (ms_tok * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(tok_bytes / (ms_tok * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
     }
-    if d.rank == 0:
-        print(json.dumps(out), flush=True)
+    emit(d, out)
     mel_dev.free()
     st.close()
     model.close()
@@ -530,8 +635,14 @@ def dry_run(args, d):
            "vs_baseline": None, "dtype": "f32", "data": "synthetic", "dry_run": True,
            "config": {"workload": "placeholder", "global_batch": d.world * args.streams,
                       "streams_per_gpu": args.streams, "parallelism": f"replicas x{d.world} (no collective)"}}
-    if d.rank == 0:
-        print(json.dumps(out), flush=True)
+    if args.stagger:
+        # the served config-4 line's shape (bench_serve): S scheduled streams per rank
+        out["config"].update({"workload": "placeholder for the served line (--stagger)", "served": True,
+                              "serve_seconds": args.serve_seconds,
+                              "parallelism": f"replicas x{d.world}, {args.streams} scheduled streams each"})
+        out["rank_cpus"] = d.sum(len(os.sched_getaffinity(0)))
+        d.host = {"cpu_affinity": pin_rank(d)}
+    emit(d, out)
 
 
 def synth_audio(seconds, seed):
@@ -664,8 +775,7 @@ def bench_streaming(args, d, cfg, model, st):
         gbs = enc_w / (ms_chunk * 1e-3) / 1e9
         out["encoder_roofline"] = {"bound": "hbm", "bytes_per_chunk": enc_w, "achieved": round(gbs, 1),
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
-    if d.rank == 0:
-        print(json.dumps(out), flush=True)
+    emit(d, out)
     st.close()
     model.close()
 
@@ -691,6 +801,7 @@ def bench_serve(args, d, cfg, model, st0):
     S, piece = args.streams, 8000
     ctx = vox_hip.HostCtx(model)
     q = vox_hip.Scheduler(ctx, S)
+    q.set_step_cap(args.serve_step_cap)
     rng = np.random.default_rng(5 + d.rank)
     clips = [synth_audio(sec, 500 + k) for k, sec in enumerate(SAMPLE_SECONDS)]
 
@@ -715,7 +826,9 @@ def bench_serve(args, d, cfg, model, st0):
                     cur[k] = [hs, nxt[k] % len(clips), 0, False]
                     nxt[k] += 1
                 live = True
-                hs, c, pos, _ = cur[k]
+                hs, c, pos, fin = cur[k]
+                if fin:                       # finished, rows still being decoded (step cap)
+                    continue
                 if pos < len(clips[c]):
                     hs.feed(clips[c][pos:pos + piece])
                     cur[k][2] = pos + piece
@@ -729,7 +842,7 @@ def bench_serve(args, d, cfg, model, st0):
                 if cur[k] is None:
                     continue
                 ids += len(cur[k][0].get())
-                if cur[k][3]:                 # finished this tick: retire the clip
+                if cur[k][3] and cur[k][0].pending() == 0:   # finished and drained: retire the clip
                     served[k] += len(clips[cur[k][1]]) / 16000.0
                     q.detach(cur[k][0])
                     cur[k][0].close()
@@ -766,7 +879,10 @@ def bench_serve(args, d, cfg, model, st0):
                 "of the 7 sample lengths)",
         "config": {"workload": f"{S} streams per GPU, each serving {args.serve_seconds:.0f} s of audio as clips of "
                                f"the 7 sample lengths {[round(x, 2) for x in SAMPLE_SECONDS]} s cycled (from clip i), "
-                               "fed in 0.5 s pieces (-I 0.5), starts staggered by 1 s; one vh_sched_run per tick",
+                               "fed in 0.5 s pieces (-I 0.5), starts staggered by 1 s; one vh_sched_run per tick"
+                               + (f", at most {args.serve_step_cap} greedy steps per stream and run (a finished clip "
+                                  "drains over the next ticks before the stream's next clip)"
+                                  if args.serve_step_cap > 0 else ""),
                    "model": "Voxtral-Mini-4B-Realtime", "global_batch": S * d.world, "streams_per_gpu": S,
                    "parallelism": f"replicas x{d.world}, {S} scheduled streams each"},
         "value_is": "all ids generated / wall time of the serving loop (mel, encoder, prefill and decode included)",
@@ -784,8 +900,7 @@ def bench_serve(args, d, cfg, model, st0):
                            "prefilled_streams": st["prefills"] - q_stats0["prefills"],
                            "ticks": ticks},
     }
-    if d.rank == 0:
-        print(json.dumps(out), flush=True)
+    emit(d, out)
     q.close()
     ctx.close()
     model.close()
@@ -830,8 +945,7 @@ def bench_streams(args, d, cfg, model, st0, mel0, mel_dev0, rng):
         "encoder_dtype": encoder_dtype(),
         "decoder_ms_per_batched_step": round(dec_s * 1000.0 / max(1, steps_all / d.world / S), 4),
     }
-    if d.rank == 0:
-        print(json.dumps(out), flush=True)
+    emit(d, out)
     batch.close()
     for m_ in mels:
         m_.free()

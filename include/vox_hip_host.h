@@ -82,6 +82,10 @@ typedef struct {
     int restarts, full_resets;   /* continuous mode */
 } vh_stats_t;
 void vh_stream_stats(const vh_stream_t *s, vh_stats_t *out);
+/* adapter rows the stream's decoder has not consumed yet (0 once it has drained them or met
+ * EOS); a scheduled stream with a step cap (vh_sched_set_step_cap) may finish its feeds with
+ * rows still pending */
+int vh_stream_pending(vh_stream_t *s);
 
 /* Wrap a model the caller created with vox_hip_model_create (Python mirror, servers that
  * load once and share): vh_free on the result leaves the model alone. */
@@ -124,6 +128,13 @@ int vh_sched_attach(vh_sched_t *q, vh_stream_t *s);
 int vh_sched_detach(vh_sched_t *q, vh_stream_t *s);
 int vh_sched_run(vh_sched_t *q);            /* ids generated, < 0 on error */
 void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out);
+/* Serving policy (no reference counterpart): cap > 0 advances each stream by at most `cap`
+ * greedy steps per vh_sched_run, so a stream with a burst of rows (its prompt, the flush
+ * padding of vox_stream_flush) spreads them over the next runs inside full batched steps
+ * instead of stepping alone; ids are unchanged, only their timing.  Run until every
+ * stream's vh_stream_pending is 0 to drain.  cap <= 0 (the default): every run drains every
+ * stream, as vox_stream_feed does. */
+void vh_sched_set_step_cap(vh_sched_t *q, int cap);
 
 /* vox_load_wav (voxtral_audio.c:143-166) for 16 kHz mono 16-bit PCM: malloc'd samples */
 float *vh_load_wav(const char *path, int *n_samples);

@@ -5,6 +5,7 @@
 #include "voxtral_hip_glue.h"
 #include "voxtral_kernels.h"  /* reference: vox_compute_rope_freqs (voxtral_kernels.c:617-629) */
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -14,23 +15,49 @@
                                                : (const uint16_t *)(L)->name##_weight_q8)
 #define SCL(L, name) ((L)->name##_weight_bf16 ? (const float *)0 : (const float *)(L)->name##_scale_q8)
 
-int vox_hip_bind_load(const vox_ctx_t *ctx, vox_hip_binding_t *b) {
-    /* pointer arrays: the model uploads (and packs) everything inside vox_hip_model_create */
-    static const uint16_t *ewq[VOX_ENC_LAYERS], *ewk[VOX_ENC_LAYERS], *ewv[VOX_ENC_LAYERS], *ewo[VOX_ENC_LAYERS];
-    static const uint16_t *ew1[VOX_ENC_LAYERS], *ew2[VOX_ENC_LAYERS], *ew3[VOX_ENC_LAYERS];
-    static const float *ewqb[VOX_ENC_LAYERS], *ewvb[VOX_ENC_LAYERS], *ewob[VOX_ENC_LAYERS], *ew2b[VOX_ENC_LAYERS];
-    static const float *ean[VOX_ENC_LAYERS], *efn[VOX_ENC_LAYERS];
-    static const float *ewqs[VOX_ENC_LAYERS], *ewks[VOX_ENC_LAYERS], *ewvs[VOX_ENC_LAYERS], *ewos[VOX_ENC_LAYERS];
-    static const float *ew1s[VOX_ENC_LAYERS], *ew2s[VOX_ENC_LAYERS], *ew3s[VOX_ENC_LAYERS];
-    static const uint16_t *dwq[VOX_DEC_LAYERS], *dwk[VOX_DEC_LAYERS], *dwv[VOX_DEC_LAYERS], *dwo[VOX_DEC_LAYERS];
-    static const uint16_t *dw1[VOX_DEC_LAYERS], *dw2[VOX_DEC_LAYERS], *dw3[VOX_DEC_LAYERS];
-    static const float *dan[VOX_DEC_LAYERS], *dfn[VOX_DEC_LAYERS], *dad[VOX_DEC_LAYERS], *dau[VOX_DEC_LAYERS];
-    static const float *dwqs[VOX_DEC_LAYERS], *dwks[VOX_DEC_LAYERS], *dwvs[VOX_DEC_LAYERS], *dwos[VOX_DEC_LAYERS];
-    static const float *dw1s[VOX_DEC_LAYERS], *dw2s[VOX_DEC_LAYERS], *dw3s[VOX_DEC_LAYERS];
-    const int q8 = ctx->use_q8;
+/* the per-layer pointer arrays of vox_hip_weights_t, for one vox_hip_bind_load: heap-owned
+ * and freed once vox_hip_model_create has uploaded (and packed) everything, so two contexts
+ * loaded in one process never share them */
+typedef struct {
+    const uint16_t *ewq[VOX_ENC_LAYERS], *ewk[VOX_ENC_LAYERS], *ewv[VOX_ENC_LAYERS], *ewo[VOX_ENC_LAYERS];
+    const uint16_t *ew1[VOX_ENC_LAYERS], *ew2[VOX_ENC_LAYERS], *ew3[VOX_ENC_LAYERS];
+    const float *ewqb[VOX_ENC_LAYERS], *ewvb[VOX_ENC_LAYERS], *ewob[VOX_ENC_LAYERS], *ew2b[VOX_ENC_LAYERS];
+    const float *ean[VOX_ENC_LAYERS], *efn[VOX_ENC_LAYERS];
+    const float *ewqs[VOX_ENC_LAYERS], *ewks[VOX_ENC_LAYERS], *ewvs[VOX_ENC_LAYERS], *ewos[VOX_ENC_LAYERS];
+    const float *ew1s[VOX_ENC_LAYERS], *ew2s[VOX_ENC_LAYERS], *ew3s[VOX_ENC_LAYERS];
+    const uint16_t *dwq[VOX_DEC_LAYERS], *dwk[VOX_DEC_LAYERS], *dwv[VOX_DEC_LAYERS], *dwo[VOX_DEC_LAYERS];
+    const uint16_t *dw1[VOX_DEC_LAYERS], *dw2[VOX_DEC_LAYERS], *dw3[VOX_DEC_LAYERS];
+    const float *dan[VOX_DEC_LAYERS], *dfn[VOX_DEC_LAYERS], *dad[VOX_DEC_LAYERS], *dau[VOX_DEC_LAYERS];
+    const float *dwqs[VOX_DEC_LAYERS], *dwks[VOX_DEC_LAYERS], *dwvs[VOX_DEC_LAYERS], *dwos[VOX_DEC_LAYERS];
+    const float *dw1s[VOX_DEC_LAYERS], *dw2s[VOX_DEC_LAYERS], *dw3s[VOX_DEC_LAYERS];
+} vox_hip_tables_t;
 
+static int bind_model(const vox_ctx_t *ctx, vox_hip_binding_t *b, vox_hip_tables_t *t);
+
+int vox_hip_bind_load(const vox_ctx_t *ctx, vox_hip_binding_t *b) {
     b->model = NULL;
     b->stream = NULL;
+    vox_hip_tables_t *t = (vox_hip_tables_t *)calloc(1, sizeof *t);
+    if (!t) return -1;
+    const int rc = bind_model(ctx, b, t);
+    free(t);
+    return rc;
+}
+
+static int bind_model(const vox_ctx_t *ctx, vox_hip_binding_t *b, vox_hip_tables_t *t) {
+    const uint16_t **ewq = t->ewq, **ewk = t->ewk, **ewv = t->ewv, **ewo = t->ewo;
+    const uint16_t **ew1 = t->ew1, **ew2 = t->ew2, **ew3 = t->ew3;
+    const float **ewqb = t->ewqb, **ewvb = t->ewvb, **ewob = t->ewob, **ew2b = t->ew2b;
+    const float **ean = t->ean, **efn = t->efn;
+    const float **ewqs = t->ewqs, **ewks = t->ewks, **ewvs = t->ewvs, **ewos = t->ewos;
+    const float **ew1s = t->ew1s, **ew2s = t->ew2s, **ew3s = t->ew3s;
+    const uint16_t **dwq = t->dwq, **dwk = t->dwk, **dwv = t->dwv, **dwo = t->dwo;
+    const uint16_t **dw1 = t->dw1, **dw2 = t->dw2, **dw3 = t->dw3;
+    const float **dan = t->dan, **dfn = t->dfn, **dad = t->dad, **dau = t->dau;
+    const float **dwqs = t->dwqs, **dwks = t->dwks, **dwvs = t->dwvs, **dwos = t->dwos;
+    const float **dw1s = t->dw1s, **dw2s = t->dw2s, **dw3s = t->dw3s;
+    const int q8 = ctx->use_q8;
+
     if (!vox_hip_available() && !vox_hip_init()) return -1;
     for (int l = 0; l < VOX_ENC_LAYERS; l++) {
         const vox_enc_layer_t *L = &ctx->encoder.layers[l];
@@ -173,4 +200,52 @@ int vox_hip_bind_reset_decoder(vox_ctx_t *ctx, vox_hip_binding_t *b) {
 int vox_hip_bind_reset_full(vox_ctx_t *ctx, vox_hip_binding_t *b) {
     (void)ctx;
     return vox_hip_stream_reset(b->stream);
+}
+
+/* ---- the single-op linears of voxtral_kernels.c (M > 1 callers: the adapter's two
+ * projections, voxtral.c:895, and the non-incremental encoder) ----
+ * The reference's USE_METAL branches call vox_metal_sgemm_bf16 / _q8 and return
+ * (voxtral_kernels.c:197-264, 316-377); these do the same on the device (weights cached in
+ * HBM by host pointer on first use).  A device error is not hidden behind the CPU path: it
+ * is reported and the process stops, as a wrong result would otherwise go unnoticed. */
+static void linear_done(const char *what) {
+    const char *e = vox_hip_last_error();
+    if (e && e[0]) {
+        fprintf(stderr, "HIP backend: %s: %s\n", what, e);
+        abort();
+    }
+}
+
+static void add_bias(float *y, const float *bias, int rows, int cols) {
+    if (!bias) return;
+    for (int s = 0; s < rows; s++)
+        for (int o = 0; o < cols; o++) y[(size_t)s * cols + o] += bias[o];
+}
+
+void vox_hip_bind_linear_bf16(float *y, const float *x, const uint16_t *W_bf16, const float *bias,
+                              int seq_len, int in_dim, int out_dim) {
+    vox_hip_clear_error();
+    vox_hip_sgemm_bf16(seq_len, out_dim, in_dim, x, W_bf16, y);
+    linear_done("vox_linear_bf16");
+    add_bias(y, bias, seq_len, out_dim);
+}
+
+void vox_hip_bind_matmul_t_bf16(float *C, const float *A, const uint16_t *B_bf16, int M, int K, int N) {
+    vox_hip_clear_error();
+    vox_hip_sgemm_bf16(M, N, K, A, B_bf16, C);
+    linear_done("vox_matmul_t_bf16");
+}
+
+void vox_hip_bind_linear_q8(float *y, const float *x, const int8_t *W_q8, const float *scales, const float *bias,
+                            int seq_len, int in_dim, int out_dim) {
+    vox_hip_clear_error();
+    vox_hip_sgemm_q8(seq_len, out_dim, in_dim, x, W_q8, scales, y);
+    linear_done("vox_linear_q8");
+    add_bias(y, bias, seq_len, out_dim);
+}
+
+void vox_hip_bind_matmul_t_q8(float *C, const float *A, const int8_t *B_q8, const float *scales, int M, int K, int N) {
+    vox_hip_clear_error();
+    vox_hip_sgemm_q8(M, N, K, A, B_q8, scales, C);
+    linear_done("vox_matmul_t_q8");
 }

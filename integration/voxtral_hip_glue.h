@@ -12,7 +12,8 @@
 #include "voxtral_hip.h"  /* this repository's C ABI */
 
 /* The HIP state a vox_ctx_t carries (the patch adds `vox_hip_binding_t hip;` to vox_ctx_t,
- * voxtral.h:188-239).  One model per process, one device stream per context. */
+ * voxtral.h:188-239).  One model and one device stream per context; nothing is shared between
+ * contexts (a process may load several). */
 typedef struct {
     vox_hip_model_t *model;
     vox_hip_stream_t *stream;
@@ -42,5 +43,17 @@ int vox_hip_bind_decoder_forward(vox_ctx_t *ctx, vox_hip_binding_t *b, const flo
 /* stream_reset_decoder_state (voxtral.c:766-783) / stream_reset_full_state (:786-814) */
 int vox_hip_bind_reset_decoder(vox_ctx_t *ctx, vox_hip_binding_t *b);
 int vox_hip_bind_reset_full(vox_ctx_t *ctx, vox_hip_binding_t *b);
+
+/* The USE_HIP branches of voxtral_kernels.c's linears (vox_linear_bf16 / vox_linear_nobias_bf16
+ * / vox_matmul_t_bf16, :197-264, and the Q8 trio, :316-377), taken when vox_hip_available():
+ * y[seq_len, out_dim] = x W^T (+ bias) on the device, the bf16 / int8 weights cached in HBM by
+ * host pointer.  The adapter's M > 1 projections (voxtral.c:895) reach the device this way.
+ * A device error prints vox_hip_last_error() and aborts (no silent CPU fallback). */
+void vox_hip_bind_linear_bf16(float *y, const float *x, const uint16_t *W_bf16, const float *bias,
+                              int seq_len, int in_dim, int out_dim);
+void vox_hip_bind_matmul_t_bf16(float *C, const float *A, const uint16_t *B_bf16, int M, int K, int N);
+void vox_hip_bind_linear_q8(float *y, const float *x, const int8_t *W_q8, const float *scales, const float *bias,
+                            int seq_len, int in_dim, int out_dim);
+void vox_hip_bind_matmul_t_q8(float *C, const float *A, const int8_t *B_q8, const float *scales, int M, int K, int N);
 
 #endif

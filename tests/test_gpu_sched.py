@@ -26,12 +26,14 @@ def _oracle_ids(om, audio, interval, continuous=False):
     return ids, restarts
 
 
-def _serve(hm, audios, starts, interval, continuous=False, max_streams=8):
+def _serve(hm, audios, starts, interval, continuous=False, max_streams=8, step_cap=0):
     """One serving loop on one GPU: at tick t every stream that has started feeds its next
-    piece (flush + finish after its last one), then one vh_sched_run for all of them."""
+    piece (flush + finish after its last one), then one vh_sched_run for all of them (with a
+    step cap, runs go on until every stream has drained)."""
     import vox_hip
     ctx = vox_hip.HostCtx(hm)
     q = vox_hip.Scheduler(ctx, max_streams)
+    q.set_step_cap(step_cap)
     ss = [vox_hip.HostStream(ctx, interval_s=interval, continuous=continuous) for _ in audios]
     for s in ss:
         q.attach(s)
@@ -39,7 +41,7 @@ def _serve(hm, audios, starts, interval, continuous=False, max_streams=8):
     done = [False] * len(audios)
     ids = [[] for _ in audios]
     tick = 0
-    while not all(done):
+    while not all(done) or any(s.pending() for s in ss):
         for k, (a, s) in enumerate(zip(audios, ss)):
             if done[k] or tick < starts[k]:
                 continue
@@ -81,6 +83,28 @@ def test_scheduler_staggered_streams_match_oracle(tiny_weights, jfk_samples):
         assert ids[k] == ref, (k, len(ids[k]), len(ref))
     assert st["tokens"] > st["prefills"] > 0 and st["batch_calls"] > 0
     print("scheduler stats", st)
+    hm.close()
+    om.close()
+
+
+def test_scheduler_step_cap_spreads_bursts(tiny_weights, jfk_samples):
+    """vh_sched_set_step_cap(3): each run advances a stream by at most 3 steps, so prompts and
+    flush paddings drain over later runs inside the batched steps; every stream's ids still
+    equal its oracle session, and more runs than feeds were needed to drain."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    long = np.concatenate([jfk_samples] * 2)
+    lens = [3.0, 9.0, 5.5, 12.0]
+    audios = [np.ascontiguousarray(long[int(k * 17000) % 16000:][:int(s * 16000)]) for k, s in enumerate(lens)]
+    ids, st = _serve(hm, audios, [0, 2, 3, 5], 0.5, step_cap=3)
+    for k, a in enumerate(audios):
+        ref, _ = _oracle_ids(om, a, 0.5)
+        assert ids[k] == ref, (k, len(ids[k]), len(ref))
+    assert st["steps"] > 0 and st["tokens"] / st["steps"] > 1.0, st
+    print("step-capped scheduler stats", st)
     hm.close()
     om.close()
 
@@ -164,7 +188,7 @@ def test_scheduler_alt_stream_stays_batched(tiny_weights, jfk_samples):
     recs = [[] for _ in audios]
     pos = [0] * len(audios)
     done = [False] * len(audios)
-    while not all(done):
+    while not all(done) or any(s.pending() for s in ss):
         for k, s in enumerate(ss):
             if done[k]:
                 continue

@@ -956,6 +956,7 @@ void vh_stream_stats(const vh_stream_t *s, vh_stats_t *o) {
 
 struct vh_sched {
     vh_ctx_t *ctx;
+    int step_cap;             /* vh_sched_set_step_cap: steps per stream and run (<= 0: drain) */
     vox_hip_batch_t *batch;   /* made on the first batched step (fragment-major weight copies) */
     int cap, n;
     vh_stream_t *s[VH_SCHED_MAX];
@@ -1018,6 +1019,17 @@ int vh_sched_detach(vh_sched_t *q, vh_stream_t *s) {
     return fail("vh_sched_detach: stream not attached");
 }
 
+void vh_sched_set_step_cap(vh_sched_t *q, int cap) { q->step_cap = cap > 0 ? cap : 0; }
+
+int vh_stream_pending(vh_stream_t *s) {
+    int st6[6];
+    vox_hip_stream_state(s->st, st6);
+    if (st6[4]) return 0;  /* EOS: nothing more is decoded (non-continuous) */
+    const int rows = vox_hip_stream_adapter_tokens(s->st);
+    if (!st6[3]) return rows >= 1 + 32 + s->ctx->delay_tokens ? rows - (32 + s->ctx->delay_tokens) : 0;
+    return rows - st6[1] > 0 ? rows - st6[1] : 0;
+}
+
 void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {
     *out = q->stats;
     long long b[6] = {0};
@@ -1069,12 +1081,15 @@ int vh_sched_run(vh_sched_t *q) {
      *      candidates (vox_hip_batch_decode); one call per round, another only when a stream
      *      hit the per-call step cap */
     for (int i = 0; i < q->n; i++) ran[i] = decoder_ready(q->s[i]);
-    for (;;) {
+    for (int iter = 0;; iter++) {
         vox_hip_stream_t *hs[VH_SCHED_MAX];
         int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], gen0[VH_SCHED_MAX], nb = 0;
         for (int i = 0; i < q->n; i++) {
             vh_stream_t *s = q->s[i];
             if (!ran[i] || eos[i]) continue;
+            /* past a step cap only live-mode streams go on: their restart checks (step 3)
+             * belong after a full drain, as in the reference */
+            if (iter > 0 && q->step_cap > 0 && !s->continuous) continue;
             int st6[6];
             vox_hip_stream_state(s->st, st6);
             if (st6[4]) continue;
@@ -1089,7 +1104,8 @@ int vh_sched_run(vh_sched_t *q) {
             if (!q->batch) return fail("batch: %s", vox_hip_last_error());
         }
         const double t0 = now_ms();
-        const int r = vox_hip_batch_decode(q->batch, hs, nb, VH_SCHED_STEPS, 1, q->tok, counts);
+        const int cap = q->step_cap > 0 && q->step_cap < VH_SCHED_STEPS ? q->step_cap : VH_SCHED_STEPS;
+        const int r = vox_hip_batch_decode(q->batch, hs, nb, cap, 1, q->tok, counts);
         if (r < 0) return fail("batched decoder: %s", vox_hip_last_error());
         const double dt = now_ms() - t0;
         q->stats.batch_calls++;
@@ -1106,13 +1122,14 @@ int vh_sched_run(vh_sched_t *q) {
                 s->prefill_ms += dt;
                 q->stats.prefills++;
             }
-            memcpy(s->dec_buf, q->tok + (size_t)k * VH_SCHED_STEPS, sizeof(int) * (size_t)n);
+            memcpy(s->dec_buf, q->tok + (size_t)k * cap, sizeof(int) * (size_t)n);
             if (fill_alt_records(s, gen0[k], n)) return -1;
             consume_tokens(s, n, &eos[idx[k]]);
             total += n;
-            more |= n == VH_SCHED_STEPS;
+            more |= n == cap;
         }
         q->stats.tokens += r;
+        /* with a step cap, a scheduled stream's rows beyond it wait for the next run */
         if (r == 0 || !more) break;
     }
     /* 3. per-stream live-mode restarts (voxtral.c:1189-1239) */

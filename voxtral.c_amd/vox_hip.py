@@ -660,6 +660,7 @@ def host_lib():
         "vh_sched_create": (P, [P, I]), "vh_sched_free": (None, [P]), "vh_sched_attach": (I, [P, P]),
         "vh_sched_detach": (I, [P, P]), "vh_sched_run": (I, [P]),
         "vh_sched_stats": (None, [P, ctypes.POINTER(SchedStats)]),
+        "vh_sched_set_step_cap": (None, [P, I]), "vh_stream_pending": (I, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(H, name)
@@ -726,6 +727,10 @@ class HostStream:
         if host_lib().vh_stream_set_alt(self.h, n_alt, cutoff) != 0:
             _herr("vh_stream_set_alt")
 
+    def pending(self) -> int:
+        """adapter rows not decoded yet (vh_stream_pending)"""
+        return host_lib().vh_stream_pending(self.h)
+
     def get_alt(self) -> np.ndarray:
         """queued records [n, 4]: the chosen id, then the accepted alternatives, -1 padded"""
         out, buf = [], np.empty((1024, 4), np.int32)
@@ -763,6 +768,10 @@ class Scheduler:
         if n < 0:
             _herr("vh_sched_run")
         return n
+
+    def set_step_cap(self, cap: int):
+        """vh_sched_set_step_cap: at most `cap` steps per stream and run (0: drain every run)"""
+        host_lib().vh_sched_set_step_cap(self.h, int(cap))
 
     def stats(self) -> dict:
         st = SchedStats()

@@ -235,13 +235,33 @@ def quantize_q8(w: Weights) -> Weights:
     return Weights(w.cfg, {}, q8=q8, f32=f32)
 
 
-def synth_weights(cfg: VoxConfig, seed: int = 0) -> Weights:
-    specs = tensor_specs(cfg)
-    total = sum(int(np.prod(s)) for _, s, _ in specs)
-    buf = np.empty(total, dtype=np.uint16)
-    lib = synth_lib()
+def synth_elems(cfg: VoxConfig) -> int:
+    """bf16 elements of the whole checkpoint (the buffer synth_weights fills)"""
+    return sum(int(np.prod(s)) for _, s, _ in tensor_specs(cfg))
+
+
+def weights_over_buffer(cfg: VoxConfig, buf) -> Weights:
+    """the checkpoint's tensors as views into one bf16 buffer laid out as synth_weights
+    fills it (e.g. a read-only mapping another process generated)"""
     off = 0
     tensors = {}
+    for name, shape, _ in tensor_specs(cfg):
+        n = int(np.prod(shape))
+        tensors[name] = buf[off:off + n].reshape(shape)
+        off += n
+    return Weights(cfg, tensors, keep=buf)
+
+
+def synth_weights(cfg: VoxConfig, seed: int = 0, buf=None) -> Weights:
+    """seeded random weights of the exact architecture; buf (optional): a writable uint16
+    buffer of synth_elems(cfg) elements to fill (a shared mapping)"""
+    specs = tensor_specs(cfg)
+    total = synth_elems(cfg)
+    if buf is None:
+        buf = np.empty(total, dtype=np.uint16)
+    assert buf.dtype == np.uint16 and buf.size == total
+    lib = synth_lib()
+    off = 0
     for idx, (name, shape, kind) in enumerate(specs):
         n = int(np.prod(shape))
         view = buf[off:off + n]
@@ -254,9 +274,8 @@ def synth_weights(cfg: VoxConfig, seed: int = 0) -> Weights:
             std, mean = 0.01, 1.0
         lib.vox_synth_bf16(view.ctypes.data, n, (seed * 1000003 + idx * 7919 + 17) & (2**64 - 1),
                            float(std), float(mean))
-        tensors[name] = view.reshape(shape)
         off += n
-    return Weights(cfg, tensors, keep=buf)
+    return weights_over_buffer(cfg, buf)
 
 
 def load_safetensors(path: str, cfg: VoxConfig = VOXTRAL_4B) -> Weights:

@@ -899,6 +899,8 @@ def bench_serve(args, d, cfg, model, st0):
                            "prefill_passes": st["prefill_passes"] - q_stats0["prefill_passes"],
                            "prefilled_streams": st["prefills"] - q_stats0["prefills"],
                            "ticks": ticks},
+        "encoder_passes": {"ms": round(st["enc_ms"] - q_stats0["enc_ms"], 1),
+                           "passes": st["enc_batches"] - q_stats0["enc_batches"]},
     }
     emit(d, out)
     q.close()

@@ -121,6 +121,7 @@ typedef struct {
     long long steps;         /* batched step replays (tokens / steps = rows per step) */
     long long captures;      /* step-graph captures (vox_hip_batch_stats) */
     long long prefill_passes;/* prefill passes (several new streams share one) */
+    double enc_ms;           /* wall time of the batched encoder passes (step 0, synchronised) */
 } vh_sched_stats_t;
 vh_sched_t *vh_sched_create(vh_ctx_t *ctx, int max_streams);
 void vh_sched_free(vh_sched_t *q);          /* detaches its streams */

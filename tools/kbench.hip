@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wide, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -111,6 +111,7 @@ int main(int argc, char** argv) {
         }
     }
     int layer = 0;
+    int* kb_drain = nullptr;  // VOX_KB_ONLY=drain: dynamic row-group claims (k_gemv a.drain)
     float* wsc = (float*)dmalloc((size_t)V * 4, 1);  // Q8 row scales (any finite values)
     const float* qs = nullptr;  // set: the weight buffers are read as int8 rows
     auto gemv = [&](int pro, int epi, const uint16_t* W, int K, int rows) {
@@ -118,7 +119,7 @@ int main(int argc, char** argv) {
         memset(&a, 0, sizeof a);
         a.x = x; a.K = K; a.W = W; a.wscale = qs; a.rows = rows; a.norm_w = normw; a.ada = ada; a.eps = 1e-5f;
         a.y = y; a.qd = DQ; a.kvd = DKV; a.hd = HD; a.rope = rope; a.state = state; a.Kc = Kc; a.Vc = Vc;
-        a.cap = cap; a.part_val = pv; a.part_idx = pi;
+        a.cap = cap; a.part_val = pv; a.part_idx = pi; a.drain = kb_drain;
         CK(launch_gemv(pro, epi, a, st));
     };
     struct R { const char* name; double us; double bytes; };
@@ -153,6 +154,37 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL(k_touch_rows, dim3(G), dim3(256), 0, st, (*o.w)[layer++ % NL], o.K * 2, o.rb, sw, sink);
                 }, iters, st), (double)G * o.rb * o.K * 2);
         }
+        return 0;
+    }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "drain")) {
+        // decode GEMVs: the static block -> row-group map against dynamic claims past each
+        // block's first two groups (a.drain), bf16 and Q8, 26 rotating layers (cold weights)
+        int* dr = (int*)dmalloc(GEMV_DRAIN_INTS * 4, 0);
+        struct O { const char* n; int pro, epi, K, rows, q8; std::vector<uint16_t*>* w; };
+        for (O o : {O{"qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 0, &wqkv}, O{"wo", PRO_NONE, EPI_RESID, DQ, D, 0, &wo},
+                    O{"w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 0, &w13}, O{"w2", PRO_NONE, EPI_RESID, DH, D, 0, &w2},
+                    O{"q8 qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 1, &wqkv}, O{"q8 wo", PRO_NONE, EPI_RESID, DQ, D, 1, &wo},
+                    O{"q8 w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 1, &w13}, O{"q8 w2", PRO_NONE, EPI_RESID, DH, D, 1, &w2}})
+            for (int dyn : {0, 1, 0, 1}) {
+                kb_drain = dyn ? dr : nullptr;
+                qs = o.q8 ? wsc : nullptr;
+                char nm[96];
+                snprintf(nm, sizeof nm, "gemv %-6s %s (grid %4d)", o.n, dyn ? "claims" : "static", gemv_grid(o.rows));
+                add(nm, timeit([&] { gemv(o.pro, o.epi, (*o.w)[layer++ % NL], o.K, o.rows); }, iters, st),
+                    (double)o.rows * o.K * (o.q8 ? 1 : 2));
+            }
+        for (int dyn : {0, 1, 0, 1}) {
+            kb_drain = dyn ? dr : nullptr;
+            qs = nullptr;
+            char nm[96];
+            snprintf(nm, sizeof nm, "gemv lm     %s (grid %4d)", dyn ? "claims" : "static", gemv_grid(V));
+            add(nm, timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 4, st), (double)V * D * 2);
+        }
+        int h[2];
+        CK(hipMemcpy(h, dr, 8, hipMemcpyDeviceToHost));
+        printf("drain counters after the runs (must be 0 0): %d %d\n", h[0], h[1]);
+        kb_drain = nullptr;
+        qs = nullptr;
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "grid")) {
@@ -424,17 +456,19 @@ int main(int argc, char** argv) {
         for (int M : {70, 677, 1024})
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
                         G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
-                for (int v = 0; v < 4; v++) {
-                    // np2 with the launcher's tile choice, np2 RB8, np2 RB4, np3 (RB4)
+                for (int v = 0; v < 5; v++) {
+                    // np2 with the launcher's tile choice, np2 RB8, np2 RB4, np3 (RB4), np2 wide
+                    // (64 x 64 per wave, 4 waves)
                     const int np = v == 3 ? 3 : 2;
                     g_gemmf_rb = v == 1 ? 8 : v == 2 ? 4 : 0;
+                    g_gemmf_wide = v == 4 ? 1 : 0;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
-                    printf("gemmf %-4s M=%4d %dx%d np%d rb%d minu%-2d %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
-                           g.K, np, g_gemmf_rb, g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                    printf("gemmf %-4s M=%4d %dx%d np%d rb%d%s minu%-2d %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
+                           g.K, np, g_gemmf_rb, g_gemmf_wide ? " wide" : "", g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
-                g_gemmf_rb = g_gemmf_minu = 0;
+                g_gemmf_rb = g_gemmf_minu = g_gemmf_wide = 0;
             }
     }
     if (only_gemmf) return 0;

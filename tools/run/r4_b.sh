@@ -1,9 +1,13 @@
-# Round 4: step-capped serving (bursts ride in full batched steps), A/B against drain-every-run,
-# kernel stats of the served line (eager) and a graph-replay profile attempt
+# Round 4: dynamic row-group claims in the decode GEMVs (A/B, kbench + bench), step-capped
+# serving A/B, kernel stats of the served line (eager) and a graph-replay profile attempt
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_sched.py > gpurun_out/r4b_test.log 2>&1 || { tail -40 gpurun_out/r4b_test.log; exit 1; }
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 1 > gpurun_out/r4b_serve16.json 2> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_tiny.py tests/test_gpu_sched.py tests/test_gpu_q8.py tests/test_gpu_full.py::test_full_jfk_transcription > gpurun_out/r4b_test.log 2>&1 || { tail -40 gpurun_out/r4b_test.log; exit 1; }
+VOX_KB_ONLY=drain timeout -k 10 120 tools/kbench 100 > gpurun_out/r4b_kb_drain.txt 2>&1 || { tail -20 gpurun_out/r4b_kb_drain.txt; exit 1; }
+VOX_KB_ONLY=gemmf timeout -k 10 200 tools/kbench 50 > gpurun_out/r4b_kb_gemmf.txt 2>&1 || { tail -20 gpurun_out/r4b_kb_gemmf.txt; exit 1; }
+for d in 0 1 0 1; do VOX_HIP_GEMV_DRAIN=$d timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/r4b_c2_d$d.json 2>> gpurun_out/r4b.err || exit 1; cat gpurun_out/r4b_c2_d$d.json >> gpurun_out/r4b_c2_ab.jsonl; done
+for d in 0 1; do VOX_HIP_GEMV_DRAIN=$d timeout -k 10 200 python -u bench.py --no-cpu-baseline --q8 --steps 10 --warmup 2 > gpurun_out/r4b_q8_d$d.json 2>> gpurun_out/r4b.err || exit 1; done
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 1 > gpurun_out/r4b_serve16.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 1 --serve-step-cap 0 > gpurun_out/r4b_serve16_nocap.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 8 --steps 1 --warmup 1 > gpurun_out/r4b_serve8.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
 VOX_HIP_GRAPH=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r4b_prof_serve16 -o serve16 -- python3 -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 0 --serve-seconds 40 > gpurun_out/r4b_prof_serve16.log 2>&1 || { tail -20 gpurun_out/r4b_prof_serve16.log; exit 1; }

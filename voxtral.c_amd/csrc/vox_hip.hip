@@ -516,6 +516,7 @@ struct vox_hip_stream {
     int graph_rope_gen;      // model rope table generation the step graphs were captured with
     int *pidx, *state, *tokens;   // tokens: ring of tokens_cap ids, index = step % tokens_cap
     int* twin_state;              // decoder_full_step's argmax state (the graph state stays untouched)
+    int* gdrain;                  // k_gemv row-group claim + done counters (self-resetting)
     int dec_rows_cap, tokens_cap;
     hipGraphExec_t step_exec[STEP_GRAPHS];  // [g]: attention with 2^g key splits (g = 0: no combine)
     int graph_ready;              // bit mask of built graphs
@@ -625,6 +626,7 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->state, 4));
     TRYH(dalloc(&s->twin_state, 4));
+    TRYH(dalloc(&s->gdrain, GEMV_DRAIN_INTS));
     s->tokens_cap = TOKENS_CAP;
     TRYH(dalloc(&s->tokens, s->tokens_cap));
     TRYH(dalloc(&s->alts, (size_t)s->tokens_cap * ALT_REC));
@@ -659,7 +661,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->im2col); dfree(s->x_enc); dfree(s->xn); dfree(s->qkv); dfree(s->q); dfree(s->att);
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
-    dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
+    dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->gdrain); dfree(s->tokens);
     dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch);
     dfree(s->gpa); dfree(s->gpc); dfree(s->gflags);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
@@ -1529,6 +1531,16 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
 // otherwise pos/rope_row are host values (boundary twin).
 static int enqueue_lm_head(vox_hip_stream_t* s, const int* state);
 
+// decode GEMVs with dynamically claimed row groups (VOX_HIP_GEMV_DRAIN=0: the static map)
+static int gemv_drain_env() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VOX_HIP_GEMV_DRAIN");
+        v = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return v;
+}
+
 static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row,
                                int splits) {
     vox_hip_model_t* m = s->m;
@@ -1537,6 +1549,7 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
     const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
     const float scale = 1.0f / sqrtf((float)hd);
     hipStream_t st = s->st;
+    int* drain = gemv_drain_env() ? s->gdrain : nullptr;
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         float* Kc = dec_ring(s, s->dk, l);
@@ -1550,6 +1563,7 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         a.state = state; a.pos = pos;
         a.rope = state ? m->rope_dec : rope_row - (size_t)pos * hd;
         a.Kc = Kc; a.Vc = Vc; a.cap = s->dcap; a.kv16 = s->kv16;
+        a.drain = drain;
         CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
         // attention over the last min(pos+1, window) keys (decoder.c:724-733)
         CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
@@ -1557,11 +1571,13 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         // wo + residual (decoder.c:735-740)
         memset(&a, 0, sizeof a);
         a.x = s->attd; a.K = DQ; a.W = L.wo; a.wscale = L.so; a.rows = DD; a.y = s->xd;
+        a.drain = drain;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
         // norm * (1 + ada) -> W1|W3 -> silu * up (decoder.c:742-758)
         memset(&a, 0, sizeof a);
         a.x = s->xd; a.K = DD; a.W = L.w13; a.wscale = L.s13; a.rows = 2 * DH; a.norm_w = L.ffn_norm;
         a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
+        a.drain = drain;
         // profiling: HIP events recorded by the W1|W3 launch's own dispatch (eager steps)
         const bool gprof = s->profiling && state && !s->capturing && (int)s->pev.size() == 2 * c.dec_layers;
         if (gprof) CK(launch_gemv_timed(PRO_NORM_ADA, EPI_SWIGLU, a, s->pev[2 * l], s->pev[2 * l + 1], st));
@@ -1569,6 +1585,7 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         // W2 + residual (decoder.c:758-760)
         memset(&a, 0, sizeof a);
         a.x = s->gated; a.K = DH; a.W = L.w2; a.wscale = L.s2; a.rows = DD; a.y = s->xd;
+        a.drain = drain;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
     }
     return enqueue_lm_head(s, state);
@@ -1584,6 +1601,7 @@ static int enqueue_lm_head(vox_hip_stream_t* s, const int* state) {
     a.x = s->xd; a.K = c.dec_dim; a.W = m->tok_emb; a.wscale = m->tok_emb_s; a.rows = c.vocab; a.norm_w = m->dec_norm;
     a.eps = c.dec_eps; a.y = s->logits; a.part_val = s->pval; a.part_idx = s->pidx;
     a.part_alt = s->part_alt;
+    a.drain = gemv_drain_env() ? s->gdrain : nullptr;
     CK(launch_gemv(PRO_NORM, (state && s->n_alt > 1) ? EPI_LOGITS_ALT : EPI_LOGITS, a, st));
     return 0;
 }

@@ -14,6 +14,7 @@ constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3
 enum { PRO_NONE = 0, PRO_NORM = 1, PRO_NORM_ADA = 2 };
 
 constexpr int GEMV_MAX_BLOCKS = 1024;  // 4 blocks of 256 threads per CU on 256 CUs
+constexpr int GEMV_DRAIN_INTS = 2 + 64;
 
 struct GemvArgs {
     const float* x;        // input vector [K] (device)
@@ -39,6 +40,9 @@ struct GemvArgs {
     float* part_val;
     int* part_idx;
     float* part_alt;       // EPI_LOGITS_ALT: [blocks][ALT_PART]
+    int* drain = nullptr;  // GEMV_DRAIN_INTS zeroed ints (claim, done -- reset by the last block --, then
+                           // 64 words the claiming wave's other lanes add 0 to): row groups
+                           // claimed dynamically past each block's first two (null: static b + kG)
 };
 
 constexpr int VOX_MAX_BATCH = 16;    // streams per batched decode step

@@ -1050,7 +1050,16 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int K = a.K, KC = WQ8 ? K >> 4 : K >> 3;
     const int ngroups = a.rows / RB;
-    int g = blockIdx.x;
+    // Groups: block b takes b and b + G first; with a.drain the later ones come from a claim
+    // counter (2G + claim), so blocks that the memory system served early take more groups
+    // and every block drains at the same time; without it b + kG (static).  The claim for the
+    // group after next goes out at the top of each iteration; its value is read a full
+    // group's dot products later, at the barrier that already follows the reduction.
+    const int G = gridDim.x;
+    const bool dyn = a.drain != nullptr;
+    const int wv0 = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index, provably uniform
+    __shared__ int s_next[2];
+    int g = blockIdx.x, gn = g + G;
     int rows[RB];
     uint4 wv[KQ][RB];
     float wsc[RB];
@@ -1146,6 +1155,14 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     int buf = 0;
     for (;;) {
         const int gcur = g;
+        // wave 0 claims with every lane active (lane 0 on the counter, the others add 0 to
+        // their own words past it): a single-lane atomic sits under an EXEC mask, and hipcc
+        // then waits vmcnt(0) for its return at the branch join -- here the value is waited
+        // for only where it is used, before the barrier
+        int claim = 0;
+        if (dyn && wv0 == 0 && gn < ngroups)
+            claim = __hip_atomic_fetch_add(a.drain + (lane ? 2 + lane : 0), lane ? 0 : 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
         // epilogue inputs of this group (independent of the dot products)
         int er0 = 0, er1 = 0;
         float ein0 = 0.f, ein1 = 0.f, esc0 = 1.f, esc1 = 1.f;
@@ -1193,7 +1210,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 scur[i] = WQ8 ? wsc[i] : 1.0f;
             }
         }
-        g += gridDim.x;
+        g = gn;
         // The next group's loads go out before this group's reduction, unconditionally: a
         // load under `if (more)` keeps the old weight registers alive across the branch and
         // doubles the weight register set (fewer resident blocks).  Past the last group they
@@ -1212,6 +1229,10 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < RB; i++) red[buf][wave][i] = acc[i];
+        }
+        if (dyn && wv0 == 0) {
+            const int c0 = __builtin_amdgcn_readfirstlane(claim);
+            if (lane == 0) s_next[buf] = g < ngroups ? min(2 * G + c0, ngroups) : ngroups;
         }
         __syncthreads();
         if (!LOGIT && owner) {
@@ -1255,10 +1276,19 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 if (EPI == EPI_LOGITS_ALT) alt_row(v[i], rcur[i], am, as, tv, ti);
             }
         }
+        gn = dyn ? s_next[buf] : g + G;
         buf ^= 1;
         if (g >= ngroups) break;
     }
     GEMV_STAMP(2);
+    if (dyn && tid == 0) {
+        // every claim of this block has returned: the last block out resets the counters for
+        // the next launch on the stream (stream order makes the reset visible to it)
+        if (__hip_atomic_fetch_add(a.drain + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+            __hip_atomic_store(a.drain, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.drain + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if ((EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT) && wave == 0 && lane == 0) {
         a.part_val[blockIdx.x] = best;
         a.part_idx[blockIdx.x] = besti;

@@ -1063,7 +1063,12 @@ int vh_sched_run(vh_sched_t *q) {
             const double t0 = now_ms();
             if (vox_hip_stream_encode_mel_batch(hs, mp, nf, nb, 1, added) < 0)
                 return fail("batched encoder: %s", vox_hip_last_error());
+            /* the pass completes here (the batched decode would wait for it anyway), so its
+             * time is the encoder's, not the decoder's */
+            for (int k = 0; k < nb; k++)
+                if (vox_hip_stream_sync(hs[k])) return fail("encoder: %s", vox_hip_last_error());
             const double dt = now_ms() - t0;
+            q->stats.enc_ms += dt;
             q->stats.enc_batches++;
             for (int k = 0; k < nb; k++) {
                 vh_stream_t *s = q->s[idx[k]];

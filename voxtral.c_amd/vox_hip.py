@@ -637,7 +637,7 @@ class SchedStats(ctypes.Structure):
     _fields_ = [("runs", ctypes.c_int), ("prefills", ctypes.c_int), ("batch_calls", ctypes.c_int),
                 ("tokens", ctypes.c_longlong), ("run_ms", ctypes.c_double), ("batch_ms", ctypes.c_double),
                 ("enc_batches", ctypes.c_int), ("steps", ctypes.c_longlong), ("captures", ctypes.c_longlong),
-                ("prefill_passes", ctypes.c_longlong)]
+                ("prefill_passes", ctypes.c_longlong), ("enc_ms", ctypes.c_double)]
 
 
 def host_lib():

@@ -137,7 +137,8 @@ void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out);
  * stream, as vox_stream_feed does. */
 void vh_sched_set_step_cap(vh_sched_t *q, int cap);
 
-/* vox_load_wav (voxtral_audio.c:143-166) for 16 kHz mono 16-bit PCM: malloc'd samples */
+/* vox_load_wav (voxtral_audio.c:49-166): 16-bit PCM WAV of any channel count and rate, mixed
+ * to mono and linearly resampled to 16 kHz as the reference does: malloc'd samples */
 float *vh_load_wav(const char *path, int *n_samples);
 
 #ifdef __cplusplus

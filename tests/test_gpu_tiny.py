@@ -114,6 +114,43 @@ def test_encode_mel_batch_matches_oracle(models, tiny_cfg):
         os_[i].close()
 
 
+def test_encode_mel_batch_rejects_duplicate_stream(models, tiny_cfg):
+    """a stream listed twice in one batched encoder pass would append its K/V
+    twice at the same positions; the call refuses it and leaves the stream untouched."""
+    import vox_hip
+    hm, _ = models
+    s = vox_hip.Stream(hm)
+    mel = np.zeros((40, tiny_cfg.mel_bins), np.float32)
+    with pytest.raises(RuntimeError, match="twice"):
+        vox_hip.encode_mel_batch([s, s], [mel, mel])
+    assert s.adapter_tokens == 0
+    s.close()
+
+
+def test_window_256_decodes_past_256(tiny_weights, jfk_samples):
+    """with a decoder window of exactly 256 the short-context attention kernel (keys
+    = ring slots 0..lp, valid only while nothing has left the window) must not serve contexts
+    at or past 256 positions; decoding ~400 positions on TINY with dec_window = 256 gives the
+    oracle's ids."""
+    import dataclasses
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY
+    cfg = dataclasses.replace(TINY, dec_window=256)
+    samples = np.concatenate([jfk_samples] * 3)
+    events = vox_oracle.transcribe_mel_schedule(samples)
+    hm = vox_hip.Model(cfg, tiny_weights)
+    om = vox_oracle.OracleModel(cfg, tiny_weights)
+    hs, os_ = vox_hip.Stream(hm), vox_oracle.OracleStream(om)
+    hsess, osess = vox_hip.Session(hs), vox_oracle.OracleSession(os_)
+    for kind, mel in events:
+        getattr(hsess, kind)(mel, stop_at_eos=False)
+        getattr(osess, kind)(mel, stop_at_eos=False)
+    assert len(osess.tokens) > 300
+    assert hsess.tokens == osess.tokens
+    hs.close(); os_.close(); hm.close(); om.close()
+
+
 def test_jfk_transcribe_tokens_match(models, jfk_samples):
     """vox_transcribe_audio schedule on jfk.wav (1355 / 140 / 1 mel-frame chunks)."""
     import vox_hip

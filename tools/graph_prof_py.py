@@ -1,0 +1,40 @@
+"""Which graph replays does rocprofv3 --kernel-trace survive?  (the C2 bench
+ends in SIGSEGV under rocprofv3 inside hipGraphLaunch.)  One mode per process, TINY shapes:
+  plain  -- single-stream decode, step graphs replayed, no profiling events
+  prof   -- the same with Stream.set_profiling(True): the last step of each batch launched
+            eagerly through hipExtLaunchKernel with dispatch-recorded events, as bench.py does
+  batch  -- the batched decode's slot-table step graphs
+Run: rocprofv3 --kernel-trace --stats -d DIR -o x -- python3 tools/graph_prof_py.py MODE"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "voxtral.c_amd"))
+import vox_hip  # noqa: E402
+from vox_weights import TINY, synth_weights  # noqa: E402
+
+mode = sys.argv[1] if len(sys.argv) > 1 else "plain"
+w = synth_weights(TINY, seed=1)
+m = vox_hip.Model(TINY, w)
+rng = np.random.default_rng(0)
+mels = [rng.uniform(-0.5, 1.5, size=(900, TINY.mel_bins)).astype(np.float32) for _ in range(4)]
+if mode == "batch":
+    ss = [vox_hip.Stream(m) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(m, 4)
+    n = sum(len(t) for t in b.decode(ss, max_steps=1000, stop_at_eos=False))
+    b.close()
+    for s in ss:
+        s.close()
+else:
+    st = vox_hip.Stream(m)
+    st.encode_mel(mels[0])
+    if mode == "prof":
+        st.set_profiling(True)
+    n = len(st.decode(stop_at_eos=False))
+    st.close()
+m.close()
+print(f"{mode}: {n} tokens, exited cleanly", flush=True)

@@ -10,6 +10,6 @@ for d in 0 1; do VOX_HIP_GEMV_DRAIN=$d timeout -k 10 200 python -u bench.py --no
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 1 > gpurun_out/r4b_serve16.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 1 --serve-step-cap 0 > gpurun_out/r4b_serve16_nocap.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 8 --steps 1 --warmup 1 > gpurun_out/r4b_serve8.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
-VOX_HIP_GRAPH=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r4b_prof_serve16 -o serve16 -- python3 -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 0 --serve-seconds 40 > gpurun_out/r4b_prof_serve16.log 2>&1 || { tail -20 gpurun_out/r4b_prof_serve16.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4b_prof_graph -o c2 -- python3 -u bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/r4b_prof_graph.log 2>&1 || { tail -30 gpurun_out/r4b_prof_graph.log; exit 1; }
-echo rc=0
+VOX_HIP_GRAPH=0 timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/r4b_prof -o serve -- python3 -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 0 --serve-seconds 40 > gpurun_out/r4b_prof_serve16.json 2> gpurun_out/r4b_prof.err || { tail -20 gpurun_out/r4b_prof.err; exit 1; }
+python3 tools/db_stats.py /tmp/r4b_prof/serve_results.db 45 > gpurun_out/r4b_serve16_kernel_stats.txt
+echo rc=$?

@@ -1146,8 +1146,74 @@ int vh_sched_run(vh_sched_t *q) {
 }
 
 /* ------------------------------------------------------------------------
- * WAV (voxtral_audio.c:49-166): RIFF / WAVE, "fmt " PCM 16-bit mono 16 kHz, "data"
+ * WAV (voxtral_audio.c:49-166): RIFF / WAVE, "fmt " 16-bit PCM, any channel count (mixed
+ * down by the mean), any sample rate (linear interpolation to 16 kHz in the reference's f32
+ * arithmetic); a "data" size of 0xFFFFFFFF (piped ffmpeg) or past the end means "to the end"
  * ------------------------------------------------------------------------ */
+static float *parse_wav(const uint8_t *d, long size, int *n_samples, const char *path) {
+    if (size < 44 || memcmp(d, "RIFF", 4) || memcmp(d + 8, "WAVE", 4)) {
+        fail("%s: not a RIFF/WAVE file", path);
+        return NULL;
+    }
+    int channels = 0, rate = 0, bits = 0, fmt = 0;
+    const uint8_t *pcm = NULL;
+    long pcm_size = 0;
+    const uint8_t *p = d + 12, *end = d + size;
+    while (p + 8 <= end) {
+        uint32_t len;
+        memcpy(&len, p + 4, 4);
+        if (!memcmp(p, "fmt ", 4) && len >= 16 && (long)len <= end - p - 8) {
+            fmt = p[8] | p[9] << 8;
+            channels = p[10] | p[11] << 8;
+            rate = p[12] | p[13] << 8 | p[14] << 16 | p[15] << 24;
+            bits = p[22] | p[23] << 8;
+        } else if (!memcmp(p, "data", 4)) {
+            pcm = p + 8;
+            pcm_size = (int32_t)len;
+            if (pcm_size <= 0 || pcm_size > end - pcm) pcm_size = end - pcm;
+            break;
+        }
+        if ((long)len > end - p - 8) break;
+        p += 8 + (long)len + (len & 1);
+    }
+    if (fmt != 1 || bits != 16 || !pcm || channels < 1 || rate <= 0) {
+        fail("%s: unsupported WAV (need 16-bit PCM; fmt %d, %d bit, %d ch, %d Hz)", path, fmt, bits, channels, rate);
+        return NULL;
+    }
+    const int n = (int)(pcm_size / (channels * 2));
+    float *x = malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) {
+        if (channels == 1) {
+            int16_t v;
+            memcpy(&v, pcm + 2 * (size_t)i, 2);
+            x[i] = v / 32768.0f;
+        } else {
+            float sum = 0;
+            for (int c = 0; c < channels; c++) {
+                int16_t v;
+                memcpy(&v, pcm + 2 * ((size_t)i * channels + c), 2);
+                sum += v;
+            }
+            x[i] = (sum / channels) / 32768.0f;
+        }
+    }
+    if (rate == 16000) {
+        *n_samples = n;
+        return x;
+    }
+    const int m = (int)((long long)n * 16000 / rate);
+    float *y = malloc(sizeof(float) * (size_t)(m > 0 ? m : 1));
+    for (int i = 0; i < m; i++) {
+        const float pos = (float)i * rate / 16000;
+        const int k = (int)pos;
+        const float fr = pos - k;
+        y[i] = k + 1 < n ? x[k] * (1.0f - fr) + x[k + 1] * fr : (k < n ? x[k] : 0.0f);
+    }
+    free(x);
+    *n_samples = m;
+    return y;
+}
+
 float *vh_load_wav(const char *path, int *n_samples) {
     FILE *fp = fopen(path, "rb");
     if (!fp) {
@@ -1161,44 +1227,8 @@ float *vh_load_wav(const char *path, int *n_samples) {
     const size_t got = size > 0 ? fread(buf, 1, (size_t)size, fp) : 0;
     fclose(fp);
     float *out = NULL;
-    if ((long)got != size) {
-        fail("%s: short read", path);
-        goto end;
-    }
-    if (size < 12 || memcmp(buf, "RIFF", 4) || memcmp(buf + 8, "WAVE", 4)) {
-        fail("%s: not a RIFF/WAVE file", path);
-        goto end;
-    }
-    int channels = 0, rate = 0, bits = 0, fmt = 0;
-    for (long p = 12; p + 8 <= size;) {
-        uint32_t len;
-        memcpy(&len, buf + p + 4, 4);
-        const uint8_t *d = buf + p + 8;
-        if (!memcmp(buf + p, "fmt ", 4) && len >= 16) {
-            fmt = d[0] | d[1] << 8;
-            channels = d[2] | d[3] << 8;
-            rate = d[4] | d[5] << 8 | d[6] << 16 | d[7] << 24;
-            bits = d[14] | d[15] << 8;
-        } else if (!memcmp(buf + p, "data", 4)) {
-            if (fmt != 1 || channels != 1 || rate != 16000 || bits != 16) {
-                fail("%s: need 16 kHz mono 16-bit PCM (fmt %d, %d ch, %d Hz, %d bit)", path, fmt, channels, rate, bits);
-                goto end;
-            }
-            if (p + 8 + (long)len > size) len = (uint32_t)(size - p - 8);
-            const int n = (int)(len / 2);
-            out = malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
-            for (int i = 0; i < n; i++) {
-                int16_t v;
-                memcpy(&v, d + 2 * i, 2);
-                out[i] = v / 32768.0f;
-            }
-            *n_samples = n;
-            goto end;
-        }
-        p += 8 + len + (len & 1);
-    }
-    fail("%s: no data chunk", path);
-end:
+    if (size <= 0 || (long)got != size) fail("%s: short read", path);
+    else out = parse_wav(buf, size, n_samples, path);
     free(buf);
     return out;
 }

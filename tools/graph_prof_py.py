@@ -16,10 +16,16 @@ import vox_hip  # noqa: E402
 from vox_weights import TINY, synth_weights  # noqa: E402
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "plain"
+# the process's mappings, so a crash's frame addresses can be put to library + offset and
+# symbolised afterwards (llvm-symbolizer --obj=LIB OFFSET on the same image)
+maps_out = os.environ.get("VOX_GP_MAPS")
 w = synth_weights(TINY, seed=1)
 m = vox_hip.Model(TINY, w)
 rng = np.random.default_rng(0)
 mels = [rng.uniform(-0.5, 1.5, size=(900, TINY.mel_bins)).astype(np.float32) for _ in range(4)]
+if maps_out:
+    with open("/proc/self/maps") as f, open(maps_out, "w") as o:
+        o.write(f.read())
 if mode == "batch":
     ss = [vox_hip.Stream(m) for _ in mels]
     for s, mel in zip(ss, mels):

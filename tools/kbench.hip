@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wide, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wide, g_sklp_bpc, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -207,6 +207,29 @@ int main(int argc, char** argv) {
         qs = nullptr;
         return 0;
     }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "sklp")) {
+        // batched decode projections at 16 rows: k_skl (one burst of loads per block) against
+        // the streaming k_sklp (persistent blocks walking their column groups), cold weights
+        uint16_t* xp = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * 9216 * 2, 1);
+        float* part = (float*)dmalloc((size_t)2 * 16 * 18 * 18432 * 4, 0);
+        float* ssq = (float*)dmalloc(16 * 16 * 4, 1);
+        struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
+        const S shapes[] = {S{"qkv 6144x3072", DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
+                            S{"wo  3072x4096", D, DQ, wo.data(), (double)D * DQ * 2},
+                            S{"w13 18432x3072", 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
+                            S{"w2  3072x9216", D, DH, w2.data(), (double)D * DH * 2}};
+        for (int rep = 0; rep < 2; rep++)
+            for (const S& g : shapes) {
+                char nm[96];
+                snprintf(nm, sizeof nm, "skl  %s nb16", g.n);
+                add(nm, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
+                snprintf(nm, sizeof nm, "sklp %s nb16", g.n);
+                add(nm, timeit([&] { CK(launch_gemm_sklp(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
+                snprintf(nm, sizeof nm, "sklp %s nb16 + rms scale", g.n);
+                add(nm, timeit([&] { CK(launch_gemm_sklp(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st, ssq, 12, 1e-5f)); }, iters, st), g.bytes);
+            }
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "skb")) {
         // batched decode projections at 16 rows: split-K k_skl (slabs, a row kernel sums them)
         // against whole-K k_skf (final rows: the row kernel's slab sum could go)
@@ -285,11 +308,45 @@ int main(int argc, char** argv) {
         int* states = nullptr;
         CK(hipMalloc(&states, 16 * 16));
         float* parts = (float*)dmalloc((size_t)16 * (H * 128 * (HD + 2) * 4 + 4096), 0);
+        BatchSlot* slots = nullptr;
+        CK(hipMalloc(&slots, sizeof(BatchSlot) * 16));
         for (int nb : {16, 8})
-            for (int L : {64, 128, 190, 256}) {
+            for (int L : {64, 128, 190, 256, 512, 1024}) {
                 std::vector<int> hs(16 * 4, 0);
                 for (int z = 0; z < 16; z++) hs[z * 4] = L - 1;
                 CK(hipMemcpy(states, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+                const int need = (L + 255) / 256;
+                int splits = 1;
+                while (splits < need) splits *= 2;
+                {
+                    // the engine's form since round 4: rings, position and liveness from the slot
+                    // table (layer base + ring_off), the graph's arguments independent of streams
+                    std::vector<BatchSlot> hsl(16);
+                    memset(hsl.data(), 0, sizeof(BatchSlot) * 16);
+                    int l = 0;
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "attn batch slots nb=%d L=%d splits=%d", nb, L, splits);
+                    for (int z = 0; z < 16; z++) {
+                        hsl[z].state = states + z * 4;
+                        hsl[z].Kc = reinterpret_cast<char*>(Ks[z * 2]);
+                        hsl[z].Vc = reinterpret_cast<char*>(Vs[z * 2]);
+                        hsl[z].live = z < nb;
+                        hsl[z].pos = L - 1;
+                    }
+                    CK(hipMemcpy(slots, hsl.data(), sizeof(BatchSlot) * 16, hipMemcpyHostToDevice));
+                    add(nm, timeit([&] {
+                            const int lay = l % 13;  // 13 layers' rings per stream (cold K/V)
+                            AttnPtrs p;
+                            memset(&p, 0, sizeof p);
+                            p.slots = slots;
+                            p.ring_off = (size_t)lay * rcap * DKV * 4;
+                            for (int z = 0; z < nb; z++) p.part[z] = parts + (size_t)z * (H * 128 * (HD + 2) + 1024);
+                            AttnFuse f{slabs, S6, N, rope, xs};
+                            CK(launch_attn_batch_fused(HD, p, f, nb, rcap, 8192, 0.088f, H, KVH, splits, st, 0));
+                            l++;
+                        }, iters, st), (double)nb * L * DKV * 2 * 4);
+                }
+                if (L > 256) continue;
                 for (int bs : {0, 1}) {
                     g_attn_bsplit = bs;
                     int l = 0;

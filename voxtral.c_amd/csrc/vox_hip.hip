@@ -2354,6 +2354,14 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     return b;
 }
 
+// the batched step's projections: k_skl (a burst per block) or the streaming k_sklp
+// (VOX_HIP_BATCH_SKLP=1); the same slabs either way
+static hipError_t batch_gemm(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* part,
+                             hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f) {
+    if (sklp_on()) return launch_gemm_sklp(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
+    return launch_gemm_skl(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
+}
+
 // one batched step over slots 0..nb-1 of the slot table (their input rows already in b->x)
 static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
     vox_hip_model_t* m = b->m;
@@ -2379,6 +2387,7 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         xw_env = (e && atoi(e) == 0) ? 0 : 1;
     }
     const bool xw = xw_env && DD % 256 == 0 && DD / 256 <= SKL_MAX_SLICES;
+    const bool sp = sklp_on();  // streaming projections: W1|W3 + k_swiglu_fplanes (no ticket fold)
     static int wox = -1;
     if (wox < 0) {
         const char* e = getenv("VOX_HIP_BATCH_WOX");
@@ -2401,17 +2410,17 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         if (xw) {
             CK(launch_resid_xw_fplanes(b->x, nb, DD, L.attn_norm, nullptr, b->xp_d, b->part, l ? Sres : 0, nullptr,
                                        b->ssq, st));
-            CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
+            CK(batch_gemm(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
         } else {
             CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, b->part, l ? Sres : 0, st));
-            CK(launch_gemm_skl(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
+            CK(batch_gemm(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
         }
         // RoPE + KV append + attention of every live slot, output into the wo planes (one
         // launch; past 256 keys the last key-range block of a kv head merges the partials)
         AttnFuse af;
         af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
         CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
-        const bool fuse_wo = xw && swx && wox && !L.so && !L.s13;
+        const bool fuse_wo = xw && swx && wox && !L.so && !L.s13 && !sp;
         if (fuse_wo) {
             // wo with the residual folded in (k_sklx: the last block of each column slice sums
             // its slabs into x and writes the slice's x * ffn_norm * (1 + ada) planes and row
@@ -2421,9 +2430,9 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
             fo.nw = L.ffn_norm; fo.ada = m->ada_scale + (size_t)l * DD;
             CK(launch_gemm_sklx(SKX_PRO_PLANES, SKX_EPI_RESID, b->xp_q, DQ, F.wo, DD, nb, fo, st));
         } else {
-            CK(launch_gemm_skl(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
+            CK(batch_gemm(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
         }
-        if (xw && swx && !L.s13) {
+        if (xw && swx && !L.s13 && !sp) {
             // W1|W3 with the SwiGLU folded in (k_sklx: the last block of each column slice
             // sums its slabs and writes the w2 planes; no k_swiglu_fplanes launch)
             if (!fuse_wo)
@@ -2434,19 +2443,19 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
             f.part = b->part; f.ticket = b->ticket;
             f.planes = b->xp_h;
             CK(launch_gemm_sklx(SKX_PRO_SCALE, SKX_EPI_SWIGLU, b->xp_d, DD, F.w13, 2 * DH, nb, f, st));
-            CK(launch_gemm_skl(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
+            CK(batch_gemm(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
             continue;
         } else if (xw) {
             CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
                                        skl_splits(DQ), nullptr, b->ssq, st));
-            CK(launch_gemm_skl(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
+            CK(batch_gemm(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
         } else {
             CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d,
                                       b->part, skl_splits(DQ), st));
-            CK(launch_gemm_skl(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st));
+            CK(batch_gemm(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st));
         }
         CK(launch_swiglu_fplanes(b->part, skl_splits(DD), DH, nb, b->xp_h, st));
-        CK(launch_gemm_skl(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
+        CK(batch_gemm(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
     }
     // final norm (after the last w2 residual) + LM head (tied embeddings) + per-slot argmax,
     // state, token log and next inputs (decoder.c:762-779)

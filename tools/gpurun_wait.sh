@@ -7,8 +7,8 @@ out=$1; script=$2; to=${3:-1200}
 for i in $(seq 1 12); do
   timeout $((to + 1800)) /usr/local/graft/bin/gpurun --timeout "$to" -- bash "$script" > "$out" 2>&1
   if grep -q -E "no free box|slot\(s\) on this pod are busy|status=transient" "$out"; then
-    echo "[wait] attempt $i: no box, retrying in 600 s" >> "$out.attempts"
-    sleep 600
+    echo "[wait] attempt $i: no box, retrying" >> "$out.attempts"
+    if grep -q "backing off" "$out"; then sleep 480; else sleep 150; fi
     continue
   fi
   break

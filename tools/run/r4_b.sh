@@ -8,15 +8,8 @@ VOX_KB_ONLY=gemmf timeout -k 10 200 tools/kbench 50 > gpurun_out/r4b_kb_gemmf.tx
 VOX_KB_ONLY=attb timeout -k 10 200 tools/kbench 100 > gpurun_out/r4b_kb_attb.txt 2>&1 || { tail -20 gpurun_out/r4b_kb_attb.txt; exit 1; }
 VOX_HIP_BATCH_SKLP=1 timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_batch.py -k "not full_size" > gpurun_out/r4b_test_sklp.log 2>&1 || { tail -40 gpurun_out/r4b_test_sklp.log; exit 1; }
 VOX_KB_ONLY=sklp timeout -k 10 120 tools/kbench 100 > gpurun_out/r4b_kb_sklp.txt 2>&1 || { tail -20 gpurun_out/r4b_kb_sklp.txt; exit 1; }
-for sp in 0 1 0 1; do VOX_HIP_BATCH_SKLP=$sp timeout -k 10 200 python -u bench.py --no-cpu-baseline --streams 16 > gpurun_out/r4b_s16_sklp$sp.json 2>> gpurun_out/r4b.err || exit 1; cat gpurun_out/r4b_s16_sklp$sp.json >> gpurun_out/r4b_s16_sklp_ab.jsonl; done
 for d in 0 1 0 1; do VOX_HIP_GEMV_DRAIN=$d timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/r4b_c2_d$d.json 2>> gpurun_out/r4b.err || exit 1; cat gpurun_out/r4b_c2_d$d.json >> gpurun_out/r4b_c2_ab.jsonl; done
 for d in 0 1; do VOX_HIP_GEMV_DRAIN=$d timeout -k 10 200 python -u bench.py --no-cpu-baseline --q8 --steps 10 --warmup 2 > gpurun_out/r4b_q8_d$d.json 2>> gpurun_out/r4b.err || exit 1; done
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 1 > gpurun_out/r4b_serve16.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 1 --serve-step-cap 0 > gpurun_out/r4b_serve16_nocap.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --stagger --streams 8 --steps 1 --warmup 1 > gpurun_out/r4b_serve8.json 2>> gpurun_out/r4b.err || { tail -20 gpurun_out/r4b.err; exit 1; }
-VOX_HIP_GRAPH=0 timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/r4b_prof -o serve -- python3 -u bench.py --no-cpu-baseline --stagger --streams 16 --steps 1 --warmup 0 --serve-seconds 40 > gpurun_out/r4b_prof_serve16.json 2> gpurun_out/r4b_prof.err || { tail -20 gpurun_out/r4b_prof.err; exit 1; }
-python3 tools/db_stats.py /tmp/r4b_prof/serve_results.db 45 > gpurun_out/r4b_serve16_kernel_stats.txt
-echo rc_stats=$?
 # rocprofv3 on graph replays: which replay survives the profiler
 for mode in plain batch prof; do
   VOX_GP_MAPS=gpurun_out/r4b_gp_maps_$mode.txt timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /tmp/r4b_gp_$mode -o gp -- python3 -u tools/graph_prof_py.py $mode > gpurun_out/r4b_gp_$mode.log 2>&1 || { echo "graph profile $mode failed rc=$?"; tail -40 gpurun_out/r4b_gp_$mode.log; exit 1; }

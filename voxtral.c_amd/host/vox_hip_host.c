@@ -1026,8 +1026,11 @@ int vh_stream_pending(vh_stream_t *s) {
     vox_hip_stream_state(s->st, st6);
     if (st6[4]) return 0;  /* EOS: nothing more is decoded (non-continuous) */
     const int rows = vox_hip_stream_adapter_tokens(s->st);
-    if (!st6[3]) return rows >= 1 + 32 + s->ctx->delay_tokens ? rows - (32 + s->ctx->delay_tokens) : 0;
-    return rows - st6[1] > 0 ? rows - st6[1] : 0;
+    int left;
+    if (!st6[3]) left = rows >= 1 + 32 + s->ctx->delay_tokens ? rows - (32 + s->ctx->delay_tokens) : 0;
+    else left = rows - st6[1] > 0 ? rows - st6[1] : 0;
+    /* a chunk deferred for the scheduler's encoder pass has rows to come */
+    return left + (s->pend_n > 0);
 }
 
 void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {

@@ -810,9 +810,11 @@ def bench_serve(args, d, cfg, model, st0):
         cur = [None] * S        # [HostStream, clip index, next sample, finished]
         nxt = list(range(S))
         ids, lat, clips_done, tick = 0, [], 0, 0
+        full = [0, 0.0]         # ids and wall time of the ticks in which all S streams were live
         t_all = time.perf_counter()
         while True:
             live = False
+            n_live = 0
             t0 = time.perf_counter()
             for k in range(S):
                 if tick < 2 * k:             # staggered start
@@ -826,6 +828,7 @@ def bench_serve(args, d, cfg, model, st0):
                     cur[k] = [hs, nxt[k] % len(clips), 0, False]
                     nxt[k] += 1
                 live = True
+                n_live += 1
                 hs, c, pos, fin = cur[k]
                 if fin:                       # finished, rows still being decoded (step cap)
                     continue
@@ -838,20 +841,25 @@ def bench_serve(args, d, cfg, model, st0):
             if not live:
                 break
             q.run()
+            tick_ids = 0
             for k in range(S):
                 if cur[k] is None:
                     continue
-                ids += len(cur[k][0].get())
+                tick_ids += len(cur[k][0].get())
                 if cur[k][3] and cur[k][0].pending() == 0:   # finished and drained: retire the clip
                     served[k] += len(clips[cur[k][1]]) / 16000.0
                     q.detach(cur[k][0])
                     cur[k][0].close()
                     cur[k] = None
                     clips_done += 1
+            ids += tick_ids
             lat.append(time.perf_counter() - t0)
+            if n_live == S:
+                full[0] += tick_ids
+                full[1] += lat[-1]
             tick += 1
         return {"wall": time.perf_counter() - t_all, "ids": ids, "lat": lat, "ticks": tick,
-                "clips": clips_done, "audio_s": sum(served)}
+                "clips": clips_done, "audio_s": sum(served), "full_ids": full[0], "full_s": full[1]}
 
     for _ in range(args.warmup):
         run(min(args.serve_seconds, 20.0))
@@ -891,6 +899,12 @@ def bench_serve(args, d, cfg, model, st0):
         "audio_seconds_per_wall_second": round(audio_all / wall, 2),
         "overall_rtf_per_stream": round(wall / (audio_all / d.world / S), 5),
         "clips": sum(r["clips"] for r in runs),
+        # the ticks in which every one of the S streams was live (the stagger ramp and the tail
+        # of the longest clips excluded): the scheduler's rate at full occupancy
+        "all_streams_live": {"ids": sum(r["full_ids"] for r in runs),
+                             "s": round(sum(r["full_s"] for r in runs), 3),
+                             "ids_per_s": round(sum(r["full_ids"] for r in runs) / max(1e-9, sum(r["full_s"] for r in runs)), 1),
+                             "share_of_wall": round(sum(r["full_s"] for r in runs) / max(1e-9, sum(r["wall"] for r in runs)), 3)},
         "batched_decode": {"ids": batch_tok, "ms": round(batch_ms, 1),
                            "ids_per_s": round(batch_tok / max(1e-9, batch_ms * 1e-3), 1),
                            "steps": batch_steps, "rows_per_step": round(batch_tok / max(1, batch_steps), 2),

@@ -220,3 +220,33 @@ def test_scheduler_alt_stream_stays_batched(tiny_weights, jfk_samples):
     assert (got[:, 1] >= 0).any()
     assert st["tokens"] == sum(len(np.concatenate(r)) for r in recs), st
     hm.close()
+
+
+@pytest.mark.slow
+def test_scheduler_full_size_matches_oracle(jfk_samples):
+    """The served composite at full Voxtral-4B shapes: three streams of
+    3-5 s fed in 0.5 s pieces with staggered starts through one scheduler (cross-stream encoder
+    passes, stacked prefills, slot-table batched steps, a step cap of 4 so prompts and flush
+    paddings drain over later runs); every stream's ids equal its own oracle session on the
+    same pieces."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import VOXTRAL_4B, synth_weights
+    w = synth_weights(VOXTRAL_4B, seed=0)
+    hm = vox_hip.Model(VOXTRAL_4B, w)
+    a = np.concatenate([jfk_samples] * 2)
+    audios = [np.ascontiguousarray(a[:16000 * 5]), np.ascontiguousarray(-a[20000:20000 + 16000 * 4]),
+              np.ascontiguousarray(a[70000:70000 + 16000 * 3])]
+    ids, st = _serve(hm, audios, [0, 2, 3], 0.5, step_cap=4)
+    hm.close()
+    om = vox_oracle.OracleModel(VOXTRAL_4B, w)
+    import os
+    vox_oracle.set_threads(min(16, os.cpu_count() or 1))
+    for k, au in enumerate(audios):
+        ref, _ = _oracle_ids(om, au, 0.5)
+        assert len(ref) > 20
+        assert ids[k] == ref, (k, len(ids[k]), len(ref), next((i for i in range(min(len(ref), len(ids[k])))
+                                                               if ids[k][i] != ref[i]), None))
+    om.close()
+    assert st["prefill_passes"] >= 1 and st["steps"] > 0
+    print("full-size scheduler stats", st)

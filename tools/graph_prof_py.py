@@ -4,6 +4,7 @@ ends in SIGSEGV under rocprofv3 inside hipGraphLaunch.)  One mode per process, T
   prof   -- the same with Stream.set_profiling(True): the last step of each batch launched
             eagerly through hipExtLaunchKernel with dispatch-recorded events, as bench.py does
   batch  -- the batched decode's slot-table step graphs
+  full   -- plain at the full Voxtral-4B shapes (synthetic weights, 200 graph-replayed steps)
 Run: rocprofv3 --kernel-trace --stats -d DIR -o x -- python3 tools/graph_prof_py.py MODE"""
 import os
 import sys
@@ -13,16 +14,18 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "voxtral.c_amd"))
 import vox_hip  # noqa: E402
-from vox_weights import TINY, synth_weights  # noqa: E402
+from vox_weights import TINY, VOXTRAL_4B, synth_weights  # noqa: E402
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "plain"
 # the process's mappings, so a crash's frame addresses can be put to library + offset and
 # symbolised afterwards (llvm-symbolizer --obj=LIB OFFSET on the same image)
 maps_out = os.environ.get("VOX_GP_MAPS")
-w = synth_weights(TINY, seed=1)
-m = vox_hip.Model(TINY, w)
+cfg = VOXTRAL_4B if mode == "full" else TINY
+w = synth_weights(cfg, seed=1)
+m = vox_hip.Model(cfg, w)
+del w
 rng = np.random.default_rng(0)
-mels = [rng.uniform(-0.5, 1.5, size=(900, TINY.mel_bins)).astype(np.float32) for _ in range(4)]
+mels = [rng.uniform(-0.5, 1.5, size=(900, cfg.mel_bins)).astype(np.float32) for _ in range(4)]
 if maps_out:
     with open("/proc/self/maps") as f, open(maps_out, "w") as o:
         o.write(f.read())
@@ -40,7 +43,7 @@ else:
     st.encode_mel(mels[0])
     if mode == "prof":
         st.set_profiling(True)
-    n = len(st.decode(stop_at_eos=False))
+    n = len(st.decode(max_steps=200, stop_at_eos=False)) if mode == "full" else len(st.decode(stop_at_eos=False))
     st.close()
 m.close()
 print(f"{mode}: {n} tokens, exited cleanly", flush=True)

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wide, g_sklp_bpc, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wide, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -205,29 +205,6 @@ int main(int argc, char** argv) {
             }
         g_gemv_maxb = 0;
         qs = nullptr;
-        return 0;
-    }
-    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "sklp")) {
-        // batched decode projections at 16 rows: k_skl (one burst of loads per block) against
-        // the streaming k_sklp (persistent blocks walking their column groups), cold weights
-        uint16_t* xp = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * 9216 * 2, 1);
-        float* part = (float*)dmalloc((size_t)2 * 16 * 18 * 18432 * 4, 0);
-        float* ssq = (float*)dmalloc(16 * 16 * 4, 1);
-        struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
-        const S shapes[] = {S{"qkv 6144x3072", DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
-                            S{"wo  3072x4096", D, DQ, wo.data(), (double)D * DQ * 2},
-                            S{"w13 18432x3072", 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
-                            S{"w2  3072x9216", D, DH, w2.data(), (double)D * DH * 2}};
-        for (int rep = 0; rep < 2; rep++)
-            for (const S& g : shapes) {
-                char nm[96];
-                snprintf(nm, sizeof nm, "skl  %s nb16", g.n);
-                add(nm, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
-                snprintf(nm, sizeof nm, "sklp %s nb16", g.n);
-                add(nm, timeit([&] { CK(launch_gemm_sklp(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st)); }, iters, st), g.bytes);
-                snprintf(nm, sizeof nm, "sklp %s nb16 + rms scale", g.n);
-                add(nm, timeit([&] { CK(launch_gemm_sklp(xp, g.K, g.W[layer++ % NL], nullptr, g.N, 16, part, st, ssq, 12, 1e-5f)); }, iters, st), g.bytes);
-            }
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "skb")) {

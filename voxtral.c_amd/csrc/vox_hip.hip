@@ -1531,12 +1531,13 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
 // otherwise pos/rope_row are host values (boundary twin).
 static int enqueue_lm_head(vox_hip_stream_t* s, const int* state);
 
-// decode GEMVs with dynamically claimed row groups (VOX_HIP_GEMV_DRAIN=0: the static map)
+// decode GEMVs with row groups claimed at run time: opt-in (VOX_HIP_GEMV_DRAIN=1); the
+// static block -> group map is the default (claims measured 3-4x slower)
 static int gemv_drain_env() {
     static int v = -1;
     if (v < 0) {
         const char* e = getenv("VOX_HIP_GEMV_DRAIN");
-        v = (e && atoi(e) == 0) ? 0 : 1;
+        v = (e && atoi(e) == 1) ? 1 : 0;
     }
     return v;
 }
@@ -2354,11 +2355,9 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     return b;
 }
 
-// the batched step's projections: k_skl (a burst per block) or the streaming k_sklp
-// (VOX_HIP_BATCH_SKLP=1); the same slabs either way
+// the batched step's projections: k_skl, one burst of column groups per block
 static hipError_t batch_gemm(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* part,
                              hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f) {
-    if (sklp_on()) return launch_gemm_sklp(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
     return launch_gemm_skl(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
 }
 
@@ -2387,7 +2386,6 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         xw_env = (e && atoi(e) == 0) ? 0 : 1;
     }
     const bool xw = xw_env && DD % 256 == 0 && DD / 256 <= SKL_MAX_SLICES;
-    const bool sp = sklp_on();  // streaming projections: W1|W3 + k_swiglu_fplanes (no ticket fold)
     static int wox = -1;
     if (wox < 0) {
         const char* e = getenv("VOX_HIP_BATCH_WOX");
@@ -2420,7 +2418,7 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         AttnFuse af;
         af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
         CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
-        const bool fuse_wo = xw && swx && wox && !L.so && !L.s13 && !sp;
+        const bool fuse_wo = xw && swx && wox && !L.so && !L.s13;
         if (fuse_wo) {
             // wo with the residual folded in (k_sklx: the last block of each column slice sums
             // its slabs into x and writes the slice's x * ffn_norm * (1 + ada) planes and row
@@ -2432,7 +2430,7 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         } else {
             CK(batch_gemm(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
         }
-        if (xw && swx && !L.s13 && !sp) {
+        if (xw && swx && !L.s13) {
             // W1|W3 with the SwiGLU folded in (k_sklx: the last block of each column slice
             // sums its slabs and writes the w2 planes; no k_swiglu_fplanes launch)
             if (!fuse_wo)

@@ -195,10 +195,6 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
                            int ldc, hipStream_t st);
 // split-K slabs part[s][16][N], s < skl_splits(K) (projections: k_skl)
 int skl_splits(int K);
-// k_sklp: the same slabs from persistent blocks that stream their column groups (<= 16 rows)
-hipError_t launch_gemm_sklp(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* part,
-                            hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f);
-bool sklp_on();  // VOX_HIP_BATCH_SKLP=1
 // ssq: RMSNorm applied to the results (planes from launch_resid_xw_fplanes, nsl slices per row)
 constexpr int SKL_MAX_SLICES = 12;  // D <= 3072
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,

@@ -2700,121 +2700,6 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
     }
 }
 
-// Streaming form of k_skl (batched decode, <= 16 rows): G persistent blocks, block b serving
-// k-split s = b % S and a contiguous range of the split's 16-column groups.  The split's planes
-// go into LDS once per block (not once per 16 x NW columns), and each wave walks its groups
-// g, g + NW, .. with the next group's KS weight blocks requested before the current group's
-// MFMAs -- the decode GEMV's streaming loop (k_gemv) instead of one burst per block.  Same
-// products, same slabs part[s][16][N] (same summation order) as k_skl.
-template <int WQ8, int KS>
-__device__ __forceinline__ void sklp_load(u32x4 (&a)[KS][WQ8 ? 1 : 2], __amdgpu_buffer_rsrc_t W, int g, int KB,
-                                          int kb0) {
-    constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int kb = 0; kb < KS; kb++)
-#pragma unroll
-        for (int t = 0; t < NH; t++)
-            a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(W, lane * 16 + t * 1024, (g * KB + kb0 + kb) * FB, 2);
-}
-
-template <int WQ8, int KS>
-__device__ __forceinline__ f32x4 sklp_mma(const u32x4 (&a)[KS][WQ8 ? 1 : 2], const uint4* xb) {
-    const int lane = threadIdx.x & 63;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < KS; kb++)
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            bf16x8 af;
-            if (WQ8) {
-                const u32x4 q = a[kb][0];
-                af = t ? i8x8_bf16(q.z, q.w) : i8x8_bf16(q.x, q.y);
-            } else {
-                const u32x4 q = a[kb][t];
-                af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
-            }
-#pragma unroll
-            for (int p = 0; p < 3; p++)
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, xb[((kb * 3 + p) * 2 + t) * 64 + lane]),
-                                                             acc, 0, 0, 0);
-        }
-    return acc;
-}
-
-template <int WQ8, int NW, int KS, int SC = 0>
-__global__ __launch_bounds__(NW * 64) void k_sklp(const uint16_t* __restrict__ xs, int K,
-                                                  const uint8_t* __restrict__ W, const float* __restrict__ wscale,
-                                                  int N, int nb, float* __restrict__ part,
-                                                  const float* __restrict__ ssq = nullptr, int nsl = 0, float eps = 0.f) {
-    __shared__ uint4 xb[KS * 6 * 64];  // [block][plane][half][lane]
-    __shared__ float s_sq[SC ? SK_ROWS * SKL_MAX_SLICES : 1];
-    constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
-    constexpr int NF = KS * 6 / NW;  // 16-B plane pieces per thread
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int KB = K >> 6, S = KB / KS, NGr = N >> 4;
-    const int b = blockIdx.x, G = gridDim.x;
-    const int s = b % S, jb = b / S, Js = (G - s + S - 1) / S;  // blocks serving split s
-    const int g0 = (int)((long long)NGr * jb / Js), g1 = (int)((long long)NGr * (jb + 1) / Js);
-    const int kb0 = s * KS;
-    const size_t P = (size_t)SK_ROWS * K;
-    const __amdgpu_buffer_rsrc_t Wd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W), 0, NGr * KB * FB, 0x00020000);
-    const __amdgpu_buffer_rsrc_t Wz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W), 0, 0, 0x00020000);
-    // planes first, then the first group's weights (vmcnt retires in issue order)
-    uint4 f[NF];
-#pragma unroll
-    for (int i = 0; i < NF; i++) {
-        const int idx = tid + i * NW * 64;
-        const int blk = idx / 384, rem = idx % 384;
-        const int p = rem >> 7, t = (rem >> 6) & 1, l = rem & 63;
-        f[i] = *reinterpret_cast<const uint4*>(xs + p * P + (size_t)((kb0 + blk) * 2 + t) * 512 + l * 8);
-    }
-    float sqv = 0.f;
-    if (SC) sqv = ssq[min(tid, nsl * SK_ROWS - 1)];
-    u32x4 a0[KS][NH], a1[KS][NH];
-    int g = g0 + wave;
-    sklp_load<WQ8, KS>(a0, g < g1 ? Wd : Wz, g < g1 ? g : 0, KB, kb0);
-#pragma unroll
-    for (int i = 0; i < NF; i++) xb[tid + i * NW * 64] = f[i];
-    if (SC && tid < nsl * SK_ROWS) s_sq[tid] = sqv;
-    __syncthreads();
-    const int j = lane & 15;
-    float inv = 1.f;
-    if (SC) {
-        float sv[SKL_MAX_SLICES];
-#pragma unroll
-        for (int t = 0; t < SKL_MAX_SLICES; t++) sv[t] = s_sq[min(t, nsl - 1) * SK_ROWS + j];
-        float ss = 0.f;
-#pragma unroll
-        for (int t = 0; t < SKL_MAX_SLICES; t++)
-            if (t < nsl) ss += sv[t];
-        inv = 1.0f / sqrtf(ss / (float)K + eps);
-    }
-    auto store = [&](const f32x4& acc, int gg) {
-        if (j < nb) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int row = gg * 16 + (lane >> 4) * 4 + i;
-                const float v = SC ? acc[i] * inv : acc[i];
-                part[((size_t)s * SK_ROWS + j) * N + row] = WQ8 ? v * wscale[row] : v;
-            }
-        }
-    };
-    // two register sets in turn (static indices): the next group's loads before this one's MFMAs
-    while (g < g1) {
-        const int ga = g + NW;
-        sklp_load<WQ8, KS>(a1, ga < g1 ? Wd : Wz, ga < g1 ? ga : 0, KB, kb0);
-        store(sklp_mma<WQ8, KS>(a0, xb), g);
-        g = ga;
-        if (g >= g1) break;
-        const int gb = g + NW;
-        sklp_load<WQ8, KS>(a0, gb < g1 ? Wd : Wz, gb < g1 ? gb : 0, KB, kb0);
-        store(sklp_mma<WQ8, KS>(a1, xb), g);
-        g = gb;
-    }
-}
-
 // Residual + the planes of an RMSNorm without its row reduction: x += the S slabs of the
 // previous projection (+ bias, summed in split order as k_resid_rmsnorm_fplanes), the row
 // written back, the planes of x * w (* (1 + ada)) -- the inverse RMS is applied by the next
@@ -3937,59 +3822,6 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
     SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4)
     SKL_X(1, 4, 8) SKL_X(1, 8, 8) SKL_X(1, 4, 4) SKL_X(1, 8, 4)
 #undef SKL_X
-    return hipErrorInvalidValue;
-}
-
-int g_sklp_bpc = 0;  // tools/kbench knob: k_sklp blocks per CU (0 = 1)
-template <int Q, int NW, int KS>
-static hipError_t sklp_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb, float* part,
-                              hipStream_t st, const float* ssq, int nsl, float eps) {
-    const int S = K / 64 / KS;
-    int cus = 256;
-    {
-        static int c = 0;
-        if (!c) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-                c = 256;
-        }
-        cus = c;
-    }
-    // one block per CU, a whole number of blocks per k-split, never more blocks per split than
-    // the split has groups
-    const int per = std::max(1, std::min((cus * (g_sklp_bpc ? g_sklp_bpc : 1) + S - 1) / S, N / 16));
-    const int grid = per * S;
-    if (ssq)
-        hipLaunchKernelGGL((k_sklp<Q, NW, KS, 1>), dim3(grid), dim3(NW * 64), 0, st, xs, K,
-                           static_cast<const uint8_t*>(W), wscale, N, nb, part, ssq, nsl, eps);
-    else
-        hipLaunchKernelGGL((k_sklp<Q, NW, KS, 0>), dim3(grid), dim3(NW * 64), 0, st, xs, K,
-                           static_cast<const uint8_t*>(W), wscale, N, nb, part, nullptr, 0, 0.f);
-    LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-int g_sklp = -1;  // streaming skinny GEMM for the batched step's projections (VOX_HIP_BATCH_SKLP=1)
-bool sklp_on() {
-    if (g_sklp < 0) {
-        const char* e = getenv("VOX_HIP_BATCH_SKLP");
-        g_sklp = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    return g_sklp != 0;
-}
-
-// one row block (nb <= 16) only; otherwise as launch_gemm_skl
-hipError_t launch_gemm_sklp(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* part,
-                            hipStream_t st, const float* ssq, int nsl, float eps) {
-    const int S = skl_splits(K);
-    if (nb < 1 || nb > SK_ROWS || K % 64 || !S || N % 16 || (ssq && (nsl < 1 || nsl > SKL_MAX_SLICES)))
-        return hipErrorInvalidValue;
-    const int ks = K / 64 / S;
-    if ((size_t)(N / 16) * (K / 64) * (wscale ? 1024 : 2048) > 0x7fffffffu) return hipErrorInvalidValue;
-#define SKLP_X(Q, KSS) \
-    if ((wscale != nullptr) == Q && ks == KSS) return sklp_launch<Q, 4, KSS>(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
-    SKLP_X(0, 8) SKLP_X(0, 4) SKLP_X(1, 8) SKLP_X(1, 4)
-#undef SKLP_X
     return hipErrorInvalidValue;
 }
 

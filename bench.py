@@ -67,6 +67,12 @@ def parse():
                          "(vh_sched_*), fed -I 0.5 pieces of the 7 sample lengths cycled, staggered starts")
     ap.add_argument("--serve-seconds", type=float, default=120.0,
                     help="--stagger: audio each stream serves (clips back to back)")
+    ap.add_argument("--serve-end", choices=["common", "per-stream"], default="common",
+                    help="--stagger: 'common' -- clips start until one common end tick (2 x serve-seconds + "
+                         "streams - 1 ticks, so a stream serves serve-seconds on average), where every live "
+                         "clip is finished and drained: all streams live from the last start to the end; "
+                         "'per-stream' -- each stream until it has served serve-seconds (whole clips: the "
+                         "streams end apart, a long tail at low occupancy)")
     ap.add_argument("--serve-step-cap", type=int, default=8,
                     help="--stagger: greedy steps per stream and scheduler run (vh_sched_set_step_cap; 0 = "
                          "drain every run): a stream's bursts (prompt, flush padding) ride in full batched "
@@ -442,6 +448,11 @@ def main():
     # the stream's queue; profiled decode steps are launched eagerly (a graph cannot carry
     # dispatch events), which runs as fast as the graph replay
     st.set_profiling(True)
+    if os.environ.get("VOX_BENCH_MAPS"):
+        # the process's mappings, to put a crash's frame addresses to library + offset
+        # (the rocprofv3 SIGSEGV of DESIGN.md 6; tools/run/r4_d.sh)
+        with open("/proc/self/maps") as f, open(os.environ["VOX_BENCH_MAPS"], "w") as o:
+            o.write(f.read())
     runs = []
     d.barrier()
     st.sync()
@@ -790,7 +801,9 @@ def bench_serve(args, d, cfg, model, st0):
     cycled, 8 per GPU, staggered starts"): S concurrent streams on this GPU, owned by the C
     host's scheduler (vh_sched_*, include/vox_hip_host.h).  Stream i starts 1 s (two ticks)
     after stream i-1 and transcribes the 7 sample lengths in turn from clip i on, a fresh
-    vh_stream per clip, until it has served --serve-seconds of audio.  One tick = every live
+    vh_stream per clip, until a common end tick (--serve-end common: 2 x --serve-seconds + S - 1
+    ticks, where every unfinished clip is finished -- its audio so far -- and drained) or until it
+    has served --serve-seconds of whole clips (--serve-end per-stream).  One tick = every live
     stream feeds its next 0.5 s piece (vox_stream_feed: device mel + encoder chunk; -I 0.5),
     or flush + finish after its clip's last piece, then one vh_sched_run (prefills + batched
     greedy steps for every stream with adapter rows).  Ticks run back to back (as fast as the
@@ -805,7 +818,10 @@ def bench_serve(args, d, cfg, model, st0):
     rng = np.random.default_rng(5 + d.rank)
     clips = [synth_audio(sec, 500 + k) for k, sec in enumerate(SAMPLE_SECONDS)]
 
+    common = args.serve_end == "common"
+
     def run(serve_s):
+        end_tick = int(round(2 * serve_s)) + S - 1  # common end (ticks of 0.5 s)
         served = [0.0] * S
         cur = [None] * S        # [HostStream, clip index, next sample, finished]
         nxt = list(range(S))
@@ -821,7 +837,7 @@ def bench_serve(args, d, cfg, model, st0):
                     live = True
                     continue
                 if cur[k] is None:
-                    if served[k] >= serve_s:
+                    if (tick >= end_tick) if common else (served[k] >= serve_s):
                         continue
                     hs = vox_hip.HostStream(ctx, interval_s=0.5)
                     q.attach(hs)
@@ -832,7 +848,10 @@ def bench_serve(args, d, cfg, model, st0):
                 hs, c, pos, fin = cur[k]
                 if fin:                       # finished, rows still being decoded (step cap)
                     continue
-                if pos < len(clips[c]):
+                if common and tick >= end_tick:  # the common end: the clip so far, flushed
+                    hs.finish()
+                    cur[k][3] = True
+                elif pos < len(clips[c]):
                     hs.feed(clips[c][pos:pos + piece])
                     cur[k][2] = pos + piece
                 else:
@@ -847,7 +866,7 @@ def bench_serve(args, d, cfg, model, st0):
                     continue
                 tick_ids += len(cur[k][0].get())
                 if cur[k][3] and cur[k][0].pending() == 0:   # finished and drained: retire the clip
-                    served[k] += len(clips[cur[k][1]]) / 16000.0
+                    served[k] += min(cur[k][2], len(clips[cur[k][1]])) / 16000.0
                     q.detach(cur[k][0])
                     cur[k][0].close()
                     cur[k] = None
@@ -885,14 +904,19 @@ def bench_serve(args, d, cfg, model, st0):
         "dtype": "f32", "weights_dtype": "q8" if args.q8 else "bf16",
         "data": "synthetic (seeded random weights of the exact architecture; synthetic speech-band audio "
                 "of the 7 sample lengths)",
-        "config": {"workload": f"{S} streams per GPU, each serving {args.serve_seconds:.0f} s of audio as clips of "
-                               f"the 7 sample lengths {[round(x, 2) for x in SAMPLE_SECONDS]} s cycled (from clip i), "
-                               "fed in 0.5 s pieces (-I 0.5), starts staggered by 1 s; one vh_sched_run per tick"
+        "config": {"workload": f"{S} streams per GPU, "
+                               + (f"clips starting until a common end after {args.serve_seconds:.0f} s of audio per "
+                                  "stream on average (every clip then finished and drained)" if common else
+                                  f"each serving {args.serve_seconds:.0f} s of audio as whole clips")
+                               + f" of the 7 sample lengths {[round(x, 2) for x in SAMPLE_SECONDS]} s cycled (from "
+                               "clip i), fed in 0.5 s pieces (-I 0.5), starts staggered by 1 s; one vh_sched_run "
+                               "per tick"
                                + (f", at most {args.serve_step_cap} greedy steps per stream and run (a finished clip "
                                   "drains over the next ticks before the stream's next clip)"
                                   if args.serve_step_cap > 0 else ""),
                    "model": "Voxtral-Mini-4B-Realtime", "global_batch": S * d.world, "streams_per_gpu": S,
-                   "parallelism": f"replicas x{d.world}, {S} scheduled streams each"},
+                   "parallelism": f"replicas x{d.world}, {S} scheduled streams each",
+                   "serve_end": args.serve_end, "serve_step_cap": args.serve_step_cap},
         "value_is": "all ids generated / wall time of the serving loop (mel, encoder, prefill and decode included)",
         "tick_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
                             "p99": round(float(np.percentile(lat, 99)), 3), "max": round(float(lat.max()), 3)},

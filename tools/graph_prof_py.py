@@ -5,6 +5,7 @@ ends in SIGSEGV under rocprofv3 inside hipGraphLaunch.)  One mode per process, T
             eagerly through hipExtLaunchKernel with dispatch-recorded events, as bench.py does
   batch  -- the batched decode's slot-table step graphs
   full   -- plain at the full Voxtral-4B shapes (synthetic weights, 200 graph-replayed steps)
+  fullprof -- full with Stream.set_profiling(True) (bench.py's roofline pass)
 Run: rocprofv3 --kernel-trace --stats -d DIR -o x -- python3 tools/graph_prof_py.py MODE"""
 import os
 import sys
@@ -20,15 +21,21 @@ mode = sys.argv[1] if len(sys.argv) > 1 else "plain"
 # the process's mappings, so a crash's frame addresses can be put to library + offset and
 # symbolised afterwards (llvm-symbolizer --obj=LIB OFFSET on the same image)
 maps_out = os.environ.get("VOX_GP_MAPS")
-cfg = VOXTRAL_4B if mode == "full" else TINY
+cfg = VOXTRAL_4B if mode.startswith("full") else TINY
 w = synth_weights(cfg, seed=1)
 m = vox_hip.Model(cfg, w)
 del w
 rng = np.random.default_rng(0)
 mels = [rng.uniform(-0.5, 1.5, size=(900, cfg.mel_bins)).astype(np.float32) for _ in range(4)]
-if maps_out:
-    with open("/proc/self/maps") as f, open(maps_out, "w") as o:
-        o.write(f.read())
+
+
+def dump_maps():
+    if maps_out:
+        with open("/proc/self/maps") as f, open(maps_out, "w") as o:
+            o.write(f.read())
+
+
+dump_maps()
 if mode == "batch":
     ss = [vox_hip.Stream(m) for _ in mels]
     for s, mel in zip(ss, mels):
@@ -41,9 +48,10 @@ if mode == "batch":
 else:
     st = vox_hip.Stream(m)
     st.encode_mel(mels[0])
-    if mode == "prof":
+    if mode in ("prof", "fullprof"):
         st.set_profiling(True)
-    n = len(st.decode(max_steps=200, stop_at_eos=False)) if mode == "full" else len(st.decode(stop_at_eos=False))
+    dump_maps()  # every library the decode loads is mapped by now
+    n = len(st.decode(max_steps=200, stop_at_eos=False)) if mode.startswith("full") else len(st.decode(stop_at_eos=False))
     st.close()
 m.close()
 print(f"{mode}: {n} tokens, exited cleanly", flush=True)

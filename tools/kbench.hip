@@ -369,6 +369,70 @@ int main(int argc, char** argv) {
                 }
             }
         g_attn_bsplit = -1;
+        // phase stamps of the slot-table fused attention (16 streams, 128-key blocks of 8
+        // waves): per-wave s_memtime deltas, averaged; the merging block's merge apart
+        {
+            unsigned long long* stamps = nullptr;
+            const int nbs = 16, nblk = 2 * KVH * nbs, nwv = 8;
+            CK(hipMalloc(&stamps, (size_t)nblk * nwv * 10 * 8));
+            std::vector<BatchSlot> hsl(16);
+            for (int L : {64, 128, 190, 256}) {
+                memset(hsl.data(), 0, sizeof(BatchSlot) * 16);
+                for (int z = 0; z < 16; z++) {
+                    hsl[z].state = states + z * 4;
+                    hsl[z].Kc = reinterpret_cast<char*>(Ks[z * 2]);
+                    hsl[z].Vc = reinterpret_cast<char*>(Vs[z * 2]);
+                    hsl[z].live = 1;
+                    hsl[z].pos = L - 1;
+                }
+                CK(hipMemcpy(slots, hsl.data(), sizeof(BatchSlot) * 16, hipMemcpyHostToDevice));
+                double acc[8] = {0}, cyc = 0, rt = 0, gstart = 0, gend = 0, n = 0;
+                const int nrun = 20;
+                for (int r = 0; r < nrun; r++) {
+                    AttnPtrs p;
+                    memset(&p, 0, sizeof p);
+                    p.slots = slots;
+                    p.ring_off = (size_t)(r % 13) * rcap * DKV * 4;
+                    for (int z = 0; z < nbs; z++) p.part[z] = parts + (size_t)z * (H * 128 * (HD + 2) + 1024);
+                    p.out[0] = reinterpret_cast<float*>(stamps);
+                    CK(hipMemset(stamps, 0, (size_t)nblk * nwv * 10 * 8));
+                    AttnFuse f{slabs, S6, N, rope, xs};
+                    CK(launch_attn_batch_dbg(p, f, nbs, rcap, 8192, 0.088f, H, KVH, 1, st));
+                    CK(hipStreamSynchronize(st));
+                    std::vector<unsigned long long> h((size_t)nblk * nwv * 10);
+                    CK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
+                    unsigned long long g0 = ~0ull, g1 = 0, e1 = 0;
+                    for (int b = 0; b < nblk; b++) {
+                        const unsigned long long* t0 = &h[(size_t)b * nwv * 10];
+                        if (!t0[8]) continue;  // a block with no keys left before its stamps
+                        for (int w = 0; w < nwv; w++) {
+                            const unsigned long long* t = &h[((size_t)b * nwv + w) * 10];
+                            acc[0] += t[6] - t[0];
+                            acc[1] += t[7] - t[6];
+                            acc[2] += t[1] - t[7];
+                            acc[3] += t[2] - t[1];
+                            acc[4] += t[3] - t[2];
+                            acc[5] += t[4] - t[3];
+                            acc[6] += t[5] - t[4];
+                            cyc += t[5] - t[0];
+                            rt += t[9] - t[8];
+                            n += 1;
+                            g0 = std::min(g0, t[8]);
+                            g1 = std::max(g1, t[8]);
+                            e1 = std::max(e1, t[9]);
+                        }
+                    }
+                    gstart += g1 - g0;
+                    gend += e1 - g0;
+                }
+                printf("attn batch stamps nb=16 L=%d per-wave cycles: issue %.0f | loads land %.0f | barrier+new key %.0f | "
+                       "QK/sm/PV %.0f | sO+sync %.0f | factors %.0f | out / partial+ticket(+merge) %.0f ; total %.0f cyc = "
+                       "%.2f us; block starts spread %.2f us; first start to last end %.2f us\n",
+                       L, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, cyc / n,
+                       rt / n / 100.0, gstart / nrun / 100.0, gend / nrun / 100.0);
+            }
+            CK(hipFree(stamps));
+        }
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attn")) {

@@ -506,6 +506,7 @@ struct vox_hip_stream {
     int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
     int enc_async;           // vox_hip_stream_encode_mel returns without a stream sync
     float* xbatch;           // stacked encoder rows of a batched pass led by this stream
+    float *abatch, *abatch_out;  // its stacked adapter input rows (4 x enc_dim) / adapter rows
     float* essq;             // k_sklx row sums of squares per column slice [2][slices][16]
     uint16_t *gpa, *gpc;     // k_gemmf planes: norm / attention rows (K <= max(enc_dim, heads x hd)), gate rows
     int* gflags;             // k_gemmf partial-tile flags + the recompute counter (gemmf_flag_ints())
@@ -662,7 +663,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->gdrain); dfree(s->tokens);
-    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch);
+    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch); dfree(s->abatch); dfree(s->abatch_out);
     dfree(s->gpa); dfree(s->gpc); dfree(s->gflags);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
@@ -1294,6 +1295,66 @@ static int enc_suffix(vox_hip_stream_t* s, float* xin, int T1) {
     return added;
 }
 
+// enc_suffix for several streams at once, on lead's queue: stream b's new encoder rows are
+// X[off[b] ..+ T1[b]); its 4-row groups (residual rows first) are stacked into one adapter
+// input, the two adapter projections run once over all of them (the adapter weights read once
+// per pass instead of once per stream), and each stream's rows are copied to its adapter
+// buffer.  Per row the same products as enc_suffix (voxtral.c:868-934).
+static int enc_suffix_batch(vox_hip_stream_t* lead, const float* X, vox_hip_stream_t* const* ss, const int* T1,
+                            const int* off, int B, int* added) {
+    vox_hip_model_t* m = lead->m;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, D = c.dec_dim;
+    hipStream_t st = lead->st;
+    const size_t ain_rows = (size_t)ENC_SUB + 4 * VOX_MAX_BATCH;  // encoder rows (+ residuals)
+    if (!lead->abatch) {
+        CK(dalloc(&lead->abatch, ain_rows * ED));
+        CK(dalloc(&lead->abatch_out, ain_rows / 4 * D));
+    }
+    std::vector<int> aoff(B, 0), n4v(B, 0);
+    int NA = 0;  // stacked adapter rows
+    for (int b = 0; b < B; b++) {
+        added[b] = 0;
+        if (T1[b] <= 0) continue;
+        vox_hip_stream_t* s = ss[b];
+        s->enc_pos += T1[b];
+        const int R = s->enc_res_count, tot = R + T1[b], usable = (tot / 4) * 4, left = tot - usable;
+        const float* xb = X + (size_t)off[b] * ED;
+        if (usable > 0) {
+            if (stream_alloc_adapter(s, s->total_adapter + usable / 4)) return -1;
+            float* dst = lead->abatch + (size_t)NA * 4 * ED;
+            if (R) CK(hipMemcpyAsync(dst, s->enc_res, (size_t)R * ED * 4, hipMemcpyDeviceToDevice, st));
+            CK(hipMemcpyAsync(dst + (size_t)R * ED, xb, (size_t)(usable - R) * ED * 4, hipMemcpyDeviceToDevice, st));
+            if (left)
+                CK(hipMemcpyAsync(s->enc_res, xb + (size_t)(usable - R) * ED, (size_t)left * ED * 4,
+                                  hipMemcpyDeviceToDevice, st));
+            aoff[b] = NA;
+            n4v[b] = usable / 4;
+            NA += usable / 4;
+        } else {
+            CK(hipMemcpyAsync(s->enc_res + (size_t)R * ED, xb, (size_t)T1[b] * ED * 4, hipMemcpyDeviceToDevice, st));
+        }
+        s->enc_res_count = left;
+    }
+    if ((size_t)NA * 4 > ain_rows) return set_err("enc_suffix_batch: %d adapter rows", NA);
+    for (int r0 = 0; r0 < NA; r0 += ENC_SUB / 4) {
+        const int nr = std::min(ENC_SUB / 4, NA - r0);
+        CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, lead->abatch + (size_t)r0 * 4 * ED, 4 * ED, m->ad0,
+                       m->ad0_s, 4 * ED, nr, D, nullptr, lead->ad_mid, D, st, lead->gws, lead->gws_n));
+        CK(launch_gemm(EPI_STORE, 3, lead->ad_mid, D, m->ad1, m->ad1_s, D, nr, D, nullptr,
+                       lead->abatch_out + (size_t)r0 * D, D, st, lead->gws, lead->gws_n));
+    }
+    for (int b = 0; b < B; b++) {
+        if (!n4v[b]) continue;
+        vox_hip_stream_t* s = ss[b];
+        CK(hipMemcpyAsync(s->adapter + (size_t)s->total_adapter * D, lead->abatch_out + (size_t)aoff[b] * D,
+                          (size_t)n4v[b] * D * 4, hipMemcpyDeviceToDevice, st));
+        s->total_adapter += n4v[b];
+        added[b] = n4v[b];
+    }
+    return 0;
+}
+
 // The 32 encoder layers over the stacked new rows of several streams (row block b = rows
 // [off[b], off[b] + nr[b]) of X belongs to ss[b], at its logical positions from pos0[b]):
 // RMSNorm and the four projections run once over all rows (every weight byte read once for
@@ -1424,19 +1485,11 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
                 CK(hipMemcpyAsync(lead->xbatch + (size_t)off[b] * ED, xin[b], (size_t)T1[b] * ED * 4,
                                   hipMemcpyDeviceToDevice, lead->st));
         if (run_encoder_rows_batch(lead, lead->xbatch, N, ss, off.data(), T1.data(), pos0.data(), B)) return -1;
-        for (int b = 0; b < B; b++)
-            if (T1[b] > 0)
-                CK(hipMemcpyAsync(xin[b], lead->xbatch + (size_t)off[b] * ED, (size_t)T1[b] * ED * 4,
-                                  hipMemcpyDeviceToDevice, lead->st));
+        // downsample + adapter of every stream in one pass on the lead's queue; the members'
+        // queues then wait for it
+        if (enc_suffix_batch(lead, lead->xbatch, ss, T1.data(), off.data(), B, added)) return -1;
         CK(hipEventRecord(lead->sev, lead->st));
-        for (int b = 0; b < B; b++) {
-            added[b] = 0;
-            if (b) CK(hipStreamWaitEvent(ss[b]->st, lead->sev, 0));
-            if (T1[b] > 0) {
-                added[b] = enc_suffix(ss[b], xin[b], T1[b]);
-                if (added[b] < 0) return -1;
-            }
-        }
+        for (int b = 1; b < B; b++) CK(hipStreamWaitEvent(ss[b]->st, lead->sev, 0));
     }
     if (!all_async)
         for (int b = 0; b < B; b++) CK(hipStreamSynchronize(ss[b]->st));

@@ -152,6 +152,8 @@ hipError_t launch_rope_kv_rows(const float* qkv, int N, int qd, int kvd, int hd,
 hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, int cap, float* O, int H, int KVH,
                             int window, float scale, float* ws, size_t ws_elems, hipStream_t st);
 constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
+hipError_t launch_attn_batch_dbg(const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window, float scale, int H,
+                                 int KVH, int splits, hipStream_t st);
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st);
 hipError_t launch_embed_step(const float* adapter, const void* emb, const float* esc, const int* state,

@@ -1367,6 +1367,20 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
         ts[0] = __builtin_amdgcn_s_memtime();
         ts[8] = __builtin_amdgcn_s_memrealtime();
     }
+    // DBG 4: the wave's phase stamps to part[0] (single stream: [y][wave]) or, fused batched,
+    // to out[0] ([z][y][x][wave])
+    auto dbg_dump = [&]() {
+        if (DBG == 4) {
+            ts[5] = __builtin_amdgcn_s_memtime();
+            ts[9] = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) {
+                const size_t bi = P.slots ? (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * NWV
+                                          : (size_t)blockIdx.y * 16;
+                unsigned long long* d = reinterpret_cast<unsigned long long*>(FUSE ? P.out[0] : P.part[0]) + (bi + wave) * 10;
+                for (int i = 0; i < 10; i++) d[i] = ts[i];
+            }
+        }
+    };
     // the query does not depend on the step state: its load goes out first
     constexpr int QPT = (HPB * HD + NT - 1) / NT;
     float qreg[QPT];
@@ -1642,6 +1656,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             *reinterpret_cast<uint4*>(F.xs + Pn + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
             *reinterpret_cast<uint4*>(F.xs + 2 * Pn + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
         }
+        dbg_dump();
         return;
     }
     // partials (S > 1) go out write-through (sc1, like k_gemmf's partial tiles): the block
@@ -1665,7 +1680,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             }
         }
     }
-    if (S > 1 && DBG == 0) {
+    if (S > 1 && (DBG == 0 || DBG == 4)) {
         // the last of the S blocks of this kv head to finish merges the S partials of its
         // heads (the former k_attn_combine, one launch and its gap fewer per layer): stores
         // drained, one arrival count per (stream, kv head) just past the partials, reset by
@@ -1678,7 +1693,11 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
         int* cnt = reinterpret_cast<int*>(part + (size_t)H * maxs * (HD + 2)) + kvh;
         if (tid == 0) sLast = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
         __syncthreads();
-        if (!sLast) return;
+        if (!sLast) {
+            dbg_dump();
+            return;
+        }
+        if (DBG == 4) ts[4] = __builtin_amdgcn_s_memtime();  // the merging block: ts5 - ts4 = merge
         auto pnum = [&](int h, int k, int d) {
             return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                 Pr, (int)(((size_t)(h0 + h) * maxs + k) * (HD + 2) + d) * 4, 0, 16));
@@ -1767,16 +1786,10 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             }
         }
         if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dbg_dump();
         return;
     }
-    if (DBG == 4) {
-        ts[5] = __builtin_amdgcn_s_memtime();
-        ts[9] = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) {
-            unsigned long long* d = reinterpret_cast<unsigned long long*>(part) + (size_t)(blockIdx.y * 16 + wave) * 10;
-            for (int i = 0; i < 10; i++) d[i] = ts[i];
-        }
-    }
+    dbg_dump();
 }
 
 // ============================================================================
@@ -3613,6 +3626,17 @@ hipError_t launch_attn_batch_fused(int hd, const AttnPtrs& p, const AttnFuse& f,
                 : attn_batch_fused<float>(p, f, nb, cap, window, scale, H, KVH, splits, maxs, st);
 }
 // diagnostic variants for tools/kbench (not used by the engine)
+// the batched fused attention (128-key blocks, the bsplit grid) with per-wave phase stamps
+// to p.out[0] (10 u64 per wave: DBG 4 in k_attn_decode)
+hipError_t launch_attn_batch_dbg(const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window, float scale, int H,
+                                 int KVH, int splits, hipStream_t st) {
+    const int maxs = attn_maxch(window);
+    if (!p.out[0] || nb < 1 || nb > VOX_MAX_BATCH || H % KVH || H / KVH > 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_attn_decode<128, 4, 4, 1, ATT_LWAVES, float>), dim3(splits * (ATT_BK / ATT_LBK) * KVH, 1, nb),
+                       dim3(ATT_LWAVES * 64), 0, st, p, cap, 0, window, scale, H, KVH, maxs, f, 1);
+    LAUNCH_CHECK();
+    return hipSuccess;
+}
 hipError_t launch_attn_dbg(int dbg, const float* q, const float* Kc, const float* Vc, int cap,
                            const int* state, float* part, float* out, hipStream_t st) {
     dim3 grid(1, 32);

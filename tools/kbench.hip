@@ -433,6 +433,46 @@ int main(int argc, char** argv) {
             }
             CK(hipFree(stamps));
         }
+        // attention + wo at 16 streams: the attention's merging block + k_skl over the planes
+        // against partials only + k_skl_attn (the wo prologue merges them)
+        {
+            float* wpart = (float*)dmalloc((size_t)8 * 16 * D * 4, 0);
+            const int maxs = attn_maxch(8192);
+            std::vector<BatchSlot> hsl(16);
+            for (int L : {64, 128, 190, 256, 400, 512}) {
+                memset(hsl.data(), 0, sizeof(BatchSlot) * 16);
+                for (int z = 0; z < 16; z++) {
+                    hsl[z].state = states + z * 4;
+                    hsl[z].Kc = reinterpret_cast<char*>(Ks[z * 2]);
+                    hsl[z].Vc = reinterpret_cast<char*>(Vs[z * 2]);
+                    hsl[z].live = 1;
+                    hsl[z].pos = L - 1;
+                }
+                CK(hipMemcpy(slots, hsl.data(), sizeof(BatchSlot) * 16, hipMemcpyHostToDevice));
+                const int splits = L > 256 ? 2 : 1;
+                for (int wm : {0, 1}) {
+                    int l = 0;
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "attn+wo nb=16 L=%d %s", L, wm ? "wo merges" : "attn merges");
+                    add(nm, timeit([&] {
+                            AttnPtrs p;
+                            memset(&p, 0, sizeof p);
+                            p.slots = slots;
+                            p.ring_off = (size_t)(l % 13) * rcap * DKV * 4;
+                            for (int z = 0; z < 16; z++) p.part[z] = parts + (size_t)z * (H * 128 * (HD + 2) + 1024);
+                            AttnFuse f{slabs, S6, N, rope, xs};
+                            f.wom = wm;
+                            CK(launch_attn_batch_fused(HD, p, f, 16, rcap, 8192, 0.088f, H, KVH, splits, st, 0));
+                            if (wm)
+                                CK(launch_gemm_skl_attn(parts, (size_t)H * 128 * (HD + 2) + 1024, maxs, 2 * splits, DQ,
+                                                        wo[l % NL], nullptr, D, 16, wpart, st));
+                            else
+                                CK(launch_gemm_skl(xs, DQ, wo[l % NL], nullptr, D, 16, wpart, st));
+                            l++;
+                        }, iters, st), (double)16 * L * DKV * 2 * 4 + (double)D * DQ * 2);
+                }
+            }
+        }
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attn")) {

@@ -2449,6 +2449,15 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         const char* e = getenv("VOX_HIP_BATCH_SWX");
         swx = (e && atoi(e) == 0) ? 0 : 1;
     }
+    // contexts <= 512 keys (<= 4 key-range blocks of 128 per head): the wo projection merges
+    // the attention's partials (VOX_HIP_BATCH_WOM=0: the attention's own merging block)
+    static int wom_env = -1;
+    if (wom_env < 0) {
+        const char* e = getenv("VOX_HIP_BATCH_WOM");
+        wom_env = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    const int maxs = attn_maxch(c.dec_window);
+    const bool wom = wom_env && hd == 128 && 2 * splits <= ATT_WOM_MAX && 2 * splits <= maxs;
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         const DecFragD& F = m->dfrag[l];
@@ -2470,9 +2479,13 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         // launch; past 256 keys the last key-range block of a kv head merges the partials)
         AttnFuse af;
         af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
-        CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
         const bool fuse_wo = xw && swx && wox && !L.so && !L.s13;
-        if (fuse_wo) {
+        af.wom = wom && !fuse_wo;
+        CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
+        if (af.wom) {
+            // wo with the attention's key-range merge as its prologue (k_skl_attn)
+            CK(launch_gemm_skl_attn(b->apart, b->apart_n, maxs, 2 * splits, DQ, F.wo, L.so, DD, nb, b->part, st));
+        } else if (fuse_wo) {
             // wo with the residual folded in (k_sklx: the last block of each column slice sums
             // its slabs into x and writes the slice's x * ffn_norm * (1 + ada) planes and row
             // sums of squares for W1|W3)

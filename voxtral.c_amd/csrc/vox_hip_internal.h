@@ -92,6 +92,10 @@ struct AttnFuse {
     int S, N;              // slab count, row length (H*hd + 2*KVH*hd)
     const float* rope;     // [pos][hd] (cos, sin) table
     uint16_t* xs;          // [3][16][H*hd] fragment-major planes of the attention output
+    // wom: every 128-key block leaves its (numerator, max, sum) partial -- blocks past the
+    // context a neutral one (max -inf, sum 0) -- and the wo projection merges them as it
+    // builds its planes (launch_gemm_skl_attn); no arrival count, no merging block, no planes
+    int wom = 0;
 };
 
 constexpr int ARGB = 64;                // argmax partial blocks per row
@@ -201,6 +205,13 @@ int skl_splits(int K);
 constexpr int SKL_MAX_SLICES = 12;  // D <= 3072
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
                            float* part, hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f);
+// the batched wo projection (k_skl) with its planes built from the decode attention's
+// partials (AttnFuse.wom): stream j, head h, partial s at apart[j * apart_n + (h * maxs + s) *
+// (hd + 2)] = {numerator[hd], max, sum}, np partials per head merged (voxtral_kernels.c:
+// 554-560's softmax over the whole key range), hd = 128; K = heads * 128
+hipError_t launch_gemm_skl_attn(const float* apart, size_t apart_n, int maxs, int np, int K, const void* Wf,
+                                const float* wscale, int N, int nb, float* part, hipStream_t st);
+constexpr int ATT_WOM_MAX = 4;  // partials per head the wo prologue merges (contexts <= 512 keys)
 // x += the S slabs (+ bias); planes of x * w (* (1 + ada)); the row's sums of squares per
 // 256-column slice to ssq[row / 16][D / 256][row % 16] (the inverse RMS is applied by
 // launch_gemm_skl)

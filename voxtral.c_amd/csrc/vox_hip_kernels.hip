@@ -1390,7 +1390,15 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     const int L = min(lp + 1, window);
     const int first = lp - L + 1;
     const int S = (L + BK - 1) / BK;
-    if (sb >= S) return;  // uniform per block
+    if (sb >= S) {  // uniform per block
+        if (FUSE && F.wom && tid < nh) {
+            // past the context: a neutral partial per head (the wo prologue merges a fixed count)
+            const size_t po = ((size_t)(h0 + tid) * maxs + sb) * (HD + 2);
+            part[po + HD] = -INFINITY;
+            part[po + HD + 1] = 0.f;
+        }
+        return;
+    }
     const int k0 = first + sb * BK + wave * ATT_CH;  // >= 0
     const int kn = min(ATT_CH, lp + 1 - k0);  // may be <= 0 for trailing waves
     const int kk = lane & 15, dq = lane >> 4;
@@ -1627,7 +1635,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     }
     __syncthreads();
     if (DBG == 4) ts[4] = __builtin_amdgcn_s_memtime();
-    if (FUSE && S == 1) {
+    if (FUSE && S == 1 && !F.wom) {
         // output row zb straight into the wo input planes: 8 consecutive dims per thread
         const size_t Pn = (size_t)SK_ROWS * H * HD;
         for (int e = tid; e < nh * HD / 8; e += NT) {
@@ -1669,7 +1677,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
         for (int w = 0; w < NWV; w++) num = fmaf(sF[w][h], sO[w][h][d], num);
         const float den = sDen[h];
         const int hh = h0 + h;
-        if (S == 1) {
+        if (S == 1 && !(FUSE && F.wom)) {
             out[(size_t)hh * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
         } else {
             const int po = (int)(((size_t)hh * maxs + sb) * (HD + 2)) * 4;
@@ -1680,7 +1688,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             }
         }
     }
-    if (S > 1 && (DBG == 0 || DBG == 4)) {
+    if (S > 1 && !(FUSE && F.wom) && (DBG == 0 || DBG == 4)) {
         // the last of the S blocks of this kv head to finish merges the S partials of its
         // heads (the former k_attn_combine, one launch and its gap fewer per layer): stores
         // drained, one arrival count per (stream, kv head) just past the partials, reset by
@@ -2713,6 +2721,117 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
     }
 }
 
+// k_skl for the batched wo projection with the decode attention's merge as its prologue
+// (AttnFuse.wom): instead of loading planes, the block reads the NP key-range partials
+// {numerator[128], max, sum} of each (stream, head) its k range covers, merges them (factors
+// exp(m_s - M) in split order, the numerator over the summed denominator: the merging block's
+// arithmetic in k_attn_decode) and writes the three planes of the attention row into LDS --
+// one dependent load round as before, no merging block and no planes round trip through HBM.
+// A partial whose max is -inf (a block past the context) adds nothing.  Dead slots' rows read
+// stale partials; their results are never used (rows are independent columns of the MFMA).
+template <int WQ8, int NW, int KS, int NP>
+__global__ __launch_bounds__(NW * 64) void k_skl_attn(const float* __restrict__ apart, int apart_n, int maxs, int K,
+                                                      const uint8_t* __restrict__ W, const float* __restrict__ wscale,
+                                                      int N, int nb, float* __restrict__ part) {
+    __shared__ uint4 xb[KS * 6 * 64];  // [block][plane][half][lane]
+    constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
+    constexpr int NJ = KS * 2 / NW;  // merge jobs (row, 8 dims) per thread
+    static_assert(KS * 2 % NW == 0, "jobs split over the waves");
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int KB = K >> 6, S = KB / KS, X = N / (16 * NW);
+    const int u = blockIdx.x;
+    const int s = u / X, kb0 = s * KS;
+    const int g = (u % X) * NW + wave;
+    // job idx -> (block blk, half t, lane l): row j = l & 15, dims k .. k + 7 of head k >> 7
+    // a partial is 130 floats: 8-byte aligned numerators (float2 loads), not 16
+    float2 nv[NJ][NP][4];
+    float mv[NJ][NP], lv[NJ][NP];
+#pragma unroll
+    for (int i = 0; i < NJ; i++) {
+        const int idx = tid + i * NW * 64;
+        const int blk = idx >> 7, t = (idx >> 6) & 1, l = idx & 63;
+        const int j = min(l & 15, nb - 1);
+        const int k = (kb0 + blk) * 64 + t * 32 + (l >> 4) * 8;
+        const float* pb = apart + (size_t)j * apart_n + (size_t)(k >> 7) * maxs * 130;
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+#pragma unroll
+            for (int e = 0; e < 4; e++) nv[i][q][e] = *reinterpret_cast<const float2*>(pb + q * 130 + (k & 127) + 2 * e);
+            mv[i][q] = pb[q * 130 + 128];
+            lv[i][q] = pb[q * 130 + 129];
+        }
+    }
+    const __amdgpu_buffer_rsrc_t Wd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g * KB * FB, 0, KB * FB, 0x00020000);
+    u32x4 a[KS][NH];
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < NH; t++) a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(Wd, lane * 16 + t * 1024, (kb0 + kb) * FB, 2);
+#pragma unroll
+    for (int i = 0; i < NJ; i++) {
+        const int idx = tid + i * NW * 64;
+        const int blk = idx >> 7, t = (idx >> 6) & 1, l = idx & 63;
+        float M = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < NP; q++) M = fmaxf(M, mv[i][q]);
+        float den = 0.f, o[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) o[e] = 0.f;
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            const bool on = mv[i][q] > -INFINITY;
+            const float f = on ? expf(mv[i][q] - M) : 0.f;
+            den = on ? fmaf(f, lv[i][q], den) : den;
+            const float nn[8] = {nv[i][q][0].x, nv[i][q][0].y, nv[i][q][1].x, nv[i][q][1].y,
+                                 nv[i][q][2].x, nv[i][q][2].y, nv[i][q][3].x, nv[i][q][3].y};
+#pragma unroll
+            for (int e = 0; e < 8; e++) o[e] = on ? fmaf(f, nn[e], o[e]) : o[e];
+        }
+        const float inv = den > 0.f ? 1.0f / den : 0.f;
+        uint32_t hp[4], mp[4], lq[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+            uint16_t a0, b0, c0, a1, b1, c1;
+            split3(den > 0.f ? o[e] * inv : 0.f, a0, b0, c0);
+            split3(den > 0.f ? o[e + 1] * inv : 0.f, a1, b1, c1);
+            hp[e / 2] = a0 | ((uint32_t)a1 << 16);
+            mp[e / 2] = b0 | ((uint32_t)b1 << 16);
+            lq[e / 2] = c0 | ((uint32_t)c1 << 16);
+        }
+        xb[((blk * 3 + 0) * 2 + t) * 64 + l] = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+        xb[((blk * 3 + 1) * 2 + t) * 64 + l] = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+        xb[((blk * 3 + 2) * 2 + t) * 64 + l] = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+    }
+    __syncthreads();
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            bf16x8 af;
+            if (WQ8) {
+                const u32x4 q = a[kb][0];
+                af = t ? i8x8_bf16(q.z, q.w) : i8x8_bf16(q.x, q.y);
+            } else {
+                const u32x4 q = a[kb][t];
+                af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
+            }
+#pragma unroll
+            for (int p = 0; p < 3; p++)
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, xb[((kb * 3 + p) * 2 + t) * 64 + lane]),
+                                                             acc, 0, 0, 0);
+        }
+    const int j = lane & 15;
+    if (j < nb) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = g * 16 + (lane >> 4) * 4 + i;
+            part[((size_t)s * SK_ROWS + j) * N + row] = WQ8 ? acc[i] * wscale[row] : acc[i];
+        }
+    }
+}
+
 // Residual + the planes of an RMSNorm without its row reduction: x += the S slabs of the
 // previous projection (+ bias, summed in split order as k_resid_rmsnorm_fplanes), the row
 // written back, the planes of x * w (* (1 + ada)) -- the inverse RMS is applied by the next
@@ -3493,7 +3612,9 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-int attn_maxch(int window) { return (window + ATT_MIN_BK - 1) / ATT_MIN_BK; }
+// at least ATT_WOM_MAX: the batched step's wo-merge mode writes 2 x splits partials per head
+// even for windows shorter than two blocks
+int attn_maxch(int window) { return std::max(ATT_WOM_MAX, (window + ATT_MIN_BK - 1) / ATT_MIN_BK); }
 int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 int g_attn_lw = 0;  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
 int g_attn_kvfast = 1;  // long-context grid with the kv heads of a key range adjacent (tools/kbench: 0 = off)
@@ -3604,7 +3725,7 @@ static hipError_t attn_batch_fused(const AttnPtrs& p, const AttnFuse& f, int nb,
     // contexts <= 256 keys: one 1024-thread block per (stream, kv head) -- unless those blocks
     // cannot fill the chip (16 streams x 8 kv heads = 128 blocks on 256 CUs): then the 128-key
     // blocks of the long path (two per (stream, kv head), last arriver merges)
-    if (splits == 1 && (!g_attn_bsplit || nb * KVH >= 256)) {
+    if (splits == 1 && !f.wom && (!g_attn_bsplit || nb * KVH >= 256)) {
         hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_WAVES, KT>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, 0,
                            window, scale, H, KVH, maxs, f);
         LAUNCH_CHECK();
@@ -3846,6 +3967,36 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
     SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4)
     SKL_X(1, 4, 8) SKL_X(1, 8, 8) SKL_X(1, 4, 4) SKL_X(1, 8, 4)
 #undef SKL_X
+    return hipErrorInvalidValue;
+}
+
+template <int Q, int NW, int KS, int NP>
+static hipError_t skl_attn_launch(const float* apart, size_t apart_n, int maxs, int K, const void* W, const float* wscale,
+                                  int N, int nb, float* part, hipStream_t st) {
+    const int grid = (N / (16 * NW)) * (K / (64 * KS));
+    hipLaunchKernelGGL((k_skl_attn<Q, NW, KS, NP>), dim3(grid), dim3(NW * 64), 0, st, apart, (int)apart_n, maxs, K,
+                       static_cast<const uint8_t*>(W), wscale, N, nb, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_gemm_skl_attn(const float* apart, size_t apart_n, int maxs, int np, int K, const void* Wf,
+                                const float* wscale, int N, int nb, float* part, hipStream_t st) {
+    const int S = skl_splits(K);
+    // one row block; K = heads x 128 in whole 64-k blocks; the waves as launch_gemm_skl picks them
+    if (!apart || nb < 1 || nb > SK_ROWS || K % 128 || !S || apart_n > 0x7fffffff || maxs < np ||
+        (np != 2 && np != 4))
+        return hipErrorInvalidValue;
+    const int ks = K / 64 / S;
+    const int nb8 = (N / 128) * S;
+    int nw = g_skl_nw ? g_skl_nw : (N % 128 == 0 && nb8 >= (N <= 4096 ? 128 : 384) ? 8 : 4);
+    if (N % (16 * nw)) nw = 4;
+    if (N % (16 * nw)) return hipErrorInvalidValue;
+#define SKA_X(Q, NWW, KSS, NPP)                                                                          \
+    if ((wscale != nullptr) == Q && nw == NWW && ks == KSS && np == NPP)                                 \
+        return skl_attn_launch<Q, NWW, KSS, NPP>(apart, apart_n, maxs, K, Wf, wscale, N, nb, part, st);
+    SKA_X(0, 8, 8, 2) SKA_X(0, 8, 8, 4) SKA_X(0, 4, 8, 2) SKA_X(0, 4, 8, 4)
+    SKA_X(1, 8, 8, 2) SKA_X(1, 8, 8, 4) SKA_X(1, 4, 8, 2) SKA_X(1, 4, 8, 4)
+#undef SKA_X
     return hipErrorInvalidValue;
 }
 

@@ -2742,7 +2742,8 @@ __global__ __launch_bounds__(NW * 64) void k_skl_attn(const float* __restrict__ 
     const int u = blockIdx.x;
     const int s = u / X, kb0 = s * KS;
     const int g = (u % X) * NW + wave;
-    // job idx -> (block blk, half t, lane l): row j = l & 15, dims k .. k + 7 of head k >> 7
+    // job idx -> (block blk, half t, lane l): row j = l & 15, dims k .. k + 7 of head k >> 7,
+    // k = 64 blk + 16 (l >> 4) + 8 t (frag_off)
     // a partial is 130 floats: 8-byte aligned numerators (float2 loads), not 16
     float2 nv[NJ][NP][4];
     float mv[NJ][NP], lv[NJ][NP];
@@ -2751,7 +2752,7 @@ __global__ __launch_bounds__(NW * 64) void k_skl_attn(const float* __restrict__ 
         const int idx = tid + i * NW * 64;
         const int blk = idx >> 7, t = (idx >> 6) & 1, l = idx & 63;
         const int j = min(l & 15, nb - 1);
-        const int k = (kb0 + blk) * 64 + t * 32 + (l >> 4) * 8;
+        const int k = (kb0 + blk) * 64 + (l >> 4) * 16 + t * 8;  // frag_off's layout of a 64-k block
         const float* pb = apart + (size_t)j * apart_n + (size_t)(k >> 7) * maxs * 130;
 #pragma unroll
         for (int q = 0; q < NP; q++) {

@@ -2449,12 +2449,13 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         const char* e = getenv("VOX_HIP_BATCH_SWX");
         swx = (e && atoi(e) == 0) ? 0 : 1;
     }
-    // contexts <= 512 keys (<= 4 key-range blocks of 128 per head): the wo projection merges
-    // the attention's partials (VOX_HIP_BATCH_WOM=0: the attention's own merging block)
+    // VOX_HIP_BATCH_WOM=1, contexts <= 512 keys (<= 4 key-range blocks of 128 per head): the
+    // wo projection merges the attention's partials.  Opt-in: measured no faster than the
+    // attention's own merging block
     static int wom_env = -1;
     if (wom_env < 0) {
         const char* e = getenv("VOX_HIP_BATCH_WOM");
-        wom_env = (e && atoi(e) == 0) ? 0 : 1;
+        wom_env = (e && atoi(e) == 1) ? 1 : 0;
     }
     const int maxs = attn_maxch(c.dec_window);
     const bool wom = wom_env && hd == 128 && 2 * splits <= ATT_WOM_MAX && 2 * splits <= maxs;

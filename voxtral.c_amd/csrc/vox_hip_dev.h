@@ -38,6 +38,21 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+// v uniform within each row of 16 lanes: the 4 rows combined through scalar reads of lanes
+// 0 / 16 / 32 / 48 (no ds_bpermute round trip); (r0 + r1) + (r2 + r3), the order of the
+// xor-16-then-32 shuffle reduction, so the sums are the same bits
+__device__ __forceinline__ float rows4_sum(float v) {
+    const int iv = __float_as_int(v);
+    const float a = __int_as_float(__builtin_amdgcn_readlane(iv, 0)), b = __int_as_float(__builtin_amdgcn_readlane(iv, 16));
+    const float c = __int_as_float(__builtin_amdgcn_readlane(iv, 32)), d = __int_as_float(__builtin_amdgcn_readlane(iv, 48));
+    return (a + b) + (c + d);
+}
+__device__ __forceinline__ float rows4_max(float v) {
+    const int iv = __float_as_int(v);
+    const float a = __int_as_float(__builtin_amdgcn_readlane(iv, 0)), b = __int_as_float(__builtin_amdgcn_readlane(iv, 16));
+    const float c = __int_as_float(__builtin_amdgcn_readlane(iv, 32)), d = __int_as_float(__builtin_amdgcn_readlane(iv, 48));
+    return fmaxf(fmaxf(a, b), fmaxf(c, d));
+}
 __device__ __forceinline__ float row_sum16(float v) {
     v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
     v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]

@@ -1349,8 +1349,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     constexpr int DQ = HD / 4;   // dims per lane for Q.K
     constexpr int DPL = HD / 64; // dims per lane for P.V
     __shared__ __attribute__((aligned(16))) float sQ[HPB][HD];
-    __shared__ float sM[NWV][4], sL[NWV][4], sF[NWV][4];
-    __shared__ float sDen[4], sMax[4];
+    __shared__ float sM[NWV][4], sL[NWV][4];
     __shared__ __attribute__((aligned(16))) float sO[NWV][HPB][HD];
     __shared__ __attribute__((aligned(16))) float sKn[FUSE ? HD : 1], sVn[FUSE ? HD : 1];  // the new key's K / V
     const int hpk = H / KVH;
@@ -1539,15 +1538,13 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             const float sa = (r < kn) ? aa * scale : -INFINITY, sbv = (r + 8 < kn) ? ab * scale : -INFINITY;
             float mx = fmaxf(sa, sbv);
             mx = fmaxf(mx, dpp<0x140>(mx));
-            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            mx = rows4_max(mx);  // the 4 rows of 16 lanes: 4 readlanes, no LDS round trip
             m[h] = (kn > 0) ? mx : -1e30f;
             p[h] = (r < kn) ? expf(sa - mx) : 0.f;
             pb[h] = (r + 8 < kn) ? expf(sbv - mx) : 0.f;
             float t = p[h] + pb[h];
             t += dpp<0x140>(t);
-            t += __shfl_xor(t, 16, 64);
-            t += __shfl_xor(t, 32, 64);
+            t = rows4_sum(t);
             l[h] = t;
 #pragma unroll
             for (int e = 0; e < DPL; e++) o[h][e] = 0.f;
@@ -1614,33 +1611,32 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             for (int e = 0; e < DPL; e++) sO[wave][h][lane * DPL + e] = o[h][e];
     __syncthreads();
     if (DBG == 4) ts[3] = __builtin_amdgcn_s_memtime();
-    if (wave == 0) {
-        const int w = lane >> 2, h = lane & 3;  // 64 lanes = 16 wave slots x 4 head slots
-        if (h < HPB) {
-            float M = -1e30f;
+    // merge factors of head h, recomputed by every thread that needs them (no second barrier):
+    // f_w = exp(m_w - M), den = sum f_w l_w added as the xor-4/8/16/32 lane tree did
+    auto factors = [&](int h, float (&f)[NWV], float& den, float& M) {
+        M = -1e30f;
 #pragma unroll
-            for (int i = 0; i < NWV; i++) M = fmaxf(M, sM[i][h]);
-            const float f = w < NWV ? expf(sM[w][h] - M) : 0.f;
-            float den = w < NWV ? f * sL[w][h] : 0.f;
-            den += __shfl_xor(den, 4, 64);
-            den += __shfl_xor(den, 8, 64);
-            den += __shfl_xor(den, 16, 64);
-            den += __shfl_xor(den, 32, 64);
-            if (w < NWV) sF[w][h] = f;
-            if (w == 0) {
-                sDen[h] = den;
-                sMax[h] = M;
-            }
+        for (int i = 0; i < NWV; i++) M = fmaxf(M, sM[i][h]);
+        float v[NWV];
+#pragma unroll
+        for (int w = 0; w < NWV; w++) {
+            f[w] = expf(sM[w][h] - M);
+            v[w] = f[w] * sL[w][h];
         }
-    }
-    __syncthreads();
+#pragma unroll
+        for (int st = 1; st < NWV; st *= 2)
+#pragma unroll
+            for (int w = 0; w < NWV; w += 2 * st) v[w] = v[w] + v[w + st];
+        den = v[0];
+    };
     if (DBG == 4) ts[4] = __builtin_amdgcn_s_memtime();
     if (FUSE && S == 1 && !F.wom) {
         // output row zb straight into the wo input planes: 8 consecutive dims per thread
         const size_t Pn = (size_t)SK_ROWS * H * HD;
         for (int e = tid; e < nh * HD / 8; e += NT) {
             const int h = e / (HD / 8), d0 = (e % (HD / 8)) * 8;
-            const float den = sDen[h];
+            float fw[NWV], den, Mx;
+            factors(h, fw, den, Mx);
             uint32_t hp[4], mp[4], lq[4];
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
@@ -1649,7 +1645,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
                 for (int u = 0; u < 2; u++) {
                     float num = 0.f;
 #pragma unroll
-                    for (int w = 0; w < NWV; w++) num = fmaf(sF[w][h], sO[w][h][d0 + i + u], num);
+                    for (int w = 0; w < NWV; w++) num = fmaf(fw[w], sO[w][h][d0 + i + u], num);
                     v2[u] = den > 0.f ? num * (1.0f / den) : 0.f;
                 }
                 uint16_t a0, b0, c0, a1, b1, c1;
@@ -1672,10 +1668,11 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     const __amdgpu_buffer_rsrc_t Pr = __builtin_amdgcn_make_buffer_rsrc(part, 0, 0x7fffffff, 0x00020000);
     for (int e = tid; e < nh * HD; e += NT) {
         const int h = e / HD, d = e % HD;
+        float fw[NWV], den, Mx;
+        factors(h, fw, den, Mx);
         float num = 0.f;
 #pragma unroll
-        for (int w = 0; w < NWV; w++) num = fmaf(sF[w][h], sO[w][h][d], num);
-        const float den = sDen[h];
+        for (int w = 0; w < NWV; w++) num = fmaf(fw[w], sO[w][h][d], num);
         const int hh = h0 + h;
         if (S == 1 && !(FUSE && F.wom)) {
             out[(size_t)hh * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
@@ -1683,7 +1680,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             const int po = (int)(((size_t)hh * maxs + sb) * (HD + 2)) * 4;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(num), Pr, po + d * 4, 0, 16);
             if (d == 0) {
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sMax[h]), Pr, po + HD * 4, 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(Mx), Pr, po + HD * 4, 0, 16);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(den), Pr, po + (HD + 1) * 4, 0, 16);
             }
         }
@@ -1853,14 +1850,12 @@ __global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q
     const float sa = (r < kn) ? aa * scale : -INFINITY, sbv = (r + 8 < kn) ? ab * scale : -INFINITY;
     float mx = fmaxf(sa, sbv);
     mx = fmaxf(mx, dpp<0x140>(mx));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = rows4_max(mx);  // the 4 rows of 16 lanes: 4 readlanes, no LDS round trip
     const float m = (kn > 0) ? mx : -1e30f;
     const float p = (r < kn) ? expf(sa - mx) : 0.f, pb = (r + 8 < kn) ? expf(sbv - mx) : 0.f;
     float t = p + pb;
     t += dpp<0x140>(t);
-    t += __shfl_xor(t, 16, 64);
-    t += __shfl_xor(t, 32, 64);
+    t = rows4_sum(t);
     float o0 = 0.f, o1 = 0.f;
 #pragma unroll
     for (int k = 0; k < ATT_CH; k++) {

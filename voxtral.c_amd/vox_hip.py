@@ -20,7 +20,8 @@ from vox_weights import (VoxConfig, Weights, build_weights_struct, config_struct
                          weights_struct_class)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvoxtral_hip.so")
+# VOX_HIP_LIB: another build of the same library (developer A/B of two builds on one box)
+LIB_PATH = os.environ.get("VOX_HIP_LIB") or os.path.join(_HERE, "libvoxtral_hip.so")
 
 TOKEN_BOS, TOKEN_EOS, TOKEN_STREAMING_PAD = 1, 2, 32
 STREAM_FIRST_CHUNK_MIN_MEL = 312          # voxtral.c:405

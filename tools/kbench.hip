@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wide, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wide, g_gemmf_ng, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -205,6 +205,26 @@ int main(int argc, char** argv) {
             }
         g_gemv_maxb = 0;
         qs = nullptr;
+        return 0;
+    }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "sklks")) {
+        // batched decode projections at 16 rows: k_skl waves per block x 64-k blocks per split
+        uint16_t* xp = (uint16_t*)dmalloc((size_t)3 * 16 * 9216 * 2, 1);
+        float* part = (float*)dmalloc((size_t)36 * 16 * 18432 * 4, 0);
+        struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
+        const S shapes[] = {S{"qkv 6144x3072", DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
+                            S{"wo  3072x4096", D, DQ, wo.data(), (double)D * DQ * 2},
+                            S{"w13 18432x3072", 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
+                            S{"w2  3072x9216", D, DH, w2.data(), (double)D * DH * 2}};
+        for (const S& g : shapes)
+            for (int nw : {4, 8})
+                for (int ks : {4, 6, 8, 12, 16}) {
+                    if ((g.K / 64) % ks || (ks * 6) % nw || g.N % (16 * nw)) continue;
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "skl %s nw%d ks%d (S %d, %d blocks)", g.n, nw, ks, g.K / 64 / ks,
+                             g.N / (16 * nw) * (g.K / 64 / ks));
+                    add(nm, timeit([&] { CK(launch_gemm_skl_cfg(nw, ks, xp, g.K, g.W[layer++ % NL], g.N, 16, part, st)); }, iters, st), g.bytes);
+                }
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "skb")) {
@@ -583,7 +603,7 @@ int main(int argc, char** argv) {
     }
     {
         // k_gemmf (stream-K, planes x fragment-major weights) at the encoder's shapes
-        const size_t wsn = gemmf_ws_floats(gemmf_grid());
+        const size_t wsn = 2 * gemmf_ws_floats(gemmf_grid());  // the NG4 RB8 tiles are twice the default
         float* gws = (float*)dmalloc(wsn * 4, 0);
         int* gfl = (int*)dmalloc(4096 * 4, 0);
         uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 5120 * 2, 1);
@@ -594,19 +614,22 @@ int main(int argc, char** argv) {
         for (int M : {70, 677, 1024})
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
                         G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
-                for (int v = 0; v < 5; v++) {
+                for (int v = 0; v < 7; v++) {
                     // np2 with the launcher's tile choice, np2 RB8, np2 RB4, np3 (RB4), np2 wide
-                    // (64 x 64 per wave, 4 waves)
+                    // (64 x 64 per wave, 4 waves), np2 NG4 RB4 (32 x 64 per wave, 8 waves, 64 x 256
+                    // tiles), np2 NG4 RB8 (64 x 64 per wave, 8 waves, 128 x 256 tiles)
+                    if (v >= 4 && g.N % 256) continue;
                     const int np = v == 3 ? 3 : 2;
-                    g_gemmf_rb = v == 1 ? 8 : v == 2 ? 4 : 0;
+                    g_gemmf_rb = v == 1 || v == 6 ? 8 : v == 2 || v == 5 ? 4 : 0;
                     g_gemmf_wide = v == 4 ? 1 : 0;
+                    g_gemmf_ng = v >= 5 ? 4 : 0;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
                     printf("gemmf %-4s M=%4d %dx%d np%d rb%d%s minu%-2d %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
-                           g.K, np, g_gemmf_rb, g_gemmf_wide ? " wide" : "", g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                           g.K, np, g_gemmf_rb, g_gemmf_wide ? " wide" : g_gemmf_ng == 4 ? " ng4" : "", g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
-                g_gemmf_rb = g_gemmf_minu = g_gemmf_wide = 0;
+                g_gemmf_rb = g_gemmf_minu = g_gemmf_wide = g_gemmf_ng = 0;
             }
     }
     if (only_gemmf) return 0;

@@ -211,6 +211,8 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
 // 554-560's softmax over the whole key range), hd = 128; K = heads * 128
 hipError_t launch_gemm_skl_attn(const float* apart, size_t apart_n, int maxs, int np, int K, const void* Wf,
                                 const float* wscale, int N, int nb, float* part, hipStream_t st);
+hipError_t launch_gemm_skl_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, int N, int nb, float* part,
+                               hipStream_t st);  // tools/kbench sweep
 constexpr int ATT_WOM_MAX = 4;  // partials per head the wo prologue merges (contexts <= 512 keys)
 // x += the S slabs (+ bias); planes of x * w (* (1 + ada)); the row's sums of squares per
 // 256-column slice to ssq[row / 16][D / 256][row % 16] (the inverse RMS is applied by

@@ -3996,6 +3996,17 @@ hipError_t launch_gemm_skl_attn(const float* apart, size_t apart_n, int maxs, in
     return hipErrorInvalidValue;
 }
 
+// tools/kbench: k_skl (bf16, 16 rows) at a given waves-per-block / 64-k blocks per split
+hipError_t launch_gemm_skl_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, int N, int nb, float* part,
+                               hipStream_t st) {
+    if (nb < 1 || nb > SK_ROWS || K % 64 || (K / 64) % ks || N % (16 * nw) || (ks * 6) % nw) return hipErrorInvalidValue;
+#define SKC_X(NWW, KSS) \
+    if (nw == NWW && ks == KSS) return skl_launch<0, NWW, KSS>(xs, K, Wf, nullptr, N, nb, part, st, nullptr, 0, 0.f);
+    SKC_X(4, 4) SKC_X(8, 4) SKC_X(4, 6) SKC_X(4, 8) SKC_X(8, 8) SKC_X(4, 12) SKC_X(8, 12) SKC_X(4, 16) SKC_X(8, 16)
+#undef SKC_X
+    return hipErrorInvalidValue;
+}
+
 static int sklx_nw(int N, int K) {
     // waves per block as launch_gemm_skl picks them
     const int S = skl_splits(K);

@@ -220,6 +220,12 @@ vox_hip_batch_t *vox_hip_batch_create(vox_hip_model_t *m, int max_streams);
 void vox_hip_batch_free(vox_hip_batch_t *b);
 int vox_hip_batch_decode(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, int max_steps,
                          int stop_at_eos, int *tokens_out, int *counts_out);
+/* The same with stream i reading only its first rows[i] adapter rows (<= its count), which the
+ * caller guarantees are complete; the streams' own queues are not waited for, so an encoder
+ * pass enqueued on them after those rows (async encode, vox_hip_stream_encode_mel_batch) runs
+ * beside the batched steps (the per-GPU scheduler's overlap, vh_sched_run). */
+int vox_hip_batch_decode_rows(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, const int *rows,
+                              int max_steps, int stop_at_eos, int *tokens_out, int *counts_out);
 /* Logits [vocab] of the last batched step, for a stream that step advanced (the logits the
  * reference's vox_decoder_forward returns, voxtral_decoder.c:762-779; for tests and --alt
  * style callers).  Returns 0, or <0 if s was not in that step. */

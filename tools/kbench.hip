@@ -614,13 +614,13 @@ int main(int argc, char** argv) {
         for (int M : {70, 677, 1024})
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
                         G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
-                for (int v = 0; v < 7; v++) {
+                for (int v = 0; v < 6; v++) {
                     // np2 with the launcher's tile choice, np2 RB8, np2 RB4, np3 (RB4), np2 wide
                     // (64 x 64 per wave, 4 waves), np2 NG4 RB4 (32 x 64 per wave, 8 waves, 64 x 256
-                    // tiles), np2 NG4 RB8 (64 x 64 per wave, 8 waves, 128 x 256 tiles)
+                    // tiles; NG4 RB8 would need 192 KB of LDS ring)
                     if (v >= 4 && g.N % 256) continue;
                     const int np = v == 3 ? 3 : 2;
-                    g_gemmf_rb = v == 1 || v == 6 ? 8 : v == 2 || v == 5 ? 4 : 0;
+                    g_gemmf_rb = v == 1 ? 8 : v == 2 || v == 5 ? 4 : 0;
                     g_gemmf_wide = v == 4 ? 1 : 0;
                     g_gemmf_ng = v >= 5 ? 4 : 0;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,

@@ -2297,6 +2297,9 @@ struct vox_hip_batch {
     int llive[VOX_MAX_BATCH];
     int lnb;
     long long n_calls, n_replays, n_rows, n_captures, n_prefill_passes, n_prefilled;
+    // split-K workspace of the stacked prefills (not the lead stream's: with an encoder pass
+    // running beside the batched steps, that stream's queue may be using its own)
+    float* pgws;
 };
 
 static int* slot_toklog(BatchSlot* slots) { return reinterpret_cast<int*>(slots + VOX_MAX_BATCH); }
@@ -2347,7 +2350,7 @@ extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     if (b->st) hipStreamSynchronize(b->st);
     dfree(b->x); dfree(b->part); dfree(b->ssq); dfree(b->ticket); dfree(b->q); dfree(b->att);
     dfree(b->logits); dfree(b->pval); dfree(b->pidx); dfree(b->palt); dfree(b->apart);
-    dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h);
+    dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h); dfree(b->pgws);
     if (b->slots) hipFree(b->slots);
     if (b->hslots) hipHostFree(b->hslots);
     batch_drop_graphs(b);
@@ -2373,7 +2376,13 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     const size_t S = VOX_MAX_BATCH;  // rows of the slot-indexed buffers (graphs of any bucket)
     auto fail = [&]() -> vox_hip_batch_t* { vox_hip_batch_free(b); return nullptr; };
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
-    TRYH(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
+    {
+        // the batched steps' queue at the highest priority: beside a cross-stream encoder pass
+        // (vox_hip_batch_decode_rows) the latency-bound step kernels go first
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+        TRYH(hipStreamCreateWithPriority(&b->st, hipStreamNonBlocking, hi));
+    }
     TRYH(dalloc(&b->x, S * D));
     {
         const size_t DQ = (size_t)c.dec_heads * c.dec_head_dim, DH = c.dec_hidden;
@@ -2590,11 +2599,13 @@ static void stream_steps_done(vox_hip_stream_t* s, int produced, int last_token)
 // RoPE + K/V append and the causal attention per stream against its own ring (the batched
 // encoder's row-offset kernels), scratch of ss[0].  One stream, or 16-bit rings, take the
 // single-stream prefill.  The member queues must be idle.
-static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B) {
+// bounded (vox_hip_batch_decode_rows): a single new stream takes the stacked path too, on the
+// batch queue -- its own queue may be busy with an encoder pass the steps overlap
+static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B, bool bounded) {
     vox_hip_model_t* m = b->m;
     const vox_hip_config_t& c = m->c;
     const int np = 32 + m->delay_tokens;
-    if (B == 1 || ss[0]->kv16 || B * np > ENC_SUB) {
+    if ((B == 1 && !bounded) || ss[0]->kv16 || B * np > ENC_SUB) {
         for (int i = 0; i < B; i++) {
             if (stream_prefill(ss[i])) return -1;
             CK(hipStreamSynchronize(ss[i]->st));
@@ -2611,6 +2622,9 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B)
     hipStream_t st = b->st;
     if (stream_alloc_dec_rows(lead, N)) return -1;
     if (ensure_rope(lead, np + 2)) return -1;
+    if (!b->pgws) CK(dalloc(&b->pgws, GEMM_WS_ELEMS));
+    float* gws = b->pgws;
+    const size_t gws_n = GEMM_WS_ELEMS;
     float* X = lead->xd;
     for (int i = 0; i < B; i++)
         CK(launch_embed_rows(ss[i]->adapter, m->tok_emb, m->tok_emb_s, 0, np, TOKEN_BOS, TOKEN_STREAMING_PAD, DD,
@@ -2631,15 +2645,14 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B)
         }
         CK(launch_rmsnorm_rows(X, DD, lead->xnd, DD, L.attn_norm, nullptr, N, DD, c.dec_eps, st));
         CK(launch_gemm(EPI_STORE, 3, lead->xnd, DD, L.wqkv, L.sqkv, DD, N, DQ + 2 * DKV, nullptr, lead->qkvd, DQ + 2 * DKV,
-                       st, lead->gws, lead->gws_n));
+                       st, gws, gws_n));
         CK(launch_rope_kv_rows(lead->qkvd, N, DQ, DKV, hd, m->rope_dec, er, lead->qd_, cap, st));
-        CK(launch_attn_rows(hd, lead->qd_, er, N, cap, lead->attd, H, KVH, c.dec_window, scale, lead->gws, lead->gws_n,
+        CK(launch_attn_rows(hd, lead->qd_, er, N, cap, lead->attd, H, KVH, c.dec_window, scale, gws, gws_n,
                             st));
-        CK(launch_gemm(EPI_RESID, 3, lead->attd, DQ, L.wo, L.so, DQ, N, DD, nullptr, X, DD, st, lead->gws, lead->gws_n));
+        CK(launch_gemm(EPI_RESID, 3, lead->attd, DQ, L.wo, L.so, DQ, N, DD, nullptr, X, DD, st, gws, gws_n));
         CK(launch_rmsnorm_rows(X, DD, lead->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, N, DD, c.dec_eps, st));
-        CK(launch_gemm(EPI_SWIGLU, 3, lead->xnd, DD, L.w13, L.s13, DD, N, 2 * DH, nullptr, lead->gated, DH, st, lead->gws,
-                       lead->gws_n));
-        CK(launch_gemm(EPI_RESID, 3, lead->gated, DH, L.w2, L.s2, DH, N, DD, nullptr, X, DD, st, lead->gws, lead->gws_n));
+        CK(launch_gemm(EPI_SWIGLU, 3, lead->xnd, DD, L.w13, L.s13, DD, N, 2 * DH, nullptr, lead->gated, DH, st, gws, gws_n));
+        CK(launch_gemm(EPI_RESID, 3, lead->gated, DH, L.w2, L.s2, DH, N, DD, nullptr, X, DD, st, gws, gws_n));
     }
     for (int i = 0; i < B; i++)
         if (stream_prefilled(ss[i], st)) return -1;
@@ -2648,8 +2661,12 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B)
     return 0;
 }
 
-extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, int max_steps,
-                                    int stop_at_eos, int* tokens_out, int* counts_out) {
+// rows == null: every stream's adapter rows, its queue synchronised first (an async encoder
+// pass finishes before the steps read its rows); rows[i]: only stream i's first rows[i] rows,
+// which the caller guarantees complete, and the members' queues are left running (an encoder
+// pass enqueued on them after those rows overlaps the steps)
+static int batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, const int* rows, int max_steps,
+                        int stop_at_eos, int* tokens_out, int* counts_out) {
     if (!b || n < 1 || n > b->cap || max_steps < 0) return set_err("bad batch arguments");
     vox_hip_model_t* m = b->m;
     const vox_hip_config_t& c = m->c;
@@ -2666,8 +2683,18 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
     b->n_calls++;
     b->lnb = 0;
     // every member's queue is idle before the batch queue touches its buffers (adapter rows
-    // of an async encoder pass, a realloc'ed adapter buffer)
-    for (int i = 0; i < n; i++) CK(hipStreamSynchronize(streams[i]->st));
+    // of an async encoder pass, a realloc'ed adapter buffer) -- unless the caller bounded the
+    // rows each stream may read
+    int avail[VOX_MAX_BATCH];
+    for (int i = 0; i < n; i++) {
+        if (rows) {
+            if (rows[i] < 0 || rows[i] > streams[i]->total_adapter) return set_err("batch rows[%d] out of range", i);
+            avail[i] = rows[i];
+        } else {
+            CK(hipStreamSynchronize(streams[i]->st));
+            avail[i] = streams[i]->total_adapter;
+        }
+    }
     if (max_steps == 0) return 0;
     // 1. streams whose prompt is complete and whose decoder has not started: their prefills
     //    in one stacked pass; they take their first token in the batched steps below
@@ -2676,9 +2703,9 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
         int np = 0;
         for (int i = 0; i < n; i++) {
             vox_hip_stream_t* s = streams[i];
-            if (!s->started && !s->eos_seen && s->total_adapter >= prompt_len) pre[np++] = s;
+            if (!s->started && !s->eos_seen && avail[i] >= prompt_len) pre[np++] = s;
         }
-        if (np && batch_prefill(b, pre, np)) return -1;
+        if (np && batch_prefill(b, pre, np, rows != nullptr)) return -1;
     }
     // 2. the slot table: slot i = streams[i], a step budget per slot, empty slots up to the
     //    bucket stopped
@@ -2692,14 +2719,14 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
         if (i >= n) continue;
         vox_hip_stream_t* s = streams[i];
         int lim = 0;
-        if (s->started && !s->eos_seen) lim = std::max(0, std::min(s->total_adapter - s->h_state[1], max_steps));
+        if (s->started && !s->eos_seen) lim = std::max(0, std::min(avail[i] - s->h_state[1], max_steps));
         hs[i].state = s->state;
         hs[i].tokens = s->tokens;
         hs[i].adapter = s->adapter;
         hs[i].Kc = reinterpret_cast<char*>(s->dk);
         hs[i].Vc = reinterpret_cast<char*>(s->dv);
         hs[i].alts = s->n_alt > 1 ? s->alts : nullptr;
-        hs[i].adapter_rows = s->total_adapter;
+        hs[i].adapter_rows = avail[i];
         hs[i].left = lim;
         hs[i].stop_tok = stop_at_eos ? TOKEN_EOS : -1;
         hs[i].live = lim > 0;
@@ -2756,6 +2783,17 @@ extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** strea
     b->lnb = n;
     b->n_rows += total;
     return total;
+}
+
+extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, int max_steps,
+                                    int stop_at_eos, int* tokens_out, int* counts_out) {
+    return batch_decode(b, streams, n, nullptr, max_steps, stop_at_eos, tokens_out, counts_out);
+}
+
+extern "C" int vox_hip_batch_decode_rows(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, const int* rows,
+                                         int max_steps, int stop_at_eos, int* tokens_out, int* counts_out) {
+    if (!rows) return set_err("batch_decode_rows: null rows");
+    return batch_decode(b, streams, n, rows, max_steps, stop_at_eos, tokens_out, counts_out);
 }
 
 extern "C" int vox_hip_batch_read_logits(vox_hip_batch_t* b, vox_hip_stream_t* s, float* out) {

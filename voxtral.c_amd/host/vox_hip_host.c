@@ -1043,10 +1043,41 @@ void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {
     }
 }
 
+static int sched_overlap(void) {
+    /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start */
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("VOX_HIP_SCHED_OVERLAP");
+        v = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return v;
+}
+
 int vh_sched_run(vh_sched_t *q) {
     const double t_run = now_ms();
     int total = 0;
     int eos[VH_SCHED_MAX] = {0}, ran[VH_SCHED_MAX] = {0};
+    /* Overlap: the batched steps decode the adapter rows that exist when the run starts while
+     * this run's encoder pass (enqueued first, on the streams' queues) computes the next ones;
+     * those are decoded by the next run.  Greedy ids do not depend on when a row is decoded, so
+     * a stream's ids are unchanged.  Live-mode streams keep the sequential order: their restart
+     * checks belong after a drain of every row of the chunk (voxtral.c:1189-1239). */
+    int overlap = sched_overlap() && sched_batch_encode();
+    for (int i = 0; i < q->n; i++) overlap = overlap && !q->s[i]->continuous;
+    int rows[VH_SCHED_MAX] = {0};
+    if (overlap)
+        for (int i = 0; i < q->n; i++) {
+            vh_stream_t *s = q->s[i];
+            /* every row counted here is complete: nothing is left on the stream's queue */
+            if (vox_hip_stream_sync(s->st)) return fail("sync: %s", vox_hip_last_error());
+            rows[i] = vox_hip_stream_adapter_tokens(s->st);
+            int st6[6];
+            vox_hip_stream_state(s->st, st6);
+            ran[i] = st6[3] || rows[i] >= 1 + 32 + s->ctx->delay_tokens;
+        }
+    vox_hip_stream_t *enc_q[VH_SCHED_MAX];
+    int enc_n = 0;
+    double enc_t0 = 0.0;
     /* 0. every attached stream's deferred chunk through one batched encoder pass (the layers'
      *    weights read once for all of them) */
     {
@@ -1066,19 +1097,27 @@ int vh_sched_run(vh_sched_t *q) {
             const double t0 = now_ms();
             if (vox_hip_stream_encode_mel_batch(hs, mp, nf, nb, 1, added) < 0)
                 return fail("batched encoder: %s", vox_hip_last_error());
-            /* the pass completes here (the batched decode would wait for it anyway), so its
-             * time is the encoder's, not the decoder's */
-            for (int k = 0; k < nb; k++)
-                if (vox_hip_stream_sync(hs[k])) return fail("encoder: %s", vox_hip_last_error());
-            const double dt = now_ms() - t0;
-            q->stats.enc_ms += dt;
+            if (!overlap) {
+                /* the pass completes here (the batched decode would wait for it anyway), so its
+                 * time is the encoder's, not the decoder's */
+                for (int k = 0; k < nb; k++)
+                    if (vox_hip_stream_sync(hs[k])) return fail("encoder: %s", vox_hip_last_error());
+                const double dt = now_ms() - t0;
+                q->stats.enc_ms += dt;
+                for (int k = 0; k < nb; k++) q->s[idx[k]]->enc_ms += dt / nb;
+            } else {
+                /* still running: waited for after the steps (step 4) */
+                for (int k = 0; k < nb; k++) enc_q[k] = hs[k];
+                enc_n = nb;
+                enc_t0 = t0;
+            }
             q->stats.enc_batches++;
             for (int k = 0; k < nb; k++) {
                 vh_stream_t *s = q->s[idx[k]];
-                s->enc_ms += dt / nb;
                 s->pend_n = 0;
                 s->chunks++;
-                if (vox_hip_mel_discard_before(s->mel, s->mel_cursor)) return -1;
+                /* the mel frames the pass reads stay: discarded after it completes */
+                if (!overlap && vox_hip_mel_discard_before(s->mel, s->mel_cursor)) return -1;
             }
         }
     }
@@ -1088,10 +1127,14 @@ int vh_sched_run(vh_sched_t *q) {
      *      stop on the device when their rows run out or at EOS, streams with --alt keep their
      *      candidates (vox_hip_batch_decode); one call per round, another only when a stream
      *      hit the per-call step cap */
-    for (int i = 0; i < q->n; i++) ran[i] = decoder_ready(q->s[i]);
+    if (!overlap)
+        for (int i = 0; i < q->n; i++) {
+            ran[i] = decoder_ready(q->s[i]);
+            rows[i] = vox_hip_stream_adapter_tokens(q->s[i]->st);
+        }
     for (int iter = 0;; iter++) {
         vox_hip_stream_t *hs[VH_SCHED_MAX];
-        int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], gen0[VH_SCHED_MAX], nb = 0;
+        int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], gen0[VH_SCHED_MAX], brows[VH_SCHED_MAX], nb = 0;
         for (int i = 0; i < q->n; i++) {
             vh_stream_t *s = q->s[i];
             if (!ran[i] || eos[i]) continue;
@@ -1101,8 +1144,9 @@ int vh_sched_run(vh_sched_t *q) {
             int st6[6];
             vox_hip_stream_state(s->st, st6);
             if (st6[4]) continue;
-            if (st6[3] && vox_hip_stream_adapter_tokens(s->st) - st6[1] <= 0) continue;
+            if (st6[3] && rows[i] - st6[1] <= 0) continue;
             gen0[nb] = st6[5];
+            brows[nb] = rows[i];
             hs[nb] = s->st;
             idx[nb++] = i;
         }
@@ -1113,7 +1157,8 @@ int vh_sched_run(vh_sched_t *q) {
         }
         const double t0 = now_ms();
         const int cap = q->step_cap > 0 && q->step_cap < VH_SCHED_STEPS ? q->step_cap : VH_SCHED_STEPS;
-        const int r = vox_hip_batch_decode(q->batch, hs, nb, cap, 1, q->tok, counts);
+        const int r = overlap ? vox_hip_batch_decode_rows(q->batch, hs, nb, brows, cap, 1, q->tok, counts)
+                              : vox_hip_batch_decode(q->batch, hs, nb, cap, 1, q->tok, counts);
         if (r < 0) return fail("batched decoder: %s", vox_hip_last_error());
         const double dt = now_ms() - t0;
         q->stats.batch_calls++;
@@ -1139,6 +1184,15 @@ int vh_sched_run(vh_sched_t *q) {
         q->stats.tokens += r;
         /* with a step cap, a scheduled stream's rows beyond it wait for the next run */
         if (r == 0 || !more) break;
+    }
+    /* 4 (overlap). the encoder pass that ran beside the steps completes; its frames go */
+    if (enc_n) {
+        for (int k = 0; k < enc_n; k++)
+            if (vox_hip_stream_sync(enc_q[k])) return fail("encoder: %s", vox_hip_last_error());
+        q->stats.enc_ms += now_ms() - enc_t0;
+        for (int i = 0; i < q->n; i++)
+            for (int k = 0; k < enc_n; k++)
+                if (q->s[i]->st == enc_q[k] && vox_hip_mel_discard_before(q->s[i]->mel, q->s[i]->mel_cursor)) return -1;
     }
     /* 3. per-stream live-mode restarts (voxtral.c:1189-1239) */
     for (int i = 0; i < q->n; i++)

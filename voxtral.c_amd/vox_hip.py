@@ -42,7 +42,8 @@ EXPORTS = [
     "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
-    "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode", "vox_hip_batch_read_logits",
+    "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode", "vox_hip_batch_decode_rows",
+    "vox_hip_batch_read_logits",
     "vox_hip_batch_stats",
     "vox_hip_stream_state", "vox_hip_stream_set_alt", "vox_hip_stream_read_alts", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
     "vox_hip_fused_ffn_bf16", "vox_hip_encoder_attention", "vox_hip_encoder_full_step",
@@ -86,6 +87,7 @@ def lib():
         "vox_hip_stream_state": (I, [P, ip]),
         "vox_hip_batch_create": (P, [P, I]), "vox_hip_batch_free": (None, [P]),
         "vox_hip_batch_decode": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, I, I, ip, ip]),
+        "vox_hip_batch_decode_rows": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, ip, I, I, ip, ip]),
         "vox_hip_batch_read_logits": (I, [P, P, fp]),
         "vox_hip_batch_stats": (I, [P, ctypes.POINTER(ctypes.c_longlong)]),
         "vox_hip_stream_set_alt": (I, [P, I, F]),
@@ -527,15 +529,22 @@ class Batch:
         if not self.h:
             _err("vox_hip_batch_create")
 
-    def decode(self, streams, max_steps: int, stop_at_eos: bool = True):
-        """Returns one int32 token array per stream."""
+    def decode(self, streams, max_steps: int, stop_at_eos: bool = True, rows=None):
+        """Returns one int32 token array per stream.  rows: each stream reads only its first
+        rows[i] adapter rows (vox_hip_batch_decode_rows; the streams' queues are not waited for)."""
         n = len(streams)
         arr = (ctypes.c_void_p * n)(*[s.h for s in streams])
         toks = np.zeros((n, max(1, max_steps)), np.int32)
         cnt = np.zeros(n, np.int32)
-        r = lib().vox_hip_batch_decode(self.h, arr, n, max_steps, int(stop_at_eos),
-                                       toks.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-                                       cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+        tp = toks.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+        cp = cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+        if rows is None:
+            r = lib().vox_hip_batch_decode(self.h, arr, n, max_steps, int(stop_at_eos), tp, cp)
+        else:
+            rw = np.ascontiguousarray(rows, np.int32)
+            assert rw.shape == (n,), "one row bound per stream"
+            r = lib().vox_hip_batch_decode_rows(self.h, arr, n, rw.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                                max_steps, int(stop_at_eos), tp, cp)
         if r < 0:
             _err("vox_hip_batch_decode")
         return [toks[i, :cnt[i]].copy() for i in range(n)]

@@ -937,8 +937,14 @@ def bench_serve(args, d, cfg, model, st0):
                            "prefill_passes": st["prefill_passes"] - q_stats0["prefill_passes"],
                            "prefilled_streams": st["prefills"] - q_stats0["prefills"],
                            "ticks": ticks},
+        # with the scheduler's overlap (VOX_HIP_SCHED_OVERLAP, default on) the pass's ms run
+        # from its enqueue to its completion, beside the batched steps
         "encoder_passes": {"ms": round(st["enc_ms"] - q_stats0["enc_ms"], 1),
-                           "passes": st["enc_batches"] - q_stats0["enc_batches"]},
+                           "passes": st["enc_batches"] - q_stats0["enc_batches"],
+                           "overlapped": os.environ.get("VOX_HIP_SCHED_OVERLAP", "1") != "0"},
+        # time inside vh_sched_run (encoder pass, prefills, steps) vs the rest of the ticks
+        # (feeding pieces: device mel, conv stems queued; reading ids)
+        "scheduler_run_ms": round(st["run_ms"] - q_stats0["run_ms"], 1),
     }
     emit(d, out)
     q.close()

@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
 
 // ---------------------------------------------------------------------------
 static int g_cus = 0;
-int g_gemmf_blocks = 0;  // tools/kbench knob: grid size (0 = one block per CU)
+int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = 0;      // tools/kbench knob: row blocks per tile with two planes (0 = by shape; 4 or 8)
 int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
 int g_gemmf_wide = -1;   // 64 x 64 per wave (4 waves, 64 x 256 tiles) with two planes (VOX_HIP_GEMMF_WIDE)
@@ -402,6 +402,13 @@ int gemmf_grid() {
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_cus <= 0)
             g_cus = 256;
+    }
+    if (g_gemmf_blocks < 0) {
+        // VOX_HIP_GEMMF_BLOCKS: blocks of the stream-K grid (default one per CU); fewer leave
+        // CUs to kernels running beside an encoder pass (the scheduler's overlap)
+        const char* e = getenv("VOX_HIP_GEMMF_BLOCKS");
+        const int v = e ? atoi(e) : 0;
+        g_gemmf_blocks = v > 0 && v <= 4 * g_cus ? v : 0;
     }
     return g_gemmf_blocks ? g_gemmf_blocks : g_cus;
 }

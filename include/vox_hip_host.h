@@ -106,6 +106,11 @@ vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int d
  *      stops on the device when it has used its adapter rows or produced EOS,
  *   3. applies each stream's live-mode restarts (vh_stream_set_continuous) as run after its
  *      own drain.
+ * By default (VOX_HIP_SCHED_OVERLAP=0: off; off too while a live-mode stream is attached) step
+ * 0's pass is only enqueued and steps 1-2 decode the rows that were complete when the run
+ * started (vox_hip_batch_decode_rows), so the pass runs beside the batched steps and beside the
+ * host's next feeds; its rows are decoded by the next run, which first waits for it.  Greedy
+ * ids do not depend on when a row is decoded.  vh_stream_pending counts those rows.
  * Called after every round of feeds, it yields per stream the ids vh_stream_feed would have
  * queued (vh_stream_get / get_alt read them as before).  Streams with --alt (n_alt > 1) stay
  * in the batch (the batched argmax keeps their candidates); a live-mode stream drains on its
@@ -121,7 +126,8 @@ typedef struct {
     long long steps;         /* batched step replays (tokens / steps = rows per step) */
     long long captures;      /* step-graph captures (vox_hip_batch_stats) */
     long long prefill_passes;/* prefill passes (several new streams share one) */
-    double enc_ms;           /* wall time of the batched encoder passes (step 0, synchronised) */
+    double enc_ms;           /* wall time of the batched encoder passes (step 0: to completion;
+                              * with the overlap, the enqueue only) */
 } vh_sched_stats_t;
 vh_sched_t *vh_sched_create(vh_ctx_t *ctx, int max_streams);
 void vh_sched_free(vh_sched_t *q);          /* detaches its streams */

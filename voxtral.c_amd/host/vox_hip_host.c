@@ -1044,11 +1044,14 @@ void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {
 }
 
 static int sched_overlap(void) {
-    /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start */
+    /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start;
+     * =2: it runs beside the steps and completes before the run returns; default (1): it may
+     * still run when the run returns (the next run waits for it first) */
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("VOX_HIP_SCHED_OVERLAP");
-        v = (e && atoi(e) == 0) ? 0 : 1;
+        v = e ? atoi(e) : 1;
+        if (v < 0 || v > 2) v = 1;
     }
     return v;
 }
@@ -1062,7 +1065,8 @@ int vh_sched_run(vh_sched_t *q) {
      * those are decoded by the next run.  Greedy ids do not depend on when a row is decoded, so
      * a stream's ids are unchanged.  Live-mode streams keep the sequential order: their restart
      * checks belong after a drain of every row of the chunk (voxtral.c:1189-1239). */
-    int overlap = sched_overlap() && sched_batch_encode();
+    const int mode = sched_overlap();
+    int overlap = mode && sched_batch_encode();
     for (int i = 0; i < q->n; i++) overlap = overlap && !q->s[i]->continuous;
     int rows[VH_SCHED_MAX] = {0};
     if (overlap)
@@ -1075,9 +1079,6 @@ int vh_sched_run(vh_sched_t *q) {
             vox_hip_stream_state(s->st, st6);
             ran[i] = st6[3] || rows[i] >= 1 + 32 + s->ctx->delay_tokens;
         }
-    vox_hip_stream_t *enc_q[VH_SCHED_MAX];
-    int enc_n = 0;
-    double enc_t0 = 0.0;
     /* 0. every attached stream's deferred chunk through one batched encoder pass (the layers'
      *    weights read once for all of them) */
     {
@@ -1106,18 +1107,20 @@ int vh_sched_run(vh_sched_t *q) {
                 q->stats.enc_ms += dt;
                 for (int k = 0; k < nb; k++) q->s[idx[k]]->enc_ms += dt / nb;
             } else {
-                /* still running: waited for after the steps (step 4) */
-                for (int k = 0; k < nb; k++) enc_q[k] = hs[k];
-                enc_n = nb;
-                enc_t0 = t0;
+                /* still running when the run returns: the next run's first step waits for it
+                 * (every stream's queue), so the host's feeding of the next pieces overlaps its
+                 * tail too; enc_ms counts the enqueue only */
+                q->stats.enc_ms += now_ms() - t0;
             }
             q->stats.enc_batches++;
             for (int k = 0; k < nb; k++) {
                 vh_stream_t *s = q->s[idx[k]];
                 s->pend_n = 0;
                 s->chunks++;
-                /* the mel frames the pass reads stay: discarded after it completes */
-                if (!overlap && vox_hip_mel_discard_before(s->mel, s->mel_cursor)) return -1;
+                /* safe with the pass in flight: discarding frees no device memory (a later grow
+                 * of the mel buffer frees the old one through hipFree, which waits for the
+                 * device) and the sample compaction is ordered on the stream's queue */
+                if (vox_hip_mel_discard_before(s->mel, s->mel_cursor)) return -1;
             }
         }
     }
@@ -1185,15 +1188,10 @@ int vh_sched_run(vh_sched_t *q) {
         /* with a step cap, a scheduled stream's rows beyond it wait for the next run */
         if (r == 0 || !more) break;
     }
-    /* 4 (overlap). the encoder pass that ran beside the steps completes; its frames go */
-    if (enc_n) {
-        for (int k = 0; k < enc_n; k++)
-            if (vox_hip_stream_sync(enc_q[k])) return fail("encoder: %s", vox_hip_last_error());
-        q->stats.enc_ms += now_ms() - enc_t0;
+    /* 4 (VOX_HIP_SCHED_OVERLAP=2). the pass beside the steps completes before the run returns */
+    if (overlap && mode == 2)
         for (int i = 0; i < q->n; i++)
-            for (int k = 0; k < enc_n; k++)
-                if (q->s[i]->st == enc_q[k] && vox_hip_mel_discard_before(q->s[i]->mel, q->s[i]->mel_cursor)) return -1;
-    }
+            if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
     /* 3. per-stream live-mode restarts (voxtral.c:1189-1239) */
     for (int i = 0; i < q->n; i++)
         if (ran[i] == 1 && after_drain(q->s[i], eos[i])) return -1;

@@ -938,7 +938,7 @@ def bench_serve(args, d, cfg, model, st0):
                            "prefilled_streams": st["prefills"] - q_stats0["prefills"],
                            "ticks": ticks},
         # with the scheduler's overlap (VOX_HIP_SCHED_OVERLAP, default on) the passes run beside
-        # the batched steps and the next feeds, and their ms count the enqueue only
+        # the batched steps and their ms count the enqueue only
         "encoder_passes": {"ms": round(st["enc_ms"] - q_stats0["enc_ms"], 1),
                            "passes": st["enc_batches"] - q_stats0["enc_batches"],
                            "overlapped": os.environ.get("VOX_HIP_SCHED_OVERLAP", "1") != "0"},

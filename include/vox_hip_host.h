@@ -108,9 +108,9 @@ vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int d
  *      own drain.
  * By default (VOX_HIP_SCHED_OVERLAP=0: off; off too while a live-mode stream is attached) step
  * 0's pass is only enqueued and steps 1-2 decode the rows that were complete when the run
- * started (vox_hip_batch_decode_rows), so the pass runs beside the batched steps and beside the
- * host's next feeds; its rows are decoded by the next run, which first waits for it.  Greedy
- * ids do not depend on when a row is decoded.  vh_stream_pending counts those rows.
+ * started (vox_hip_batch_decode_rows), so the pass runs beside the batched steps; it completes
+ * before the run returns and its rows are decoded by the next run.  Greedy ids do not depend
+ * on when a row is decoded.  vh_stream_pending counts those rows.
  * Called after every round of feeds, it yields per stream the ids vh_stream_feed would have
  * queued (vh_stream_get / get_alt read them as before).  Streams with --alt (n_alt > 1) stay
  * in the batch (the batched argmax keeps their candidates); a live-mode stream drains on its

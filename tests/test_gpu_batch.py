@@ -326,3 +326,37 @@ def test_batch_alternatives_match_stream_fill_alts(models, tiny_cfg):
     for s in ss:
         s.close()
     b.close()
+
+
+def test_batch_decode_rows_bounds_each_stream(models, tiny_cfg):
+    """vox_hip_batch_decode_rows: stream i reads only its first rows[i] adapter rows (the
+    scheduler's overlap decodes the rows complete at a run's start while the next encoder
+    pass runs); decoding in row-bounded pieces -- a bound below the prompt (no prefill yet),
+    the prompt plus a few rows, then everything -- gives the oracle's ids."""
+    import vox_hip
+    hm, om = models
+    mels = _mels(tiny_cfg, [420, 510, 380], 77)
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    total = [s.adapter_tokens for s in ss]
+    b = vox_hip.Batch(hm, 4)
+    got = [[] for _ in ss]
+    # below the prompt: nothing runs
+    out = b.decode(ss, max_steps=1000, stop_at_eos=False, rows=[10, 20, 5])
+    assert all(len(t) == 0 for t in out)
+    # ragged bounds, then the rest in two more pieces
+    for frac in (0.45, 0.8, 1.0):
+        bounds = [max(1, int(round(t * frac))) for t in total]
+        out = b.decode(ss, max_steps=1000, stop_at_eos=False, rows=bounds)
+        for i, t in enumerate(out):
+            got[i] += t.tolist()
+            gp = ss[i].state()["gen_pos"]
+            assert gp <= bounds[i], (i, gp, bounds[i])   # next adapter row within the bound
+    for i, mel in enumerate(mels):
+        assert got[i] == _reference_tokens(om, mel), i
+    with pytest.raises(RuntimeError):
+        b.decode(ss, max_steps=10, stop_at_eos=False, rows=[total[0] + 1, 1, 1])  # past the rows
+    for s in ss:
+        s.close()
+    b.close()

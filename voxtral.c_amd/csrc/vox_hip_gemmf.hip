@@ -376,8 +376,6 @@ static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = 0;      // tools/kbench knob: row blocks per tile with two planes (0 = by shape; 4 or 8)
 int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
-int g_gemmf_wide = -1;   // 64 x 64 per wave (4 waves, 64 x 256 tiles) with two planes (VOX_HIP_GEMMF_WIDE)
-int g_gemmf_ng = 0;      // tools/kbench knob: 4 = 4 column groups per wave with 8 waves (x 256-column tiles)
 
 template <int EPI, int NP, int RB, int NG, int WR>
 static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
@@ -433,17 +431,11 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     // two planes: 128-row tiles while they alone give every CU a tile; narrower outputs (the
     // N = 1280 wo / W2 passes: 10 column tiles) take 64-row tiles -- a stream-K tile split over
     // many blocks costs more than the lower weight reuse (kbench, profiles/r3_gemmf_sweep.txt)
-    if (g_gemmf_wide < 0) {
-        const char* e = getenv("VOX_HIP_GEMMF_WIDE");
-        g_gemmf_wide = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    // wide: each wave owns 64 rows x 64 columns (4 x 4 MFMA tiles): 12 fragment reads per 32
-    // MFMAs instead of 10 per 16 (the LDS reads per MFMA bound the 8-wave kernel)
-    const bool wide = g_gemmf_wide && np == 2 && N % 256 == 0;
-    const bool ng4 = !wide && g_gemmf_ng == 4 && np == 2 && N % 256 == 0;
-    const int NGx = (wide || ng4) ? 4 : NG;
+    // (wider per-wave tiles -- 64 x 64 with 4 waves, 32 x 64 with 8 -- measured slower on every
+    // encoder shape: DESIGN.md 14.2, profiles/r4_kbench_gemmf*.txt)
+    const int NGx = NG;
     const int t8 = ((M + 127) / 128) * (N / (64 * NG));
-    const int RB = wide ? 4 : np == 3 ? 4 : g_gemmf_rb ? g_gemmf_rb : (t8 >= gemmf_grid() ? 8 : 4);
+    const int RB = np == 3 ? 4 : g_gemmf_rb ? g_gemmf_rb : (t8 >= gemmf_grid() ? 8 : 4);
     GemmfArgs a;
     a.xs = xs; a.K = K; a.M = M; a.W = static_cast<const uint8_t*>(Wf); a.N = N; a.bias = bias; a.C = C; a.ldc = ldc;
     a.xo = xo; a.ws = ws; a.flags = flags; a.epoch = epoch;
@@ -462,9 +454,7 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     if ((size_t)G * 4 * RB * NGx * 256 > ws_floats) return hipErrorInvalidValue;
 #define GF_EPI(E)                                                                               \
     if (epi == E)                                                                               \
-        return wide ? gemmf_launch<E, 2, 4, 4, 1>(a, G, st)                                     \
-               : ng4 ? (RB == 8 ? gemmf_launch<E, 2, 8, 4, WR>(a, G, st) : gemmf_launch<E, 2, 4, 4, WR>(a, G, st)) \
-               : np == 3 ? gemmf_launch<E, 3, 4, NG, WR>(a, G, st)                              \
+        return np == 3 ? gemmf_launch<E, 3, 4, NG, WR>(a, G, st)                                \
                : RB == 8 ? gemmf_launch<E, 2, 8, NG, WR>(a, G, st) : gemmf_launch<E, 2, 4, NG, WR>(a, G, st);
     GF_EPI(EPI_STORE) GF_EPI(EPI_RESID) GF_EPI(EPI_GELU) GF_EPI(EPI_GELU_ERF) GF_EPI(EPI_SWIGLU)
 #undef GF_EPI

@@ -1044,14 +1044,11 @@ void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {
 }
 
 static int sched_overlap(void) {
-    /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start;
-     * =2: it runs beside the steps and completes before the run returns; default (1): it may
-     * still run when the run returns (the next run waits for it first) */
+    /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start */
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("VOX_HIP_SCHED_OVERLAP");
-        v = e ? atoi(e) : 1;
-        if (v < 0 || v > 2) v = 1;
+        v = (e && atoi(e) == 0) ? 0 : 1;
     }
     return v;
 }
@@ -1065,8 +1062,7 @@ int vh_sched_run(vh_sched_t *q) {
      * those are decoded by the next run.  Greedy ids do not depend on when a row is decoded, so
      * a stream's ids are unchanged.  Live-mode streams keep the sequential order: their restart
      * checks belong after a drain of every row of the chunk (voxtral.c:1189-1239). */
-    const int mode = sched_overlap();
-    int overlap = mode && sched_batch_encode();
+    int overlap = sched_overlap() && sched_batch_encode();
     for (int i = 0; i < q->n; i++) overlap = overlap && !q->s[i]->continuous;
     int rows[VH_SCHED_MAX] = {0};
     if (overlap)
@@ -1107,9 +1103,9 @@ int vh_sched_run(vh_sched_t *q) {
                 q->stats.enc_ms += dt;
                 for (int k = 0; k < nb; k++) q->s[idx[k]]->enc_ms += dt / nb;
             } else {
-                /* still running when the run returns: the next run's first step waits for it
-                 * (every stream's queue), so the host's feeding of the next pieces overlaps its
-                 * tail too; enc_ms counts the enqueue only */
+                /* still running: it completes beside the steps (step 4); enc_ms counts the
+                 * enqueue.  (Leaving it running past the run's end, for the next run to wait
+                 * for, measured no faster: profiles/r4_serve_overlap_ab.txt.) */
                 q->stats.enc_ms += now_ms() - t0;
             }
             q->stats.enc_batches++;
@@ -1188,8 +1184,8 @@ int vh_sched_run(vh_sched_t *q) {
         /* with a step cap, a scheduled stream's rows beyond it wait for the next run */
         if (r == 0 || !more) break;
     }
-    /* 4 (VOX_HIP_SCHED_OVERLAP=2). the pass beside the steps completes before the run returns */
-    if (overlap && mode == 2)
+    /* 4 (overlap). the pass beside the steps completes before the run returns */
+    if (overlap)
         for (int i = 0; i < q->n; i++)
             if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
     /* 3. per-stream live-mode restarts (voxtral.c:1189-1239) */

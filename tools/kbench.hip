@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -614,18 +614,20 @@ int main(int argc, char** argv) {
         for (int M : {70, 677, 1024})
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
                         G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
-                for (int v = 0; v < 4; v++) {
-                    // np2 with the launcher's tile choice, np2 RB8, np2 RB4, np3 (RB4); the wider
-                    // per-wave tiles measured in round 4 are in profiles/r4_kbench_gemmf*.txt
+                for (int v = 0; v < 7; v++) {
+                    // np2 with the launcher's tile choice, np2 RB8, np2 RB4, np3 (RB4), then the
+                    // same np2 tiles with 16 waves per block (wr4: 4 row shares, 32 x 32 / 16 x 32
+                    // per wave); the wider per-wave tiles of round 4 are in profiles/r4_kbench_gemmf*.txt
                     const int np = v == 3 ? 3 : 2;
-                    g_gemmf_rb = v == 1 ? 8 : v == 2 ? 4 : 0;
+                    g_gemmf_rb = v == 1 || v == 5 ? 8 : v == 2 || v == 6 ? 4 : 0;
+                    g_gemmf_wr = v >= 4 ? 4 : 0;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
                     printf("gemmf %-4s M=%4d %dx%d np%d rb%d%s minu%-2d %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
-                           g.K, np, g_gemmf_rb, "", g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                           g.K, np, g_gemmf_rb, g_gemmf_wr == 4 ? " wr4" : "", g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
-                g_gemmf_rb = g_gemmf_minu = 0;
+                g_gemmf_rb = g_gemmf_minu = g_gemmf_wr = 0;
             }
     }
     if (only_gemmf) return 0;

@@ -376,6 +376,7 @@ static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = 0;      // tools/kbench knob: row blocks per tile with two planes (0 = by shape; 4 or 8)
 int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
+int g_gemmf_wr = 0;      // tools/kbench knob: 4 = 16 waves per block (4 row shares, two planes)
 
 template <int EPI, int NP, int RB, int NG, int WR>
 static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
@@ -455,6 +456,8 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
 #define GF_EPI(E)                                                                               \
     if (epi == E)                                                                               \
         return np == 3 ? gemmf_launch<E, 3, 4, NG, WR>(a, G, st)                                \
+               : g_gemmf_wr == 4 ? (RB == 8 ? gemmf_launch<E, 2, 8, NG, 4>(a, G, st)             \
+                                            : gemmf_launch<E, 2, 4, NG, 4>(a, G, st))            \
                : RB == 8 ? gemmf_launch<E, 2, 8, NG, WR>(a, G, st) : gemmf_launch<E, 2, 4, NG, WR>(a, G, st);
     GF_EPI(EPI_STORE) GF_EPI(EPI_RESID) GF_EPI(EPI_GELU) GF_EPI(EPI_GELU_ERF) GF_EPI(EPI_SWIGLU)
 #undef GF_EPI

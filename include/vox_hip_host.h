@@ -104,7 +104,8 @@ vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int d
  *      argmax per stream): streams whose prompt rows just completed are prefilled together
  *      in one stacked pass and take their first token in the batched steps, and every stream
  *      stops on the device when it has used its adapter rows or produced EOS,
- *   3. applies each stream's live-mode restarts (vh_stream_set_continuous) as run after its
+ *   3. waits for step 0's pass when it ran beside the steps (below),
+ *   4. applies each stream's live-mode restarts (vh_stream_set_continuous) as run after its
  *      own drain.
  * By default (VOX_HIP_SCHED_OVERLAP=0: off; off too while a live-mode stream is attached) step
  * 0's pass is only enqueued and steps 1-2 decode the rows that were complete when the run

@@ -620,14 +620,15 @@ int main(int argc, char** argv) {
                     // per wave); the wider per-wave tiles of round 4 are in profiles/r4_kbench_gemmf*.txt
                     const int np = v == 3 ? 3 : 2;
                     g_gemmf_rb = v == 1 || v == 5 ? 8 : v == 2 || v == 6 ? 4 : 0;
-                    g_gemmf_wr = v >= 4 ? 4 : 0;
+                    g_gemmf_wr = v >= 4 ? 4 : 2;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
                     printf("gemmf %-4s M=%4d %dx%d np%d rb%d%s minu%-2d %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
                            g.K, np, g_gemmf_rb, g_gemmf_wr == 4 ? " wr4" : "", g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
-                g_gemmf_rb = g_gemmf_minu = g_gemmf_wr = 0;
+                g_gemmf_rb = g_gemmf_minu = 0;
+                g_gemmf_wr = -1;
             }
     }
     if (only_gemmf) return 0;

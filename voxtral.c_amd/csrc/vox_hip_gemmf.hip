@@ -7,9 +7,10 @@
 // fragment-major layout of k_frag_pack / frag_at: every 1 KiB of either is one
 // v_mfma_f32_16x16x32_bf16 operand fragment (16 rows x 32 k, lane-linear).
 //
-// Block = 4 waves, tile = RB row blocks of 16 x 4 NG column groups of 16; wave w owns column
-// groups w NG .. w NG + NG - 1 against every row block (W fragments are per wave, the planes
-// are shared).  K runs in 64-deep stages:
+// Block = 4 WR waves, tile = RB row blocks of 16 x 4 NG column groups of 16; wave w owns
+// column groups (w % 4) NG .. + NG - 1 against row share w / 4 (RB / WR row blocks): W
+// fragments per column slot, planes per row share, both through LDS.  K runs in 64-deep
+// stages:
 //   * planes: global_load_lds (LDS-DMA, no VGPRs) into a 3-slot LDS ring, 2 stages ahead;
 //     each 1 KiB chunk lands lane-linear and is read back by one conflict-free ds_read_b128;
 //   * weights: straight to VGPRs through a buffer descriptor, a 3-deep register ring, 2
@@ -376,7 +377,12 @@ static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = 0;      // tools/kbench knob: row blocks per tile with two planes (0 = by shape; 4 or 8)
 int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
-int g_gemmf_wr = 0;      // tools/kbench knob: 4 = 16 waves per block (4 row shares, two planes)
+// waves per block with two planes: 16 (4 row shares of a 128- or 64-row tile: 32 x 32 or 16 x
+// 32 per wave, four waves per SIMD) by default, 8 with VOX_HIP_GEMMF_WR=2 (64 x 32 per wave,
+// two per SIMD).  Same unit ranges, same per-output summation order: the same bits.  tools/
+// kbench (profiles/r4_kbench_gemmf_wr4.txt): M = 677 W1|W3 47.9 -> 44.6, W2 25.6 -> 23.8 us,
+// QKV / wo equal; M = 1024 W1|W3 54.5 -> 48.4 us.  Three planes keep 8 (24 chunks a stage).
+int g_gemmf_wr = -1;
 
 template <int EPI, int NP, int RB, int NG, int WR>
 static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
@@ -425,7 +431,8 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
                         float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
                         hipStream_t st) {
     // tiles: 128 x 128 with two planes; 64 x 128 with three (a 3-slot ring of 8 row blocks'
-    // three planes would not fit the 160 KB of LDS); 8 waves (two per SIMD)
+    // three planes would not fit the 160 KB of LDS); 16 waves with two planes (g_gemmf_wr),
+    // 8 with three
     constexpr int NG = 2, WR = 2;
     if (!gemmf_ok(M, N, K) || (np != 2 && np != 3) || !ws || !flags || (g_gemmf_rb && g_gemmf_rb != 4 && g_gemmf_rb != 8))
         return hipErrorInvalidValue;
@@ -459,6 +466,10 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
                : g_gemmf_wr == 4 ? (RB == 8 ? gemmf_launch<E, 2, 8, NG, 4>(a, G, st)             \
                                             : gemmf_launch<E, 2, 4, NG, 4>(a, G, st))            \
                : RB == 8 ? gemmf_launch<E, 2, 8, NG, WR>(a, G, st) : gemmf_launch<E, 2, 4, NG, WR>(a, G, st);
+    if (g_gemmf_wr < 0) {
+        const char* e = getenv("VOX_HIP_GEMMF_WR");
+        g_gemmf_wr = (e && atoi(e) == 2) ? 2 : 4;
+    }
     GF_EPI(EPI_STORE) GF_EPI(EPI_RESID) GF_EPI(EPI_GELU) GF_EPI(EPI_GELU_ERF) GF_EPI(EPI_SWIGLU)
 #undef GF_EPI
     return hipErrorInvalidValue;

@@ -1103,7 +1103,7 @@ int vh_sched_run(vh_sched_t *q) {
                 q->stats.enc_ms += dt;
                 for (int k = 0; k < nb; k++) q->s[idx[k]]->enc_ms += dt / nb;
             } else {
-                /* still running: it completes beside the steps (step 4); enc_ms counts the
+                /* still running: it completes beside the steps (step 3); enc_ms counts the
                  * enqueue.  (Leaving it running past the run's end, for the next run to wait
                  * for, measured no faster: profiles/r4_serve_overlap_ab.txt.) */
                 q->stats.enc_ms += now_ms() - t0;
@@ -1137,7 +1137,7 @@ int vh_sched_run(vh_sched_t *q) {
         for (int i = 0; i < q->n; i++) {
             vh_stream_t *s = q->s[i];
             if (!ran[i] || eos[i]) continue;
-            /* past a step cap only live-mode streams go on: their restart checks (step 3)
+            /* past a step cap only live-mode streams go on: their restart checks (step 4)
              * belong after a full drain, as in the reference */
             if (iter > 0 && q->step_cap > 0 && !s->continuous) continue;
             int st6[6];
@@ -1184,11 +1184,11 @@ int vh_sched_run(vh_sched_t *q) {
         /* with a step cap, a scheduled stream's rows beyond it wait for the next run */
         if (r == 0 || !more) break;
     }
-    /* 4 (overlap). the pass beside the steps completes before the run returns */
+    /* 3 (overlap). the pass beside the steps completes before the run returns */
     if (overlap)
         for (int i = 0; i < q->n; i++)
             if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
-    /* 3. per-stream live-mode restarts (voxtral.c:1189-1239) */
+    /* 4. per-stream live-mode restarts (voxtral.c:1189-1239) */
     for (int i = 0; i < q->n; i++)
         if (ran[i] == 1 && after_drain(q->s[i], eos[i])) return -1;
     q->stats.runs++;

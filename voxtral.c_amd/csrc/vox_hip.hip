@@ -720,13 +720,6 @@ struct vox_hip_mel {
     int mel_cap, mel_phys0;
     int frame_offset, n_frames;             // live frames: global [frame_offset, frame_offset + n_frames)
     int finished;
-    // pinned staging of the fed samples: the host -> device copy is then asynchronous (a
-    // pageable copy waits for the stream's earlier work, e.g. an encoder pass, and blocks the
-    // feeding thread); pin_ev marks the last copy out of it
-    float* pin;
-    int pin_cap;
-    hipEvent_t pin_ev;
-    int pin_used;
 };
 
 // hertz_to_mel / mel_to_hertz / build_mel_filters (voxtral_audio.c:223-285), f32 as there
@@ -747,8 +740,6 @@ extern "C" void vox_hip_mel_free(vox_hip_mel_t* m) {
     if (!m) return;
     if (m->s) hipStreamSynchronize(m->s->st);
     dfree(m->window); dfree(m->dcosT); dfree(m->dsinT); dfree(m->filtT); dfree(m->samples); dfree(m->mel);
-    if (m->pin) hipHostFree(m->pin);
-    if (m->pin_ev) hipEventDestroy(m->pin_ev);
     delete m;
 }
 
@@ -871,33 +862,7 @@ extern "C" int vox_hip_mel_feed(vox_hip_mel_t* m, const float* samples, int n) {
     if (!m || m->finished) return set_err("vox_hip_mel_feed: no context or already finished");
     if (n <= 0) return 0;
     if (mel_reserve_samples(m, m->n_samples + n)) return -1;
-    static int pin_env = -1;  // VOX_HIP_MEL_PIN=0: copy straight from the caller's pageable memory
-    if (pin_env < 0) {
-        const char* e = getenv("VOX_HIP_MEL_PIN");
-        pin_env = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    if (!pin_env) {
-        CK(hipMemcpyAsync(m->samples + m->n_samples, samples, (size_t)n * 4, hipMemcpyHostToDevice, m->s->st));
-        m->n_samples += n;
-        const int nf = mel_compute(m);
-        if (nf < 0 || mel_compact(m)) return -1;
-        return nf;
-    }
-    if (m->pin_used) CK(hipEventSynchronize(m->pin_ev));  // the previous copy out of the staging
-    if (n > m->pin_cap) {
-        if (m->pin) CK(hipHostFree(m->pin));
-        m->pin = nullptr;
-        m->pin_cap = 0;
-        int cap = 8192;
-        while (cap < n) cap *= 2;
-        CK(hipHostMalloc((void**)&m->pin, (size_t)cap * 4, hipHostMallocDefault));
-        m->pin_cap = cap;
-    }
-    if (!m->pin_ev) CK(hipEventCreateWithFlags(&m->pin_ev, hipEventDisableTiming));
-    memcpy(m->pin, samples, (size_t)n * 4);
-    CK(hipMemcpyAsync(m->samples + m->n_samples, m->pin, (size_t)n * 4, hipMemcpyHostToDevice, m->s->st));
-    CK(hipEventRecord(m->pin_ev, m->s->st));
-    m->pin_used = 1;
+    CK(hipMemcpyAsync(m->samples + m->n_samples, samples, (size_t)n * 4, hipMemcpyHostToDevice, m->s->st));
     m->n_samples += n;
     const int nf = mel_compute(m);
     if (nf < 0 || mel_compact(m)) return -1;

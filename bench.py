@@ -827,6 +827,7 @@ def bench_serve(args, d, cfg, model, st0):
         nxt = list(range(S))
         ids, lat, clips_done, tick = 0, [], 0, 0
         full = [0, 0.0]         # ids and wall time of the ticks in which all S streams were live
+        host = [0.0, 0.0, 0.0]  # wall in the feeds, in vh_sched_run, in reading ids / retiring clips
         t_all = time.perf_counter()
         while True:
             live = False
@@ -859,7 +860,11 @@ def bench_serve(args, d, cfg, model, st0):
                     cur[k][3] = True
             if not live:
                 break
+            t1 = time.perf_counter()
             q.run()
+            t2 = time.perf_counter()
+            host[0] += t1 - t0
+            host[1] += t2 - t1
             tick_ids = 0
             for k in range(S):
                 if cur[k] is None:
@@ -873,12 +878,14 @@ def bench_serve(args, d, cfg, model, st0):
                     clips_done += 1
             ids += tick_ids
             lat.append(time.perf_counter() - t0)
+            host[2] += time.perf_counter() - t2
             if n_live == S:
                 full[0] += tick_ids
                 full[1] += lat[-1]
             tick += 1
         return {"wall": time.perf_counter() - t_all, "ids": ids, "lat": lat, "ticks": tick,
-                "clips": clips_done, "audio_s": sum(served), "full_ids": full[0], "full_s": full[1]}
+                "clips": clips_done, "audio_s": sum(served), "full_ids": full[0], "full_s": full[1],
+                "host": host}
 
     for _ in range(args.warmup):
         run(min(args.serve_seconds, 20.0))
@@ -945,6 +952,10 @@ def bench_serve(args, d, cfg, model, st0):
         # time inside vh_sched_run (encoder pass, prefills, steps) vs the rest of the ticks
         # (feeding pieces: device mel, conv stems queued; reading ids)
         "scheduler_run_ms": round(st["run_ms"] - q_stats0["run_ms"], 1),
+        # the tick loop's wall split: feeding the pieces (device mel, conv stems queued), the
+        # scheduler run, reading ids and retiring finished clips
+        "tick_wall_ms": {k: round(1000.0 * sum(r["host"][i] for r in runs), 1)
+                         for i, k in enumerate(("feed", "run", "collect"))},
     }
     emit(d, out)
     q.close()

@@ -73,6 +73,9 @@ def parse():
                          "clip is finished and drained: all streams live from the last start to the end; "
                          "'per-stream' -- each stream until it has served serve-seconds (whole clips: the "
                          "streams end apart, a long tail at low occupancy)")
+    ap.add_argument("--serve-fresh-streams", action="store_true",
+                    help="--stagger: vh_stream_init / free for every clip instead of reusing a slot's stream "
+                         "through vh_stream_reset")
     ap.add_argument("--serve-step-cap", type=int, default=8,
                     help="--stagger: greedy steps per stream and scheduler run (vh_sched_set_step_cap; 0 = "
                          "drain every run): a stream's bursts (prompt, flush padding) ride in full batched "
@@ -819,6 +822,7 @@ def bench_serve(args, d, cfg, model, st0):
     clips = [synth_audio(sec, 500 + k) for k, sec in enumerate(SAMPLE_SECONDS)]
 
     common = args.serve_end == "common"
+    pool = [[] for _ in range(S)]   # reusable vh_streams per stream slot
 
     def run(serve_s):
         end_tick = int(round(2 * serve_s)) + S - 1  # common end (ticks of 0.5 s)
@@ -840,7 +844,10 @@ def bench_serve(args, d, cfg, model, st0):
                 if cur[k] is None:
                     if (tick >= end_tick) if common else (served[k] >= serve_s):
                         continue
-                    hs = vox_hip.HostStream(ctx, interval_s=0.5)
+                    # a fresh vh_stream per clip, reused from the slot's pool (vh_stream_reset:
+                    # the state vh_stream_init leaves, without its device allocations) unless
+                    # --serve-fresh-streams
+                    hs = pool[k].pop() if pool[k] else vox_hip.HostStream(ctx, interval_s=0.5)
                     q.attach(hs)
                     cur[k] = [hs, nxt[k] % len(clips), 0, False]
                     nxt[k] += 1
@@ -873,7 +880,11 @@ def bench_serve(args, d, cfg, model, st0):
                 if cur[k][3] and cur[k][0].pending() == 0:   # finished and drained: retire the clip
                     served[k] += min(cur[k][2], len(clips[cur[k][1]])) / 16000.0
                     q.detach(cur[k][0])
-                    cur[k][0].close()
+                    if args.serve_fresh_streams:
+                        cur[k][0].close()
+                    else:
+                        cur[k][0].reset()
+                        pool[k].append(cur[k][0])
                     cur[k] = None
                     clips_done += 1
             ids += tick_ids
@@ -894,6 +905,9 @@ def bench_serve(args, d, cfg, model, st0):
     runs = [run(args.serve_seconds) for _ in range(args.steps)]
     d.barrier()
     st = q.stats()
+    for p in pool:
+        for hs in p:
+            hs.close()
     wall = d.max(sum(r["wall"] for r in runs))
     ids_all = d.sum(sum(r["ids"] for r in runs))
     audio_all = d.sum(sum(r["audio_s"] for r in runs))
@@ -923,7 +937,9 @@ def bench_serve(args, d, cfg, model, st0):
                                   if args.serve_step_cap > 0 else ""),
                    "model": "Voxtral-Mini-4B-Realtime", "global_batch": S * d.world, "streams_per_gpu": S,
                    "parallelism": f"replicas x{d.world}, {S} scheduled streams each",
-                   "serve_end": args.serve_end, "serve_step_cap": args.serve_step_cap},
+                   "serve_end": args.serve_end, "serve_step_cap": args.serve_step_cap,
+                   "streams_per_clip": "fresh (vh_stream_init)" if args.serve_fresh_streams
+                                       else "reused (vh_stream_reset)"},
         "value_is": "all ids generated / wall time of the serving loop (mel, encoder, prefill and decode included)",
         "tick_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
                             "p99": round(float(np.percentile(lat, 99)), 3), "max": round(float(lat.max()), 3)},

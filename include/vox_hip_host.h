@@ -47,6 +47,11 @@ const char *vh_last_error(void);
 /* vox_stream_init (voxtral.c:1242-1286) */
 vh_stream_t *vh_stream_init(vh_ctx_t *ctx);
 void vh_stream_free(vh_stream_t *s);
+/* A detached stream back to the state vh_stream_init leaves, keeping its device buffers and its
+ * settings (processing interval, live mode, alternatives): new audio on a reused stream, as a
+ * server keeps a pool of them, without vh_stream_init's allocations (no reference counterpart;
+ * the state reset is stream_reset_full_state's, voxtral.c:786-814).  0, or -1. */
+int vh_stream_reset(vh_stream_t *s);
 /* vox_set_processing_interval (voxtral.c:1669-1675) */
 void vh_set_processing_interval(vh_stream_t *s, float seconds);
 /* vox_stream_feed / vox_stream_flush / vox_stream_finish (voxtral.c:1288-1316,

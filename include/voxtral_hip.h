@@ -182,6 +182,9 @@ int vox_hip_mel_discard_before(vox_hip_mel_t *m, int keep_from_frame);
 int vox_hip_mel_read(vox_hip_mel_t *m, int global_first, int n, float *out);
 /* vox_mel_free (voxtral_audio.c:664-671) */
 void vox_hip_mel_free(vox_hip_mel_t *m);
+/* The state vox_hip_mel_create leaves (200 + left_pad_samples zeros, no frames), keeping the
+ * context's device tables and buffers: a reused stream's new audio (vh_stream_reset). */
+int vox_hip_mel_reset(vox_hip_mel_t *m, int left_pad_samples);
 /* Copy adapter rows [first, first+n) to host (tests). */
 int vox_hip_stream_read_adapter(vox_hip_stream_t *s, int first, int n, float *out);
 

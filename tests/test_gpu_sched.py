@@ -250,3 +250,66 @@ def test_scheduler_full_size_matches_oracle(jfk_samples):
     om.close()
     assert st["prefill_passes"] >= 1 and st["steps"] > 0
     print("full-size scheduler stats", st)
+
+
+def test_host_stream_reset_reuses_like_fresh(tiny_weights, jfk_samples):
+    """vh_stream_reset: a stream that served one clip, was detached and reset serves the next
+    clip (scheduled, with another stream beside it) with the ids of a fresh stream -- the
+    oracle's for that clip; bench.py --stagger reuses its streams this way."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    long = np.concatenate([jfk_samples] * 2)
+    clip1 = np.ascontiguousarray(long[:int(7.3 * 16000)])
+    clip2 = np.ascontiguousarray(long[8000:8000 + int(9.1 * 16000)])
+    other = np.ascontiguousarray(long[3000:3000 + int(6.0 * 16000)])
+    ctx = vox_hip.HostCtx(hm)
+    q = vox_hip.Scheduler(ctx, 4)
+    q.set_step_cap(8)
+
+    def serve(pairs):
+        """pairs of (stream, audio): fed together, one vh_sched_run per tick, drained"""
+        pos = [0] * len(pairs)
+        fin = [False] * len(pairs)
+        ids = [[] for _ in pairs]
+        while not all(fin) or any(s.pending() for s, _ in pairs):
+            for k, (s, a) in enumerate(pairs):
+                if fin[k]:
+                    continue
+                if pos[k] < len(a):
+                    s.feed(a[pos[k]:pos[k] + PIECE])
+                    pos[k] += PIECE
+                else:
+                    s.finish()
+                    fin[k] = True
+            q.run()
+            for k, (s, _) in enumerate(pairs):
+                ids[k] += s.get()
+        return ids
+
+    a = vox_hip.HostStream(ctx, interval_s=0.5)
+    b = vox_hip.HostStream(ctx, interval_s=0.5)
+    q.attach(a)
+    q.attach(b)
+    got1, _ = serve([(a, clip1), (b, other)])
+    q.detach(a)
+    a.reset()
+    b2 = vox_hip.HostStream(ctx, interval_s=0.5)
+    q.detach(b)
+    b.close()
+    q.attach(a)
+    q.attach(b2)
+    got2, _ = serve([(a, clip2), (b2, other)])
+    want1, _ = _oracle_ids(om, clip1, 0.5)
+    want2, _ = _oracle_ids(om, clip2, 0.5)
+    assert got1 == want1
+    assert got2 == want2, (len(got2), len(want2))
+    for s in (a, b2):
+        q.detach(s)
+        s.close()
+    q.close()
+    ctx.close()
+    hm.close()
+    om.close()

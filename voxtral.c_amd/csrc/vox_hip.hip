@@ -858,6 +858,20 @@ static int mel_compact(vox_hip_mel_t* m) {
     return 0;
 }
 
+extern "C" int vox_hip_mel_reset(vox_hip_mel_t* m, int left_pad_samples) {
+    if (!m || left_pad_samples < 0) return set_err("vox_hip_mel_reset: bad arguments");
+    const long long n0 = 200 + (long long)left_pad_samples;
+    if (mel_reserve_samples(m, n0)) return -1;
+    CK(hipMemsetAsync(m->samples, 0, (size_t)n0 * 4, m->s->st));
+    m->n_samples = n0;
+    m->sample_offset = 0;
+    m->mel_phys0 = 0;
+    m->frame_offset = 0;
+    m->n_frames = 0;
+    m->finished = 0;
+    return 0;
+}
+
 extern "C" int vox_hip_mel_feed(vox_hip_mel_t* m, const float* samples, int n) {
     if (!m || m->finished) return set_err("vox_hip_mel_feed: no context or already finished");
     if (n <= 0) return 0;

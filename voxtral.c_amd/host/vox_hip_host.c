@@ -647,6 +647,23 @@ void vh_stream_free(vh_stream_t *s) {
     free(s);
 }
 
+int vh_stream_reset(vh_stream_t *s) {
+    if (!s) return -1;
+    if (s->sched) return fail("vh_stream_reset: detach the stream from its scheduler first");
+    if (vox_hip_stream_sync(s->st)) return fail("sync: %s", vox_hip_last_error());
+    if (vox_hip_mel_reset(s->mel, 32 * RAW_AUDIO_LENGTH_PER_TOK) || vox_hip_stream_reset(s->st))
+        return fail("reset: %s", vox_hip_last_error());
+    /* everything vh_stream_init leaves zero goes back to zero; buffers and settings stay */
+    s->mel_cursor = s->conv_started = s->finished = 0;
+    s->real_samples = s->last_decode_sample = 0;
+    s->q_head = s->q_tail = 0;
+    s->generated = s->chunks = s->started_decoding = 0;
+    s->pend_first = s->pend_n = 0;
+    s->nontext_streak = s->text_since_restart = s->empty_restarts = s->restarts = s->full_resets = 0;
+    s->enc_ms = s->dec_ms = s->prefill_ms = 0.0;
+    return 0;
+}
+
 void vh_stream_set_continuous(vh_stream_t *s, int on) { s->continuous = on ? 1 : 0; }
 
 int vh_stream_set_alt(vh_stream_t *s, int n_alt, float cutoff) {

@@ -51,7 +51,7 @@ EXPORTS = [
     "vox_hip_decoder_full_step", "vox_hip_stream_set_profiling", "vox_hip_stream_profile",
     "vox_hip_stream_sync", "vox_hip_stream_set_async_encode", "vox_hip_stream_encode_mel_batch", "vox_hip_device_upload", "vox_hip_device_free",
     "vox_hip_mel_create", "vox_hip_mel_feed", "vox_hip_mel_finish", "vox_hip_mel_frames",
-    "vox_hip_mel_frame_ptr", "vox_hip_mel_discard_before", "vox_hip_mel_read", "vox_hip_mel_free",
+    "vox_hip_mel_frame_ptr", "vox_hip_mel_discard_before", "vox_hip_mel_read", "vox_hip_mel_free", "vox_hip_mel_reset",
 ]
 
 _lib = None
@@ -111,7 +111,7 @@ def lib():
         "vox_hip_mel_create": (P, [P, I]), "vox_hip_mel_feed": (I, [P, fp, I]),
         "vox_hip_mel_finish": (I, [P, I]), "vox_hip_mel_frames": (I, [P, ip]),
         "vox_hip_mel_frame_ptr": (P, [P, I]), "vox_hip_mel_discard_before": (I, [P, I]),
-        "vox_hip_mel_read": (I, [P, I, I, fp]), "vox_hip_mel_free": (None, [P]),
+        "vox_hip_mel_read": (I, [P, I, I, fp]), "vox_hip_mel_free": (None, [P]), "vox_hip_mel_reset": (I, [P, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -662,7 +662,7 @@ def host_lib():
     ip = ctypes.POINTER(ctypes.c_int)
     sig = {
         "vh_ctx_wrap": (P, [P, P, I]), "vh_free": (None, [P]), "vh_last_error": (ctypes.c_char_p, []),
-        "vh_stream_init": (P, [P]), "vh_stream_free": (None, [P]),
+        "vh_stream_init": (P, [P]), "vh_stream_free": (None, [P]), "vh_stream_reset": (I, [P]),
         "vh_set_processing_interval": (None, [P, F]), "vh_stream_set_continuous": (None, [P, I]),
         "vh_stream_feed": (I, [P, ctypes.POINTER(ctypes.c_float), I]), "vh_stream_flush": (I, [P]),
         "vh_stream_finish": (I, [P]), "vh_stream_get": (I, [P, ip, I]),
@@ -723,6 +723,11 @@ class HostStream:
     def finish(self):
         if host_lib().vh_stream_finish(self.h) != 0:
             _herr("vh_stream_finish")
+
+    def reset(self):
+        """vh_stream_reset: new audio on this (detached) stream, its buffers and settings kept"""
+        if host_lib().vh_stream_reset(self.h) != 0:
+            _herr("vh_stream_reset")
 
     def get(self) -> list[int]:
         out, buf = [], np.empty(4096, np.int32)

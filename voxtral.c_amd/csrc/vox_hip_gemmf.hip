@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
 // ---------------------------------------------------------------------------
 static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
-int g_gemmf_rb = 0;      // tools/kbench knob: row blocks per tile with two planes (0 = by shape; 4 or 8)
+int g_gemmf_rb = -1;     // row blocks per tile with two planes (0 = by shape; 4 or 8; -1: VOX_HIP_GEMMF_RB once)
 int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
 // waves per block with two planes: 16 (4 row shares of a 128- or 64-row tile: 32 x 32 or 16 x
 // 32 per wave, four waves per SIMD) by default, 8 with VOX_HIP_GEMMF_WR=2 (64 x 32 per wave,
@@ -434,6 +434,13 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     // three planes would not fit the 160 KB of LDS); 16 waves with two planes (g_gemmf_wr),
     // 8 with three
     constexpr int NG = 2, WR = 2;
+    if (g_gemmf_rb < 0) {
+        // VOX_HIP_GEMMF_RB=4: 64-row tiles on every shape (a 96 KB LDS ring instead of 144 KB,
+        // which leaves room on a CU for kernels running beside an encoder pass)
+        const char* e = getenv("VOX_HIP_GEMMF_RB");
+        const int v = e ? atoi(e) : 0;
+        g_gemmf_rb = (v == 4 || v == 8) ? v : 0;
+    }
     if (!gemmf_ok(M, N, K) || (np != 2 && np != 3) || !ws || !flags || (g_gemmf_rb && g_gemmf_rb != 4 && g_gemmf_rb != 8))
         return hipErrorInvalidValue;
     // two planes: 128-row tiles while they alone give every CU a tile; narrower outputs (the

@@ -1808,7 +1808,10 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
 // (their slots hold older, finite values or zeros).  Grid: one block per query head, the 4
 // heads of a kv head on one XCD (blocks y, y + 8, ..: the K/V rows go through one L2).
 // ============================================================================
-template <int HD, class KT = float>
+// LATE: waves 8..15 (keys 128..255) read the position first and load only the keys inside
+// the context, so a context of <= 128 keys moves half the K/V bytes through the CU; waves
+// 0..7 keep the speculative loads
+template <int HD, class KT = float, int LATE = 0>
 __global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q, const KT* __restrict__ Kc,
                                                      const KT* __restrict__ Vc, const int* __restrict__ state,
                                                      int pos_host, float scale, int H, int KVH,
@@ -1824,12 +1827,21 @@ __global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q
     const int r = lane >> 3, c = lane & 7;
     // K: load i covers keys r + 8 (i & 1), quarter row i >> 1 (8 whole lines per instruction)
     float4 kv[DQ / 4];
-#pragma unroll
-    for (int i = 0; i < DQ / 4; i++)
-        kv[i] = kv_ld4(Kc + (size_t)(k0 + r + 8 * (i & 1)) * kvd + kvh * HD + (i >> 1) * DQ + c * 4);
     float2 vv[ATT_CH];
+    int kpre = ATT_CH;
+    if (LATE && wave >= 8) kpre = min(ATT_CH, (state ? state[0] : pos_host) + 1 - k0);  // wave-uniform
+    if (kpre > 0) {
 #pragma unroll
-    for (int k = 0; k < ATT_CH; k++) vv[k] = kv_ld2(Vc + (size_t)(k0 + k) * kvd + kvh * HD + lane * DPL);
+        for (int i = 0; i < DQ / 4; i++)
+            kv[i] = kv_ld4(Kc + (size_t)(k0 + r + 8 * (i & 1)) * kvd + kvh * HD + (i >> 1) * DQ + c * 4);
+#pragma unroll
+        for (int k = 0; k < ATT_CH; k++) vv[k] = kv_ld2(Vc + (size_t)(k0 + k) * kvd + kvh * HD + lane * DPL);
+    } else {
+#pragma unroll
+        for (int i = 0; i < DQ / 4; i++) kv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < ATT_CH; k++) vv[k] = make_float2(0.f, 0.f);
+    }
     float4 qv[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) qv[j] = *reinterpret_cast<const float4*>(q + (size_t)h * HD + j * DQ + c * 4);
@@ -3677,12 +3689,17 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
 // splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
 // step the launch serves); 1 -> one block per query head, no combine kernel.
 int g_attn_short = -1;  // k_attn_short for one stream's contexts <= 256 keys (VOX_HIP_ATT_SHORT=0: off)
+int g_attn_late = -1;   // its keys 128..255 loaded after the position read (VOX_HIP_ATT_SHORT_LATE=1)
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
                               int KVH, float* part, float* out, int splits, hipStream_t st, int kv16) {
     if (g_attn_short < 0) {
         const char* e = getenv("VOX_HIP_ATT_SHORT");
         g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    if (g_attn_late < 0) {
+        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");
+        g_attn_late = (e && atoi(e) == 1) ? 1 : 0;
     }
     if (g_attn_short && splits == 1 && hd == 128 && window > ATT_BK && cap >= ATT_BK && H % KVH == 0) {
         // contexts of <= 256 keys (splits == 1) with a window of > 256: nothing has left the
@@ -3691,6 +3708,9 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
         if (kv16)
             hipLaunchKernelGGL((k_attn_short<128, kvh_t>), dim3(H), dim3(1024), 0, st, q,
                                reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
+                               scale, H, KVH, out);
+        else if (g_attn_late)
+            hipLaunchKernelGGL((k_attn_short<128, float, 1>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
                                scale, H, KVH, out);
         else
             hipLaunchKernelGGL((k_attn_short<128, float>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host, scale,

@@ -1808,9 +1808,9 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
 // (their slots hold older, finite values or zeros).  Grid: one block per query head, the 4
 // heads of a kv head on one XCD (blocks y, y + 8, ..: the K/V rows go through one L2).
 // ============================================================================
-// LATE: waves 8..15 (keys 128..255) read the position first and load only the keys inside
-// the context, so a context of <= 128 keys moves half the K/V bytes through the CU; waves
-// 0..7 keep the speculative loads
+// LATE = w > 0: waves w..15 (keys 16 w..255) read the position first and load only the keys
+// inside the context (w = 8: a context of <= 128 keys moves half the K/V bytes through the
+// CU); waves 0..w-1 keep the speculative loads
 template <int HD, class KT = float, int LATE = 0>
 __global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q, const KT* __restrict__ Kc,
                                                      const KT* __restrict__ Vc, const int* __restrict__ state,
@@ -1829,7 +1829,7 @@ __global__ __launch_bounds__(1024) void k_attn_short(const float* __restrict__ q
     float4 kv[DQ / 4];
     float2 vv[ATT_CH];
     int kpre = ATT_CH;
-    if (LATE && wave >= 8) kpre = min(ATT_CH, (state ? state[0] : pos_host) + 1 - k0);  // wave-uniform
+    if (LATE && wave >= LATE) kpre = min(ATT_CH, (state ? state[0] : pos_host) + 1 - k0);  // wave-uniform
     if (kpre > 0) {
 #pragma unroll
         for (int i = 0; i < DQ / 4; i++)
@@ -3701,23 +3701,26 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
         g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
     }
     if (g_attn_late < 0) {
-        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");
-        g_attn_late = (e && atoi(e) == 0) ? 0 : 1;
+        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");  // 0: off; 4: from wave 4 on; else 8
+        g_attn_late = !e ? 8 : atoi(e) == 0 ? 0 : atoi(e) == 4 ? 4 : 8;
     }
     if (g_attn_short && splits == 1 && hd == 128 && window > ATT_BK && cap >= ATT_BK && H % KVH == 0) {
         // contexts of <= 256 keys (splits == 1) with a window of > 256: nothing has left the
         // window (lp < 256 < window) and the ring has not wrapped, so keys = slots 0..lp (a
         // window of exactly 256 would reach L = 256 again at lp >= 256 with wrapped slots)
         if (kv16 && g_attn_late)
-            hipLaunchKernelGGL((k_attn_short<128, kvh_t, 1>), dim3(H), dim3(1024), 0, st, q,
+            hipLaunchKernelGGL((k_attn_short<128, kvh_t, 8>), dim3(H), dim3(1024), 0, st, q,
                                reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
                                scale, H, KVH, out);
         else if (kv16)
             hipLaunchKernelGGL((k_attn_short<128, kvh_t>), dim3(H), dim3(1024), 0, st, q,
                                reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
                                scale, H, KVH, out);
+        else if (g_attn_late == 4)
+            hipLaunchKernelGGL((k_attn_short<128, float, 4>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
+                               scale, H, KVH, out);
         else if (g_attn_late)
-            hipLaunchKernelGGL((k_attn_short<128, float, 1>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
+            hipLaunchKernelGGL((k_attn_short<128, float, 8>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
                                scale, H, KVH, out);
         else
             hipLaunchKernelGGL((k_attn_short<128, float>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host, scale,

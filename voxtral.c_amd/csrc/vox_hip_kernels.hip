@@ -3689,9 +3689,10 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
 // splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
 // step the launch serves); 1 -> one block per query head, no combine kernel.
 int g_attn_short = -1;  // k_attn_short for one stream's contexts <= 256 keys (VOX_HIP_ATT_SHORT=0: off)
-// k_attn_short's keys 128..255 loaded after the position read (VOX_HIP_ATT_SHORT_LATE=0: all
-// 256 speculative): C2 655.3 / 655.4 / 655.7 -> 663.7 / 667.7 / 666.7 tok/s on one box
-// (profiles/r4_attn_short_late_ab.txt) -- contexts <= 128 keys move half the K/V bytes
+// k_attn_short's keys 64..255 loaded after the position read (VOX_HIP_ATT_SHORT_LATE=8: keys
+// 128..255; =0: all 256 speculative).  C2 on one box: all speculative 655.3 / 655.4 / 655.7,
+// from wave 8 663.7 / 667.7 / 666.7 tok/s; on another, from wave 8 672.3 / 670.7 / 673.2,
+// from wave 4 676.6 / 676.7 / 676.2 (profiles/r4_attn_short_late_ab.txt)
 int g_attn_late = -1;
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
@@ -3701,15 +3702,15 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
         g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
     }
     if (g_attn_late < 0) {
-        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");  // 0: off; 4: from wave 4 on; else 8
-        g_attn_late = !e ? 8 : atoi(e) == 0 ? 0 : atoi(e) == 4 ? 4 : 8;
+        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");  // 0: off; 8: from wave 8 on; else 4
+        g_attn_late = !e ? 4 : atoi(e) == 0 ? 0 : atoi(e) == 8 ? 8 : 4;
     }
     if (g_attn_short && splits == 1 && hd == 128 && window > ATT_BK && cap >= ATT_BK && H % KVH == 0) {
         // contexts of <= 256 keys (splits == 1) with a window of > 256: nothing has left the
         // window (lp < 256 < window) and the ring has not wrapped, so keys = slots 0..lp (a
         // window of exactly 256 would reach L = 256 again at lp >= 256 with wrapped slots)
         if (kv16 && g_attn_late)
-            hipLaunchKernelGGL((k_attn_short<128, kvh_t, 8>), dim3(H), dim3(1024), 0, st, q,
+            hipLaunchKernelGGL((k_attn_short<128, kvh_t, 4>), dim3(H), dim3(1024), 0, st, q,
                                reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
                                scale, H, KVH, out);
         else if (kv16)

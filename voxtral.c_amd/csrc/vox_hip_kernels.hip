@@ -3702,8 +3702,9 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
         g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
     }
     if (g_attn_late < 0) {
-        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");  // 0: off; 8: from wave 8 on; else 4
-        g_attn_late = !e ? 4 : atoi(e) == 0 ? 0 : atoi(e) == 8 ? 8 : 4;
+        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");  // 0: off; 8 / 2: from wave 8 / 2 on; else 4
+        const int v = e ? atoi(e) : 4;
+        g_attn_late = (v == 0 || v == 2 || v == 8) ? v : 4;
     }
     if (g_attn_short && splits == 1 && hd == 128 && window > ATT_BK && cap >= ATT_BK && H % KVH == 0) {
         // contexts of <= 256 keys (splits == 1) with a window of > 256: nothing has left the
@@ -3719,6 +3720,9 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
                                scale, H, KVH, out);
         else if (g_attn_late == 4)
             hipLaunchKernelGGL((k_attn_short<128, float, 4>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
+                               scale, H, KVH, out);
+        else if (g_attn_late == 2)
+            hipLaunchKernelGGL((k_attn_short<128, float, 2>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
                                scale, H, KVH, out);
         else if (g_attn_late)
             hipLaunchKernelGGL((k_attn_short<128, float, 8>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,

@@ -107,9 +107,9 @@ int vox_hip_model_ada_scale(vox_hip_model_t *m, float *out);
 int vox_hip_model_set_kv_fp16(vox_hip_model_t *m, int on);
 /* Arithmetic of the M > 1 GEMMs (encoder, adapter, prefill; no reference counterpart: the
  * CPU path's cblas_sgemm, voxtral_kernels.c:197-240, is f32): every f32 activation is split
- * into bf16 planes that multiply the exact bf16 weights on MFMA.  planes = 3 (hi + mid + lo)
- * reproduces the f32 activation exactly (only the summation order differs from sgemm);
- * planes = 2 (the default, or VOX_HIP_GEMM_PLANES) keeps ~2^-18 of it and issues 2/3 of the
+ * into bf16 planes that multiply the exact bf16 weights on MFMA.  planes = 3 (hi + mid + lo,
+ * the default) reproduces the f32 activation exactly (only the summation order differs from
+ * sgemm); planes = 2 (or VOX_HIP_GEMM_PLANES=2) keeps ~2^-18 of it and issues 2/3 of the
  * MFMAs (measured against the 5e-5 parity bar in tests/test_gpu_gemm_planes.py).
  * Process-wide; returns 0, or -1 for another value. */
 int vox_hip_set_gemm_planes(int planes);

@@ -1,11 +1,11 @@
-"""k_gemm2's activation planes (csrc/vox_hip_kernels.hip, gemm_planes): the default two bf16
-planes (hi + lo, ~2^-18 relative per activation) and the exact three-plane split
-(VOX_HIP_GEMM_PLANES=3, hi + mid + lo = the f32 value, so only summation order differs from
-the reference's sgemm, voxtral_kernels.c:197-240).  The switch is read once per process, so
+"""The M > 1 GEMMs' activation planes (csrc/vox_hip_kernels.hip, gemm_planes): the default
+exact three-plane split (hi + mid + lo = the f32 value, so only summation order differs from
+the reference's sgemm, voxtral_kernels.c:197-240) and the approximate two-plane split
+(VOX_HIP_GEMM_PLANES=2: hi + lo, ~2^-18 relative per activation).  The switch is read once per process, so
 each mode runs in a child process: the sgemm twin at encoder / prefill shapes against an f64
 statement of the same product, and the TINY jfk transcription against the oracle.  Bars:
-identical ids; 5e-5 of the largest magnitude for the default, 2e-6 (sgemm) and 1e-5
-(pipeline) for the exact split."""
+identical ids; 2e-6 (sgemm) and 1e-5 (pipeline) for the exact default, 5e-5 of the largest
+magnitude for the two-plane split."""
 import os
 import subprocess
 import sys

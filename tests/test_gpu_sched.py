@@ -109,6 +109,48 @@ def test_scheduler_step_cap_spreads_bursts(tiny_weights, jfk_samples):
     om.close()
 
 
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_scheduler_finish_then_one_run_drains(tiny_weights, jfk_samples, monkeypatch, overlap):
+    """without a step cap one vh_sched_run drains every stream, including the rows
+    of the chunk vh_stream_finish queued for that run's encoder pass (with the pass beside
+    the steps, VOX_HIP_SCHED_OVERLAP=1, and sequentially): feed everything, finish, run once,
+    and every stream's ids equal its oracle session with nothing pending."""
+    import vox_hip
+    from vox_weights import TINY_LONG
+    monkeypatch.setenv("VOX_HIP_SCHED_OVERLAP", overlap)
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    import vox_oracle
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    audios = [np.ascontiguousarray(jfk_samples[:int(s * 16000)]) for s in (3.0, 6.5)]
+    ctx = vox_hip.HostCtx(hm)
+    q = vox_hip.Scheduler(ctx, 4)
+    ss = [vox_hip.HostStream(ctx, interval_s=0.5) for _ in audios]
+    for s in ss:
+        q.attach(s)
+    ids = [[] for _ in audios]
+    for a, s in zip(audios, ss):
+        for i in range(0, len(a), PIECE):
+            s.feed(a[i:i + PIECE])
+    q.run()
+    for k, s in enumerate(ss):
+        ids[k] += s.get()
+    for s in ss:
+        s.finish()
+    q.run()   # exactly one run after finish
+    for k, s in enumerate(ss):
+        ids[k] += s.get()
+        assert s.pending() == 0
+    for k, a in enumerate(audios):
+        ref, _ = _oracle_ids(om, a, 0.5)
+        assert ids[k] == ref, (k, len(ids[k]), len(ref))
+    for s in ss:
+        s.close()
+    q.close()
+    ctx.close()
+    hm.close()
+    om.close()
+
+
 def test_scheduler_continuous_restarts_per_stream(tiny_weights, jfk_samples):
     """Live mode (vh_stream_set_continuous) on two scheduled streams of 88 s: each stream's
     restarts (64-token non-text streaks on the random TINY model, voxtral.c:1189-1239) stay

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_qt, g_attn_valu, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -111,7 +111,6 @@ int main(int argc, char** argv) {
         }
     }
     int layer = 0;
-    int* kb_drain = nullptr;  // VOX_KB_ONLY=drain: dynamic row-group claims (k_gemv a.drain)
     float* wsc = (float*)dmalloc((size_t)V * 4, 1);  // Q8 row scales (any finite values)
     const float* qs = nullptr;  // set: the weight buffers are read as int8 rows
     auto gemv = [&](int pro, int epi, const uint16_t* W, int K, int rows) {
@@ -119,7 +118,7 @@ int main(int argc, char** argv) {
         memset(&a, 0, sizeof a);
         a.x = x; a.K = K; a.W = W; a.wscale = qs; a.rows = rows; a.norm_w = normw; a.ada = ada; a.eps = 1e-5f;
         a.y = y; a.qd = DQ; a.kvd = DKV; a.hd = HD; a.rope = rope; a.state = state; a.Kc = Kc; a.Vc = Vc;
-        a.cap = cap; a.part_val = pv; a.part_idx = pi; a.drain = kb_drain;
+        a.cap = cap; a.part_val = pv; a.part_idx = pi;
         CK(launch_gemv(pro, epi, a, st));
     };
     struct R { const char* name; double us; double bytes; };
@@ -154,37 +153,6 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL(k_touch_rows, dim3(G), dim3(256), 0, st, (*o.w)[layer++ % NL], o.K * 2, o.rb, sw, sink);
                 }, iters, st), (double)G * o.rb * o.K * 2);
         }
-        return 0;
-    }
-    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "drain")) {
-        // decode GEMVs: the static block -> row-group map against dynamic claims past each
-        // block's first two groups (a.drain), bf16 and Q8, 26 rotating layers (cold weights)
-        int* dr = (int*)dmalloc(GEMV_DRAIN_INTS * 4, 0);
-        struct O { const char* n; int pro, epi, K, rows, q8; std::vector<uint16_t*>* w; };
-        for (O o : {O{"qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 0, &wqkv}, O{"wo", PRO_NONE, EPI_RESID, DQ, D, 0, &wo},
-                    O{"w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 0, &w13}, O{"w2", PRO_NONE, EPI_RESID, DH, D, 0, &w2},
-                    O{"q8 qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 1, &wqkv}, O{"q8 wo", PRO_NONE, EPI_RESID, DQ, D, 1, &wo},
-                    O{"q8 w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 1, &w13}, O{"q8 w2", PRO_NONE, EPI_RESID, DH, D, 1, &w2}})
-            for (int dyn : {0, 1, 0, 1}) {
-                kb_drain = dyn ? dr : nullptr;
-                qs = o.q8 ? wsc : nullptr;
-                char nm[96];
-                snprintf(nm, sizeof nm, "gemv %-6s %s (grid %4d)", o.n, dyn ? "claims" : "static", gemv_grid(o.rows));
-                add(nm, timeit([&] { gemv(o.pro, o.epi, (*o.w)[layer++ % NL], o.K, o.rows); }, iters, st),
-                    (double)o.rows * o.K * (o.q8 ? 1 : 2));
-            }
-        for (int dyn : {0, 1, 0, 1}) {
-            kb_drain = dyn ? dr : nullptr;
-            qs = nullptr;
-            char nm[96];
-            snprintf(nm, sizeof nm, "gemv lm     %s (grid %4d)", dyn ? "claims" : "static", gemv_grid(V));
-            add(nm, timeit([&] { gemv(PRO_NORM, EPI_LOGITS, emb, D, V); }, iters / 4, st), (double)V * D * 2);
-        }
-        int h[2];
-        CK(hipMemcpy(h, dr, 8, hipMemcpyDeviceToHost));
-        printf("drain counters after the runs (must be 0 0): %d %d\n", h[0], h[1]);
-        kb_drain = nullptr;
-        qs = nullptr;
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "grid")) {
@@ -453,46 +421,6 @@ int main(int argc, char** argv) {
             }
             CK(hipFree(stamps));
         }
-        // attention + wo at 16 streams: the attention's merging block + k_skl over the planes
-        // against partials only + k_skl_attn (the wo prologue merges them)
-        {
-            float* wpart = (float*)dmalloc((size_t)8 * 16 * D * 4, 0);
-            const int maxs = attn_maxch(8192);
-            std::vector<BatchSlot> hsl(16);
-            for (int L : {64, 128, 190, 256, 400, 512}) {
-                memset(hsl.data(), 0, sizeof(BatchSlot) * 16);
-                for (int z = 0; z < 16; z++) {
-                    hsl[z].state = states + z * 4;
-                    hsl[z].Kc = reinterpret_cast<char*>(Ks[z * 2]);
-                    hsl[z].Vc = reinterpret_cast<char*>(Vs[z * 2]);
-                    hsl[z].live = 1;
-                    hsl[z].pos = L - 1;
-                }
-                CK(hipMemcpy(slots, hsl.data(), sizeof(BatchSlot) * 16, hipMemcpyHostToDevice));
-                const int splits = L > 256 ? 2 : 1;
-                for (int wm : {0, 1}) {
-                    int l = 0;
-                    char nm[96];
-                    snprintf(nm, sizeof nm, "attn+wo nb=16 L=%d %s", L, wm ? "wo merges" : "attn merges");
-                    add(nm, timeit([&] {
-                            AttnPtrs p;
-                            memset(&p, 0, sizeof p);
-                            p.slots = slots;
-                            p.ring_off = (size_t)(l % 13) * rcap * DKV * 4;
-                            for (int z = 0; z < 16; z++) p.part[z] = parts + (size_t)z * (H * 128 * (HD + 2) + 1024);
-                            AttnFuse f{slabs, S6, N, rope, xs};
-                            f.wom = wm;
-                            CK(launch_attn_batch_fused(HD, p, f, 16, rcap, 8192, 0.088f, H, KVH, splits, st, 0));
-                            if (wm)
-                                CK(launch_gemm_skl_attn(parts, (size_t)H * 128 * (HD + 2) + 1024, maxs, 2 * splits, DQ,
-                                                        wo[l % NL], nullptr, D, 16, wpart, st));
-                            else
-                                CK(launch_gemm_skl(xs, DQ, wo[l % NL], nullptr, D, 16, wpart, st));
-                            l++;
-                        }, iters, st), (double)16 * L * DKV * 2 * 4 + (double)D * DQ * 2);
-                }
-            }
-        }
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "attn")) {
@@ -710,40 +638,25 @@ int main(int argc, char** argv) {
         float* ews = (float*)dmalloc(wsn * 4, 0);
         uint16_t* exs = (uint16_t*)dmalloc((size_t)2 * 3 * 16 * EQ * 2, 0);
         char nm0[64];
-        for (int qt : {0, 16, 32}) {
-            // 0: k_attn_mf (MFMA, 16 queries); 16 / 32: the VALU k_attn_tiled
-            g_attn_valu = qt != 0;
-            g_attn_qt = qt ? qt : 16;
-            for (int q0 : {750, 2000}) {
-                snprintf(nm0, sizeof nm0, "attn tiled enc M=25 q0=%d QT=%d", q0, qt);
-                add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, q0, 0, 750, 0.125f, st, ews, wsn)); }, iters, st),
-                    (double)std::min(q0 + M, 750 + M - 1) * EQ * 2 * 4);
-            }
-            snprintf(nm0, sizeof nm0, "attn tiled enc M=25 QT=%d -> planes", qt);
-            add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, 2000, 0, 750, 0.125f, st, ews, wsn, exs)); }, iters, st),
-                (double)(750 + M - 1) * EQ * 2 * 4);
+        for (int q0 : {750, 2000}) {
+            snprintf(nm0, sizeof nm0, "attn mf enc M=25 q0=%d", q0);
+            add(nm0, timeit([&] { CK(launch_attn_rows_mf(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, q0, 0, 750, 0.125f, st, ews, wsn)); }, iters, st),
+                (double)std::min(q0 + M, 750 + M - 1) * EQ * 2 * 4);
         }
-        g_attn_qt = 0;
-        g_attn_valu = 0;
         for (int nbk : {128, 256, 1024}) {
             g_attn_blocks = nbk;
             snprintf(nm0, sizeof nm0, "attn mf enc M=25 -> planes, ~%d blocks", nbk);
-            add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, 2000, 0, 750, 0.125f, st, ews, wsn, exs)); }, iters, st),
+            add(nm0, timeit([&] { CK(launch_attn_rows_mf(EHd, eq, EQ, Kc, Vc, ecap, eo, EQ, M, EH, EH, 2000, 0, 750, 0.125f, st, ews, wsn, exs)); }, iters, st),
                 (double)(750 + M - 1) * EQ * 2 * 4);
         }
         g_attn_blocks = 0;
-        // one-shot encoder pass (jfk: 677 rows, keys from 0): MFMA vs VALU
+        // one-shot encoder pass (jfk: 677 rows, keys from 0)
         {
             const int M1 = 677;
             float* q1 = (float*)dmalloc((size_t)M1 * EQ * 4, 1);
             float* o1 = (float*)dmalloc((size_t)M1 * EQ * 4, 0);
-            for (int valu : {0, 1}) {
-                g_attn_valu = valu;
-                snprintf(nm0, sizeof nm0, "attn tiled enc M=677 %s", valu ? "VALU" : "MFMA");
-                add(nm0, timeit([&] { CK(launch_attn_tiled(EHd, q1, EQ, Kc, Vc, ecap, o1, EQ, M1, EH, EH, 0, 0, 750, 0.125f, st, ews, wsn)); }, iters / 4 + 1, st),
-                    (double)M1 * EQ * 2 * 4);
-            }
-            g_attn_valu = 0;
+            add("attn mf enc M=677", timeit([&] { CK(launch_attn_rows_mf(EHd, q1, EQ, Kc, Vc, ecap, o1, EQ, M1, EH, EH, 0, 0, 750, 0.125f, st, ews, wsn)); }, iters / 4 + 1, st),
+                (double)M1 * EQ * 2 * 4);
         }
     }
     {

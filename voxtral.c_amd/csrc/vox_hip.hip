@@ -517,7 +517,6 @@ struct vox_hip_stream {
     int graph_rope_gen;      // model rope table generation the step graphs were captured with
     int *pidx, *state, *tokens;   // tokens: ring of tokens_cap ids, index = step % tokens_cap
     int* twin_state;              // decoder_full_step's argmax state (the graph state stays untouched)
-    int* gdrain;                  // k_gemv row-group claim + done counters (self-resetting)
     int dec_rows_cap, tokens_cap;
     hipGraphExec_t step_exec[STEP_GRAPHS];  // [g]: attention with 2^g key splits (g = 0: no combine)
     int graph_ready;              // bit mask of built graphs
@@ -627,7 +626,6 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     TRYH(dalloc(&s->pidx, GEMV_MAX_BLOCKS));
     TRYH(dalloc(&s->state, 4));
     TRYH(dalloc(&s->twin_state, 4));
-    TRYH(dalloc(&s->gdrain, GEMV_DRAIN_INTS));
     s->tokens_cap = TOKENS_CAP;
     TRYH(dalloc(&s->tokens, s->tokens_cap));
     TRYH(dalloc(&s->alts, (size_t)s->tokens_cap * ALT_REC));
@@ -662,7 +660,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->im2col); dfree(s->x_enc); dfree(s->xn); dfree(s->qkv); dfree(s->q); dfree(s->att);
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
-    dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->gdrain); dfree(s->tokens);
+    dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
     dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch); dfree(s->abatch); dfree(s->abatch_out);
     dfree(s->gpa); dfree(s->gpc); dfree(s->gflags);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
@@ -1049,7 +1047,7 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
             q.Kc = Kc;
             q.Vc = Vc;
             CK(launch_gemm_sklx(l ? SKX_PRO_SCALE : SKX_PRO_PLANES, SKX_EPI_QKV, xa, ED, F.wqkv, NQKV, n, q, st));
-            CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale,
+            CK(launch_attn_rows_mf(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale,
                                  st, s->gws, s->gws_n, xq));
             // wo + bias residual (encoder.c:640-644); the FFN norm's planes and row sums of squares
             SklFused o = f;
@@ -1091,7 +1089,7 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
         // QKV slabs + biases -> RoPE -> K/V append (one pass), attention with its output
         // merged straight into the wo planes
         CK(launch_slabs_rope_kv(sl, skl_splits(ED), n, L.bqkv, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
-        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
+        CK(launch_attn_rows_mf(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
                              s->gws, s->gws_n, xp));
         CK(launch_gemm_skl(xp, EQ, F.wo, L.so, ED, n, sl, st));
         // wo residual (+ bias) then the FFN RMSNorm -> planes (encoder.c:640-650)
@@ -1163,7 +1161,7 @@ static int run_encoder_rows_gemmf(vox_hip_stream_t* s, float* x, int n, long lon
         if (gemmf(s, EPI_STORE, s->gpa, ED, n, F.wqkv, NQKV, L.bqkv, s->qkv, NQKV, nullptr)) return -1;
         CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
         // windowed attention, output as the wo input planes (encoder.c:609-638)
-        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
+        CK(launch_attn_rows_mf(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
                              s->gws, s->gws_n, s->gpa));
         // wo + bias residual (encoder.c:640-644)
         if (gemmf(s, EPI_RESID, s->gpa, EQ, n, F.wo, ED, L.bo, x, ED, nullptr)) return -1;
@@ -1202,7 +1200,7 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.attn_norm, nullptr, n, ED, c.enc_eps, st));
         CK(launch_gemm(EPI_STORE, 3, s->xn, ED, L.wqkv, L.sqkv, ED, n, EQ + 2 * EKV, L.bqkv, s->qkv, EQ + 2 * EKV, st, s->gws, s->gws_n));
         CK(launch_rope_kv(s->qkv, n, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
-        CK(launch_attn_tiled(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
+        CK(launch_attn_rows_mf(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
                              s->gws, s->gws_n));
         CK(launch_gemm(EPI_RESID, 3, s->att, EQ, L.wo, L.so, EQ, n, ED, L.bo, x, ED, st, s->gws, s->gws_n));
         CK(launch_rmsnorm_rows(x, ED, s->xn, ED, L.ffn_norm, nullptr, n, ED, c.enc_eps, st));
@@ -1327,6 +1325,16 @@ static int enc_suffix_batch(vox_hip_stream_t* lead, const float* X, vox_hip_stre
     }
     std::vector<int> aoff(B, 0), n4v(B, 0);
     int NA = 0;  // stacked adapter rows
+    // the stacked rows are bounded before any copy is queued; every adapter buffer was sized
+    // before the pass was enqueued (vox_hip_stream_encode_mel_batch), so nothing here waits on a queue
+    for (int b = 0; b < B; b++)
+        if (T1[b] > 0) {
+            const int tot = ss[b]->enc_res_count + T1[b];
+            if (ss[b]->total_adapter + tot / 4 > ss[b]->adapter_cap) return set_err("enc_suffix_batch: adapter buffer");
+            NA += tot / 4;
+        }
+    if ((size_t)NA * 4 > ain_rows) return set_err("enc_suffix_batch: %d adapter rows", NA);
+    NA = 0;
     for (int b = 0; b < B; b++) {
         added[b] = 0;
         if (T1[b] <= 0) continue;
@@ -1335,7 +1343,6 @@ static int enc_suffix_batch(vox_hip_stream_t* lead, const float* X, vox_hip_stre
         const int R = s->enc_res_count, tot = R + T1[b], usable = (tot / 4) * 4, left = tot - usable;
         const float* xb = X + (size_t)off[b] * ED;
         if (usable > 0) {
-            if (stream_alloc_adapter(s, s->total_adapter + usable / 4)) return -1;
             float* dst = lead->abatch + (size_t)NA * 4 * ED;
             if (R) CK(hipMemcpyAsync(dst, s->enc_res, (size_t)R * ED * 4, hipMemcpyDeviceToDevice, st));
             CK(hipMemcpyAsync(dst + (size_t)R * ED, xb, (size_t)(usable - R) * ED * 4, hipMemcpyDeviceToDevice, st));
@@ -1350,7 +1357,6 @@ static int enc_suffix_batch(vox_hip_stream_t* lead, const float* X, vox_hip_stre
         }
         s->enc_res_count = left;
     }
-    if ((size_t)NA * 4 > ain_rows) return set_err("enc_suffix_batch: %d adapter rows", NA);
     for (int r0 = 0; r0 < NA; r0 += ENC_SUB / 4) {
         const int nr = std::min(ENC_SUB / 4, NA - r0);
         CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, lead->abatch + (size_t)r0 * 4 * ED, 4 * ED, m->ad0,
@@ -1498,6 +1504,11 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
             if (T1[b] > 0)
                 CK(hipMemcpyAsync(lead->xbatch + (size_t)off[b] * ED, xin[b], (size_t)T1[b] * ED * 4,
                                   hipMemcpyDeviceToDevice, lead->st));
+        // adapter buffers sized now, before the pass is on the lead's queue: growing one later
+        // (stream_alloc_adapter synchronises the stream's queue) would wait for the whole pass
+        for (int b = 0; b < B; b++)
+            if (T1[b] > 0 && stream_alloc_adapter(ss[b], ss[b]->total_adapter + (ss[b]->enc_res_count + T1[b]) / 4))
+                return -1;
         if (run_encoder_rows_batch(lead, lead->xbatch, N, ss, off.data(), T1.data(), pos0.data(), B)) return -1;
         // downsample + adapter of every stream in one pass on the lead's queue; the members'
         // queues then wait for it
@@ -1583,7 +1594,7 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.attn_norm, nullptr, n, DD, c.dec_eps, st));
         CK(launch_gemm(EPI_STORE, 3, s->xnd, DD, L.wqkv, L.sqkv, DD, n, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, st, s->gws, s->gws_n));
         CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st, s->kv16));
-        CK(launch_attn_tiled(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st,
+        CK(launch_attn_rows_mf(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale, st,
                              s->gws, s->gws_n, nullptr, s->kv16));
         CK(launch_gemm(EPI_RESID, 3, s->attd, DQ, L.wo, L.so, DQ, n, DD, nullptr, x, DD, st, s->gws, s->gws_n));
         CK(launch_rmsnorm_rows(x, DD, s->xnd, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, n, DD, c.dec_eps, st));
@@ -1598,17 +1609,6 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
 // otherwise pos/rope_row are host values (boundary twin).
 static int enqueue_lm_head(vox_hip_stream_t* s, const int* state);
 
-// decode GEMVs with row groups claimed at run time: opt-in (VOX_HIP_GEMV_DRAIN=1); the
-// static block -> group map is the default (claims measured 3-4x slower)
-static int gemv_drain_env() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("VOX_HIP_GEMV_DRAIN");
-        v = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    return v;
-}
-
 static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row,
                                int splits) {
     vox_hip_model_t* m = s->m;
@@ -1617,7 +1617,6 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
     const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
     const float scale = 1.0f / sqrtf((float)hd);
     hipStream_t st = s->st;
-    int* drain = gemv_drain_env() ? s->gdrain : nullptr;
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         float* Kc = dec_ring(s, s->dk, l);
@@ -1631,7 +1630,6 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         a.state = state; a.pos = pos;
         a.rope = state ? m->rope_dec : rope_row - (size_t)pos * hd;
         a.Kc = Kc; a.Vc = Vc; a.cap = s->dcap; a.kv16 = s->kv16;
-        a.drain = drain;
         CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
         // attention over the last min(pos+1, window) keys (decoder.c:724-733)
         CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
@@ -1639,13 +1637,11 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         // wo + residual (decoder.c:735-740)
         memset(&a, 0, sizeof a);
         a.x = s->attd; a.K = DQ; a.W = L.wo; a.wscale = L.so; a.rows = DD; a.y = s->xd;
-        a.drain = drain;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
         // norm * (1 + ada) -> W1|W3 -> silu * up (decoder.c:742-758)
         memset(&a, 0, sizeof a);
         a.x = s->xd; a.K = DD; a.W = L.w13; a.wscale = L.s13; a.rows = 2 * DH; a.norm_w = L.ffn_norm;
         a.ada = m->ada_scale + (size_t)l * DD; a.eps = c.dec_eps; a.y = s->gated;
-        a.drain = drain;
         // profiling: HIP events recorded by the W1|W3 launch's own dispatch (eager steps)
         const bool gprof = s->profiling && state && !s->capturing && (int)s->pev.size() == 2 * c.dec_layers;
         if (gprof) CK(launch_gemv_timed(PRO_NORM_ADA, EPI_SWIGLU, a, s->pev[2 * l], s->pev[2 * l + 1], st));
@@ -1653,7 +1649,6 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         // W2 + residual (decoder.c:758-760)
         memset(&a, 0, sizeof a);
         a.x = s->gated; a.K = DH; a.W = L.w2; a.wscale = L.s2; a.rows = DD; a.y = s->xd;
-        a.drain = drain;
         CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
     }
     return enqueue_lm_head(s, state);
@@ -1669,7 +1664,6 @@ static int enqueue_lm_head(vox_hip_stream_t* s, const int* state) {
     a.x = s->xd; a.K = c.dec_dim; a.W = m->tok_emb; a.wscale = m->tok_emb_s; a.rows = c.vocab; a.norm_w = m->dec_norm;
     a.eps = c.dec_eps; a.y = s->logits; a.part_val = s->pval; a.part_idx = s->pidx;
     a.part_alt = s->part_alt;
-    a.drain = gemv_drain_env() ? s->gdrain : nullptr;
     CK(launch_gemv(PRO_NORM, (state && s->n_alt > 1) ? EPI_LOGITS_ALT : EPI_LOGITS, a, st));
     return 0;
 }
@@ -2179,7 +2173,7 @@ static int twin_attention(float* out, const float* Q, const float* K, const floa
         if (twin_buf(&g_tWs, &g_tWs_n, wsn)) return -1;
         ws = g_tWs;
     }
-    CK(launch_attn_tiled(head_dim, g_tQ, n_heads * head_dim, g_tK, g_tV, seq_k, g_tO, n_heads * head_dim, seq_q,
+    CK(launch_attn_rows_mf(head_dim, g_tQ, n_heads * head_dim, g_tK, g_tV, seq_k, g_tO, n_heads * head_dim, seq_q,
                          n_heads, n_kv_heads, q_offset, 0, W, scale, g_twin_st, ws, wsn));
     CK(hipMemcpyAsync(out, g_tO, qn * 4, hipMemcpyDeviceToHost, g_twin_st));
     CK(hipStreamSynchronize(g_twin_st));
@@ -2378,8 +2372,9 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
         return nullptr;
     }
     const vox_hip_config_t& c = m->c;
-    if (c.dec_head_dim != 128 || c.dec_heads % c.dec_kv_heads || c.dec_heads / c.dec_kv_heads > 4) {
-        set_err("batched decode needs head_dim 128 and <= 4 query heads per kv head");
+    if (c.dec_head_dim != 128 || c.dec_heads % c.dec_kv_heads || c.dec_heads / c.dec_kv_heads > 4 ||
+        c.dec_dim % 256 || c.dec_dim / 256 > SKL_MAX_SLICES) {
+        set_err("batched decode needs head_dim 128, <= 4 query heads per kv head and dec_dim = 256 k <= 3072");
         return nullptr;
     }
     vox_hip_batch_t* b = new vox_hip_batch_t();
@@ -2456,93 +2451,39 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         ap.out[i] = b->att + (size_t)i * DQ;
     }
     const int Sres = skl_splits(DH);  // slabs the previous layer's w2 left for the residual
-    static int xw_env = -1;
-    if (xw_env < 0) {
-        const char* e = getenv("VOX_HIP_BATCH_XW");
-        xw_env = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    const bool xw = xw_env && DD % 256 == 0 && DD / 256 <= SKL_MAX_SLICES;
-    static int wox = -1;
-    if (wox < 0) {
-        const char* e = getenv("VOX_HIP_BATCH_WOX");
-        wox = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    static int swx = -1;
-    if (swx < 0) {
-        const char* e = getenv("VOX_HIP_BATCH_SWX");
-        swx = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    // VOX_HIP_BATCH_WOM=1, contexts <= 512 keys (<= 4 key-range blocks of 128 per head): the
-    // wo projection merges the attention's partials.  Opt-in: measured no faster than the
-    // attention's own merging block
-    static int wom_env = -1;
-    if (wom_env < 0) {
-        const char* e = getenv("VOX_HIP_BATCH_WOM");
-        wom_env = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    const int maxs = attn_maxch(c.dec_window);
-    const bool wom = wom_env && hd == 128 && 2 * splits <= ATT_WOM_MAX && 2 * splits <= maxs;
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         const DecFragD& F = m->dfrag[l];
         ap.ring_off = (size_t)l * ring_layer;
         // skinny MFMA GEMMs over fragment-major weights: the slots are the 16-column B
         // operand, every weight byte read once per step; each projection leaves split-K slabs
-        // in b->part that the next kernel sums (with the residual for wo / w2)
-        // residual + RMSNorm: slice-parallel rows (x * w planes + slice sums of squares, the
-        // inverse RMS applied by the projection) or one block per row (VOX_HIP_BATCH_XW=0)
-        if (xw) {
-            CK(launch_resid_xw_fplanes(b->x, nb, DD, L.attn_norm, nullptr, b->xp_d, b->part, l ? Sres : 0, nullptr,
-                                       b->ssq, st));
-            CK(batch_gemm(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
-        } else {
-            CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.attn_norm, nullptr, c.dec_eps, b->xp_d, b->part, l ? Sres : 0, st));
-            CK(batch_gemm(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st));
-        }
+        // in b->part that the next kernel sums (with the residual for wo / w2).
+        // residual + RMSNorm as slice-parallel rows: x * w planes + slice sums of squares, the
+        // inverse RMS applied by the projection
+        CK(launch_resid_xw_fplanes(b->x, nb, DD, L.attn_norm, nullptr, b->xp_d, b->part, l ? Sres : 0, nullptr,
+                                   b->ssq, st));
+        CK(batch_gemm(b->xp_d, DD, F.wqkv, L.sqkv, DQ + 2 * DKV, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
         // RoPE + KV append + attention of every live slot, output into the wo planes (one
         // launch; past 256 keys the last key-range block of a kv head merges the partials)
         AttnFuse af;
         af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
-        const bool fuse_wo = xw && swx && wox && !L.so && !L.s13;
-        af.wom = wom && !fuse_wo;
         CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
-        if (af.wom) {
-            // wo with the attention's key-range merge as its prologue (k_skl_attn)
-            CK(launch_gemm_skl_attn(b->apart, b->apart_n, maxs, 2 * splits, DQ, F.wo, L.so, DD, nb, b->part, st));
-        } else if (fuse_wo) {
-            // wo with the residual folded in (k_sklx: the last block of each column slice sums
-            // its slabs into x and writes the slice's x * ffn_norm * (1 + ada) planes and row
-            // sums of squares for W1|W3)
-            SklFused fo;
-            fo.part = b->part; fo.ticket = b->ticket; fo.x = b->x; fo.ssq_out = b->ssq; fo.planes = b->xp_d;
-            fo.nw = L.ffn_norm; fo.ada = m->ada_scale + (size_t)l * DD;
-            CK(launch_gemm_sklx(SKX_PRO_PLANES, SKX_EPI_RESID, b->xp_q, DQ, F.wo, DD, nb, fo, st));
-        } else {
-            CK(batch_gemm(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
-        }
-        if (xw && swx && !L.s13) {
+        CK(batch_gemm(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
+        CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
+                                   skl_splits(DQ), nullptr, b->ssq, st));
+        if (!L.s13) {
             // W1|W3 with the SwiGLU folded in (k_sklx: the last block of each column slice
-            // sums its slabs and writes the w2 planes; no k_swiglu_fplanes launch)
-            if (!fuse_wo)
-                CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
-                                           skl_splits(DQ), nullptr, b->ssq, st));
+            // sums its slabs and writes the w2 planes)
             SklFused f;
-            f.ssq_in = b->ssq; f.nsl = fuse_wo ? sklx_slices(DD, DQ) : DD / 256; f.eps = c.dec_eps;
+            f.ssq_in = b->ssq; f.nsl = DD / 256; f.eps = c.dec_eps;
             f.part = b->part; f.ticket = b->ticket;
             f.planes = b->xp_h;
             CK(launch_gemm_sklx(SKX_PRO_SCALE, SKX_EPI_SWIGLU, b->xp_d, DD, F.w13, 2 * DH, nb, f, st));
-            CK(batch_gemm(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
-            continue;
-        } else if (xw) {
-            CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
-                                       skl_splits(DQ), nullptr, b->ssq, st));
-            CK(batch_gemm(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
         } else {
-            CK(launch_rmsnorm_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, b->xp_d,
-                                      b->part, skl_splits(DQ), st));
-            CK(batch_gemm(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st));
+            // Q8: the int8 projection, then the SwiGLU rows
+            CK(batch_gemm(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
+            CK(launch_swiglu_fplanes(b->part, skl_splits(DD), DH, nb, b->xp_h, st));
         }
-        CK(launch_swiglu_fplanes(b->part, skl_splits(DD), DH, nb, b->xp_h, st));
         CK(batch_gemm(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
     }
     // final norm (after the last w2 residual) + LM head (tied embeddings) + per-slot argmax,

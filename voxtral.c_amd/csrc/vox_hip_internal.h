@@ -14,7 +14,6 @@ constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3
 enum { PRO_NONE = 0, PRO_NORM = 1, PRO_NORM_ADA = 2 };
 
 constexpr int GEMV_MAX_BLOCKS = 1024;  // 4 blocks of 256 threads per CU on 256 CUs
-constexpr int GEMV_DRAIN_INTS = 2 + 64;
 
 struct GemvArgs {
     const float* x;        // input vector [K] (device)
@@ -40,9 +39,6 @@ struct GemvArgs {
     float* part_val;
     int* part_idx;
     float* part_alt;       // EPI_LOGITS_ALT: [blocks][ALT_PART]
-    int* drain = nullptr;  // GEMV_DRAIN_INTS zeroed ints (claim, done -- reset by the last block --, then
-                           // 64 words the claiming wave's other lanes add 0 to): row groups
-                           // claimed dynamically past each block's first two (null: static b + kG)
 };
 
 constexpr int VOX_MAX_BATCH = 16;    // streams per batched decode step
@@ -92,10 +88,6 @@ struct AttnFuse {
     int S, N;              // slab count, row length (H*hd + 2*KVH*hd)
     const float* rope;     // [pos][hd] (cos, sin) table
     uint16_t* xs;          // [3][16][H*hd] fragment-major planes of the attention output
-    // wom: every 128-key block leaves its (numerator, max, sum) partial -- blocks past the
-    // context a neutral one (max -inf, sum 0) -- and the wo projection merges them as it
-    // builds its planes (launch_gemm_skl_attn); no arrival count, no merging block, no planes
-    int wom = 0;
 };
 
 constexpr int ARGB = 64;                // argmax partial blocks per row
@@ -110,10 +102,9 @@ hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const
 hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void* W,
                        const float* wscale, int K, int M, int N, const float* bias, float* C,
                        int ldc, hipStream_t st, float* ws = nullptr, size_t ws_elems = 0);
-int gemm_ksplit(int M, int N, int K, size_t ws_elems);
 hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, const float* rope,
                           int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st, int kv16 = 0);
-hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
+hipError_t launch_attn_rows_mf(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
                              int k_first, int window, float scale, hipStream_t st, float* ws = nullptr,
                              size_t ws_elems = 0, uint16_t* xs = nullptr, int kv16 = 0);
@@ -205,15 +196,8 @@ int skl_splits(int K);
 constexpr int SKL_MAX_SLICES = 12;  // D <= 3072
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
                            float* part, hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f);
-// the batched wo projection (k_skl) with its planes built from the decode attention's
-// partials (AttnFuse.wom): stream j, head h, partial s at apart[j * apart_n + (h * maxs + s) *
-// (hd + 2)] = {numerator[hd], max, sum}, np partials per head merged (voxtral_kernels.c:
-// 554-560's softmax over the whole key range), hd = 128; K = heads * 128
-hipError_t launch_gemm_skl_attn(const float* apart, size_t apart_n, int maxs, int np, int K, const void* Wf,
-                                const float* wscale, int N, int nb, float* part, hipStream_t st);
 hipError_t launch_gemm_skl_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, int N, int nb, float* part,
                                hipStream_t st);  // tools/kbench sweep
-constexpr int ATT_WOM_MAX = 4;  // partials per head the wo prologue merges (contexts <= 512 keys)
 // x += the S slabs (+ bias); planes of x * w (* (1 + ada)); the row's sums of squares per
 // 256-column slice to ssq[row / 16][D / 256][row % 16] (the inverse RMS is applied by
 // launch_gemm_skl)

@@ -94,158 +94,17 @@ __global__ __launch_bounds__(256) void k_rmsnorm_rows(const float* __restrict__ 
 }
 
 // ============================================================================
-// MFMA GEMM for M>1:  C[M,N] (op)= A[M,K] (f32) * W[N,K]^T (bf16, or int8 with per-row
-// scales: the Q8 "fused dequant -> bf16 MFMA" path, voxtral_kernels.c:320-393)
-// tile 64x64x32, 256 threads = 4 waves in 2x2, each wave 32x32 = 2x2 16x16 tiles,
-// v_mfma_f32_16x16x32_bf16.  A is split into NSPLIT bf16 terms in the staging pass; an
-// int8 weight is exact in bf16, so Q8 tiles are converted while staging and the row scale
-// is applied to the f32 result (s * sum(x q), where the reference sums x (q s)).
-// ============================================================================
-#define GB_M 64
-#define GB_N 64
-#define GB_K 32
-#define GB_LDS (GB_K + 8)  // padded bf16 row (80 B) to spread ds_read_b128 lanes
-
-template <int EPI, int NSPLIT, int WQ8>
-__global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ A, int lda,
-                                              const void* __restrict__ W, int K, int M, int N,
-                                              const float* __restrict__ wscale,
-                                              const float* __restrict__ bias,
-                                              float* __restrict__ C, int ldc) {
-    __shared__ __attribute__((aligned(16))) uint16_t sA[NSPLIT][GB_M][GB_LDS];
-    __shared__ __attribute__((aligned(16))) uint16_t sW[GB_N][GB_LDS];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
-    const int m0 = blockIdx.y * GB_M, n0 = blockIdx.x * GB_N;
-    const int srow = tid >> 2, skq = (tid & 3) * 8;
-
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // split-K: slice z of gridDim.z covers K range [kb, kb + Ks) (EPI_PARTIAL only)
-    const int Ks = K / gridDim.z, kb = blockIdx.z * Ks;
-    const bool arow_ok = (m0 + srow) < M;
-    const float* Ap = A + (size_t)(m0 + srow) * lda + skq;
-    const uint16_t* Wp = static_cast<const uint16_t*>(W) + (size_t)(n0 + srow) * K + skq;
-    const int8_t* Wq = static_cast<const int8_t*>(W) + (size_t)(n0 + srow) * K + skq;
-
-    for (int k0 = kb; k0 < kb + Ks; k0 += GB_K) {
-        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
-        if (arow_ok) {
-            a0 = *reinterpret_cast<const float4*>(Ap + k0);
-            a1 = *reinterpret_cast<const float4*>(Ap + k0 + 4);
-        }
-        uint4 wv;
-        if (WQ8) {
-            const uint2 q = *reinterpret_cast<const uint2*>(Wq + k0);
-            uint32_t h[8];
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                h[b] = __float_as_uint(i8f(q.x, b)) >> 16;
-                h[4 + b] = __float_as_uint(i8f(q.y, b)) >> 16;
-            }
-            wv.x = h[0] | (h[1] << 16);
-            wv.y = h[2] | (h[3] << 16);
-            wv.z = h[4] | (h[5] << 16);
-            wv.w = h[6] | (h[7] << 16);
-        } else {
-            wv = *reinterpret_cast<const uint4*>(Wp + k0);
-        }
-        __syncthreads();
-        {
-            float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            uint32_t t[NSPLIT][8];
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                float r = v[e];
-#pragma unroll
-                for (int s = 0; s < NSPLIT; s++) {
-                    uint32_t b = f2bf(r);
-                    t[s][e] = b;
-                    r = r - __uint_as_float(b << 16);
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < NSPLIT; s++) {
-                uint4 pk;
-                pk.x = t[s][0] | (t[s][1] << 16);
-                pk.y = t[s][2] | (t[s][3] << 16);
-                pk.z = t[s][4] | (t[s][5] << 16);
-                pk.w = t[s][6] | (t[s][7] << 16);
-                *reinterpret_cast<uint4*>(&sA[s][srow][skq]) = pk;
-            }
-            *reinterpret_cast<uint4*>(&sW[srow][skq]) = wv;
-        }
-        __syncthreads();
-        const int fr = lane & 15, fk = (lane >> 4) * 8;
-        bf16x8 bfrag[2];
-#pragma unroll
-        for (int ni = 0; ni < 2; ni++)
-            bfrag[ni] = *reinterpret_cast<const bf16x8*>(&sW[wc * 32 + ni * 16 + fr][fk]);
-#pragma unroll
-        for (int mi = 0; mi < 2; mi++) {
-#pragma unroll
-            for (int s = 0; s < NSPLIT; s++) {
-                bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&sA[s][wr * 32 + mi * 16 + fr][fk]);
-#pragma unroll
-                for (int ni = 0; ni < 2; ni++)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag[ni], acc[mi][ni], 0, 0, 0);
-            }
-        }
-    }
-
-    // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r
-    const int cc = lane & 15, rq = (lane >> 4) * 4;
-#pragma unroll
-    for (int mi = 0; mi < 2; mi++) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int m = m0 + wr * 32 + mi * 16 + rq + r;
-            if (m >= M) continue;
-            if (EPI == EPI_PARTIAL) {
-#pragma unroll
-                for (int ni = 0; ni < 2; ni++)
-                    C[((size_t)blockIdx.z * M + m) * N + n0 + wc * 32 + ni * 16 + cc] = acc[mi][ni][r];
-            } else if (EPI == EPI_SWIGLU) {
-                // wave's 32 columns = one interleave group: tile 0 = w1 rows, tile 1 = w3 rows
-                const int g = (n0 + wc * 32) >> 5;
-                const int j = g * 16 + cc;
-                float gt = acc[mi][0][r], up = acc[mi][1][r];
-                if (WQ8) {
-                    gt *= wscale[n0 + wc * 32 + cc];
-                    up *= wscale[n0 + wc * 32 + 16 + cc];
-                }
-                C[(size_t)m * ldc + j] = silu(gt) * up;
-            } else {
-#pragma unroll
-                for (int ni = 0; ni < 2; ni++) {
-                    const int n = n0 + wc * 32 + ni * 16 + cc;
-                    float v = acc[mi][ni][r];
-                    if (WQ8) v *= wscale[n];
-                    if (bias) v += bias[n];
-                    float* cp = C + (size_t)m * ldc + n;
-                    if (EPI == EPI_STORE) *cp = v;
-                    else if (EPI == EPI_RESID) *cp += v;
-                    else if (EPI == EPI_GELU) *cp = gelu_tanh(v);
-                    else if (EPI == EPI_GELU_ERF) *cp = gelu_erf(v);
-                }
-            }
-        }
-    }
-}
-
-// ============================================================================
-// Pipelined MFMA GEMM (the production M>1 path): C[M,N] (op)= A[M,K] * W[N,K]^T.
+// Pipelined MFMA GEMM (the M>1 path of prefill, adapter, conv stem and the twins):
+// C[M,N] (op)= A[M,K] (f32) * W[N,K]^T (bf16, or int8 with per-row scales: the Q8 "fused
+// dequant -> bf16 MFMA" path, voxtral_kernels.c:320-393; an int8 weight is exact in bf16 and
+// the row scale is applied to the f32 result, s * sum(x q), where the reference sums x (q s)).
 // Block tile 128x128, 4 waves in 2x2, each wave 64x64 = 4x4 v_mfma_f32_16x16x32_bf16
 // tiles (the large wave tile keeps the LDS fragment traffic of the 3 A planes under the
 // LDS rate).  K advances in 64-deep stages: the stage's A (f32) and W tiles are loaded to
 // registers one stage ahead (issued before the current stage's MFMAs), split into the three
 // bf16 planes hi/mid/lo (A = hi + mid + lo exactly; Q8 weights -> exact bf16) and written
-// to one of two LDS buffers, so one barrier per stage suffices.  Epilogues as k_gemm
-// (incl. EPI_PARTIAL for split-K slices over blockIdx.z).
+// to one of two LDS buffers, so one barrier per stage suffices.  Epilogues: store, residual
+// add, GELU (tanh / erf), SwiGLU pairs and EPI_PARTIAL for split-K slices over blockIdx.z.
 // ============================================================================
 #define G2_M 128
 #define G2_N 128
@@ -446,14 +305,17 @@ __global__ __launch_bounds__(128 * WN, 2) void k_gemm2(const float* __restrict__
     }
 }
 constexpr size_t G2_LDS_BYTES = (size_t)4 * G2_M * G2_LDS * 2;  // 73,728 B: two blocks per CU
-// Activation planes of k_gemm2: 2 by default (hi + lo, ~2^-18 relative per activation:
-// full-size jfk logits 1.5e-5 / adapter rows 1.4e-5 of the largest magnitude against the
-// 5e-5 bar, ids identical; 20 % less GEMM time), VOX_HIP_GEMM_PLANES=3 for the exact split.
+// Activation planes of the M > 1 GEMMs (k_gemm2, k_gemmf): 3 by default (hi + mid + lo = the
+// f32 activation exactly, so the products with the exact-bf16 weights are exact and only the
+// summation order differs from the reference's f32 sgemm, voxtral_kernels.c:197-240);
+// VOX_HIP_GEMM_PLANES=2 / vox_hip_set_gemm_planes(2) is the faster approximate split (hi +
+// lo, ~2^-18 relative per activation: full-size jfk logits 1.5e-5 / adapter rows 1.4e-5 of
+// the largest magnitude against the 5e-5 bar, ids identical; ~20 % less GEMM time).
 int g_gemm_planes = 0;
 static int gemm_planes() {
     if (!g_gemm_planes) {
         const char* e = getenv("VOX_HIP_GEMM_PLANES");
-        g_gemm_planes = (e && atoi(e) == 3) ? 3 : 2;
+        g_gemm_planes = (e && atoi(e) == 2) ? 2 : 3;
     }
     return g_gemm_planes;
 }
@@ -466,7 +328,7 @@ int set_gemm_planes(int np) {
 
 // ============================================================================
 // Split-K finish: sum the S partial tiles in slice order (deterministic), then the GEMM
-// epilogue (Q8 row scale, bias, residual / GELU / SwiGLU pairing) as in k_gemm.
+// epilogue (Q8 row scale, bias, residual / GELU / SwiGLU pairing).
 // One thread per output element; part is [S][M][N].
 // ============================================================================
 template <int EPI>
@@ -569,164 +431,21 @@ __global__ __launch_bounds__(256) void k_rope_kv_rows(const float* __restrict__ 
 }
 
 // ============================================================================
-// Tiled causal/windowed attention for M>1 queries (encoder chunks, decoder prefill).
-// Semantics of vox_causal_attention (voxtral_kernels.c:541-611) with logical positions:
-// query i sits at q_pos0+i and sees keys p with max(k_first, qp-window+1) <= p <= qp.
-// Block = (head, QT queries): 16, or 32 for chunks of <= 32 rows (a streaming encoder
-// chunk: each K/V tile is then read once per head).  LQ = 256 / QT lanes per query hold
-// KPL keys of a tile for Q.K and DPT dims for P.V.  K/V tiles of 64 keys staged in LDS;
-// online softmax.
-// ============================================================================
-template <int HD, int QT, class ET = float>
-__global__ __launch_bounds__(256) void k_attn_tiled(const float* __restrict__ Q, int ldq,
-                                                    const float* __restrict__ Kc,
-                                                    const float* __restrict__ Vc, int cap,
-                                                    float* __restrict__ O, int ldo, int M, int H,
-                                                    int KVH, int q_pos0, int k_first, int window,
-                                                    float scale, int ns, float* __restrict__ part) {
-    // ns > 1 (few query rows, long key range: streaming encoder chunks): blockIdx.z takes
-    // the z-th of ns key ranges and writes an unnormalised (o, m, l) partial per query row
-    // to part[(h * M + q) * ns + z][HD + 2]; k_attn_tiled_combine merges them in z order.
-    constexpr int KT = 64, LQ = 256 / QT, KPL = KT / LQ, DPT = HD / LQ;
-    // rows padded by 4 floats: the lanes of a wave read QT / 4 different query rows
-    __shared__ __attribute__((aligned(16))) float sQ[QT][HD + 4];
-    __shared__ __attribute__((aligned(16))) float sK[KT][HD + 4];
-    __shared__ __attribute__((aligned(16))) float sV[KT][HD];
-    __shared__ __attribute__((aligned(16))) float sP[QT][KT + 4];
-    const int h = blockIdx.x, q0 = blockIdx.y * QT;
-    const int kvh = h / (H / KVH);
-    const int kvd = KVH * HD;
-    const int nq = min(QT, M - q0);
-    const int tid = threadIdx.x, qi = tid / LQ, j = tid % LQ;
-
-    for (int e = tid; e < QT * HD; e += 256) {
-        int r = e / HD, d = e % HD;
-        sQ[r][d] = (r < nq) ? Q[(size_t)(q0 + r) * ldq + h * HD + d] : 0.f;
-    }
-    const int qp = q_pos0 + q0 + qi;
-    const int qfirst = q_pos0 + q0, qlast = q_pos0 + q0 + nq - 1;
-    int kstart = qfirst - window + 1;
-    if (kstart < k_first) kstart = k_first;
-    int kend = qlast;
-    if (ns > 1) {
-        const int span = ((kend - kstart + 1 + ns - 1) / ns + KT - 1) / KT * KT;
-        const int z = blockIdx.z;
-        kstart += z * span;
-        kend = min(kend, kstart + span - 1);
-    }
-
-    float m = -1e30f, l = 0.f;
-    float o[DPT];
-#pragma unroll
-    for (int e = 0; e < DPT; e++) o[e] = 0.f;
-    const bool qvalid = qi < nq;
-
-    for (int kb = kstart; kb <= kend; kb += KT) {
-        __syncthreads();
-        for (int e = tid; e < KT * (HD / 4); e += 256) {
-            int r = e / (HD / 4), c4 = e % (HD / 4);
-            int kp = kb + r;
-            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
-            if (kp <= kend) {
-                size_t off = (size_t)(kp % cap) * kvd + kvh * HD + c4 * 4;
-                kv = kv_ld4(reinterpret_cast<const ET*>(Kc) + off);
-                vv = kv_ld4(reinterpret_cast<const ET*>(Vc) + off);
-            }
-            *reinterpret_cast<float4*>(&sK[r][c4 * 4]) = kv;
-            *reinterpret_cast<float4*>(&sV[r][c4 * 4]) = vv;
-        }
-        __syncthreads();
-        float s[KPL];
-        float tmax = -INFINITY;
-        {
-            // the query slice is read once per 4 dims for all KPL keys, and the products run
-            // as packed f32 FMAs (v_pk_fma_f32)
-            f32x2 acc[KPL][2];
-#pragma unroll
-            for (int jj = 0; jj < KPL; jj++) acc[jj][0] = acc[jj][1] = f32x2{0.f, 0.f};
-#pragma unroll(32 / KPL)
-            for (int d = 0; d < HD; d += 4) {
-                const float4 a = *reinterpret_cast<const float4*>(&sQ[qi][d]);
-                const f32x2 alo = {a.x, a.y}, ahi = {a.z, a.w};
-#pragma unroll
-                for (int jj = 0; jj < KPL; jj++) {
-                    const float4 b = *reinterpret_cast<const float4*>(&sK[j + LQ * jj][d]);
-                    acc[jj][0] = __builtin_elementwise_fma(alo, f32x2{b.x, b.y}, acc[jj][0]);
-                    acc[jj][1] = __builtin_elementwise_fma(ahi, f32x2{b.z, b.w}, acc[jj][1]);
-                }
-            }
-#pragma unroll
-            for (int jj = 0; jj < KPL; jj++) {
-                const int kp = kb + j + LQ * jj;
-                const bool valid = qvalid && kp <= qp && kp >= qp - window + 1 && kp >= k_first && kp <= kend;
-                const float dot = (acc[jj][0].x + acc[jj][1].x) + (acc[jj][0].y + acc[jj][1].y);
-                s[jj] = valid ? dot * scale : -INFINITY;
-                tmax = fmaxf(tmax, s[jj]);
-            }
-        }
-#pragma unroll
-        for (int off = LQ / 2; off > 0; off >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, off, LQ));
-        const float mnew = fmaxf(m, tmax);
-        float psum = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < KPL; jj++) {
-            float p = (s[jj] == -INFINITY) ? 0.f : expf(s[jj] - mnew);
-            sP[qi][j + LQ * jj] = p;
-            psum += p;
-        }
-#pragma unroll
-        for (int off = LQ / 2; off > 0; off >>= 1) psum += __shfl_xor(psum, off, LQ);
-        const float alpha = expf(m - mnew);
-        l = l * alpha + psum;
-        m = mnew;
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < DPT; e++) o[e] *= alpha;
-        const int d0 = j * DPT;
-        for (int key = 0; key < KT; key += 4) {
-            const float4 p4 = *reinterpret_cast<const float4*>(&sP[qi][key]);
-            const float pk[4] = {p4.x, p4.y, p4.z, p4.w};
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const f32x2 pp = {pk[u], pk[u]};
-#pragma unroll
-                for (int e = 0; e < DPT; e += 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(&sV[key + u][d0 + e]);
-                    f32x2 lo = {o[e], o[e + 1]}, hi = {o[e + 2], o[e + 3]};
-                    lo = __builtin_elementwise_fma(pp, f32x2{v.x, v.y}, lo);
-                    hi = __builtin_elementwise_fma(pp, f32x2{v.z, v.w}, hi);
-                    o[e] = lo.x; o[e + 1] = lo.y; o[e + 2] = hi.x; o[e + 3] = hi.y;
-                }
-            }
-        }
-    }
-    if (qvalid && ns > 1) {
-        float* pp = part + ((size_t)(h * M + q0 + qi) * ns + blockIdx.z) * (HD + 2);
-#pragma unroll
-        for (int e = 0; e < DPT; e++) pp[j * DPT + e] = o[e];
-        if (j == 0) {
-            pp[HD] = m;
-            pp[HD + 1] = l;
-        }
-    } else if (qvalid) {
-        float inv = l > 0.f ? 1.0f / l : 0.f;
-        float* op = O + (size_t)(q0 + qi) * ldo + h * HD + j * DPT;
-#pragma unroll
-        for (int e = 0; e < DPT; e++) op[e] = o[e] * inv;
-    }
-}
-
-// ============================================================================
-// The same attention on f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32
-// accumulation), with k_attn_tiled's semantics, grid and partial layout.  Block = (head, 16
+// Causal / windowed attention for M>1 queries (encoder chunks, decoder prefill) with the
+// semantics of vox_causal_attention (voxtral_kernels.c:541-611) at logical positions: query
+// i sits at q_pos0+i and sees keys p with max(k_first, qp-window+1) <= p <= qp.  On f32 MFMA
+// (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation).  ns > 1 (few query rows,
+// a long key range): blockIdx.z takes the z-th of ns key ranges and writes an unnormalised
+// (o, m, l) partial per query row to part[(h * M + q) * ns + z][HD + 2], merged in z order
+// by k_attn_tiled_combine.  Block = (head, 16
 // queries, key range z) of 4 waves; wave w takes the range's 16-key chunks w, w+4, ...  Per
 // chunk: S^T = K Q^T, A = the K rows straight from the cache, B = the block's query rows held
 // in registers (lane l: row l & 15, dims [g HD/4, (g+1) HD/4) of group g = l >> 4); online
 // softmax on the accumulator (keys 4g + i in the registers, query l & 15 on the lane); then
 // O += P V with P taken from the S^T registers as the A operand (no LDS) and V as B (lane l:
 // dims [NB j, NB j + NB) of rows 4g + c).  The next chunk's K / V load while the current one
-// computes.  The four waves' (o, m, l) meet in LDS at the end.  The VALU kernel staged K / V
-// tiles in LDS and was bound by their reads (160 ds_read_b128 per thread per 64-key tile).
+// computes.  The four waves' (o, m, l) meet in LDS at the end.  (A VALU kernel that staged
+// K / V tiles in LDS was bound by their reads: 160 ds_read_b128 per thread per 64-key tile.)
 // ============================================================================
 // BAT: a batched encoder pass -- blockIdx.z = stream * ns + key split; Q / O / the partials'
 // rows are the stacked rows (stream b's from er.off[b], M = the stacked total), Kc / Vc /
@@ -899,7 +618,7 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
     }
 }
 
-// merge of k_attn_tiled's ns key-range partials: one block per (head, query row); with xs the
+// merge of k_attn_mf's ns key-range partials: one block per (head, query row); with xs the
 // row goes straight into the fragment-major planes of the wo input (H * HD columns)
 template <int HD>
 __global__ __launch_bounds__(HD) void k_attn_tiled_combine(const float* __restrict__ part, int ns, int M,
@@ -1050,16 +769,10 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int K = a.K, KC = WQ8 ? K >> 4 : K >> 3;
     const int ngroups = a.rows / RB;
-    // Groups: block b takes b and b + G first; with a.drain the later ones come from a claim
-    // counter (2G + claim), so blocks that the memory system served early take more groups
-    // and every block drains at the same time; without it b + kG (static).  The claim for the
-    // group after next goes out at the top of each iteration; its value is read a full
-    // group's dot products later, at the barrier that already follows the reduction.
+    // Groups: block b takes b, b + G, b + 2G, ... (static; run-time claims measured 3-4x
+    // slower)
     const int G = gridDim.x;
-    const bool dyn = a.drain != nullptr;
-    const int wv0 = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index, provably uniform
-    __shared__ int s_next[2];
-    int g = blockIdx.x, gn = g + G;
+    int g = blockIdx.x;
     int rows[RB];
     uint4 wv[KQ][RB];
     float wsc[RB];
@@ -1155,14 +868,6 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     int buf = 0;
     for (;;) {
         const int gcur = g;
-        // wave 0 claims with every lane active (lane 0 on the counter, the others add 0 to
-        // their own words past it): a single-lane atomic sits under an EXEC mask, and hipcc
-        // then waits vmcnt(0) for its return at the branch join -- here the value is waited
-        // for only where it is used, before the barrier
-        int claim = 0;
-        if (dyn && wv0 == 0 && gn < ngroups)
-            claim = __hip_atomic_fetch_add(a.drain + (lane ? 2 + lane : 0), lane ? 0 : 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
         // epilogue inputs of this group (independent of the dot products)
         int er0 = 0, er1 = 0;
         float ein0 = 0.f, ein1 = 0.f, esc0 = 1.f, esc1 = 1.f;
@@ -1210,7 +915,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 scur[i] = WQ8 ? wsc[i] : 1.0f;
             }
         }
-        g = gn;
+        g += G;
         // The next group's loads go out before this group's reduction, unconditionally: a
         // load under `if (more)` keeps the old weight registers alive across the branch and
         // doubles the weight register set (fewer resident blocks).  Past the last group they
@@ -1229,10 +934,6 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < RB; i++) red[buf][wave][i] = acc[i];
-        }
-        if (dyn && wv0 == 0) {
-            const int c0 = __builtin_amdgcn_readfirstlane(claim);
-            if (lane == 0) s_next[buf] = g < ngroups ? min(2 * G + c0, ngroups) : ngroups;
         }
         __syncthreads();
         if (!LOGIT && owner) {
@@ -1276,19 +977,10 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 if (EPI == EPI_LOGITS_ALT) alt_row(v[i], rcur[i], am, as, tv, ti);
             }
         }
-        gn = dyn ? s_next[buf] : g + G;
         buf ^= 1;
         if (g >= ngroups) break;
     }
     GEMV_STAMP(2);
-    if (dyn && tid == 0) {
-        // every claim of this block has returned: the last block out resets the counters for
-        // the next launch on the stream (stream order makes the reset visible to it)
-        if (__hip_atomic_fetch_add(a.drain + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
-            __hip_atomic_store(a.drain, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.drain + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
     if ((EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT) && wave == 0 && lane == 0) {
         a.part_val[blockIdx.x] = best;
         a.part_idx[blockIdx.x] = besti;
@@ -1389,15 +1081,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     const int L = min(lp + 1, window);
     const int first = lp - L + 1;
     const int S = (L + BK - 1) / BK;
-    if (sb >= S) {  // uniform per block
-        if (FUSE && F.wom && tid < nh) {
-            // past the context: a neutral partial per head (the wo prologue merges a fixed count)
-            const size_t po = ((size_t)(h0 + tid) * maxs + sb) * (HD + 2);
-            part[po + HD] = -INFINITY;
-            part[po + HD + 1] = 0.f;
-        }
-        return;
-    }
+    if (sb >= S) return;  // uniform per block
     const int k0 = first + sb * BK + wave * ATT_CH;  // >= 0
     const int kn = min(ATT_CH, lp + 1 - k0);  // may be <= 0 for trailing waves
     const int kk = lane & 15, dq = lane >> 4;
@@ -1630,7 +1314,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
         den = v[0];
     };
     if (DBG == 4) ts[4] = __builtin_amdgcn_s_memtime();
-    if (FUSE && S == 1 && !F.wom) {
+    if (FUSE && S == 1) {
         // output row zb straight into the wo input planes: 8 consecutive dims per thread
         const size_t Pn = (size_t)SK_ROWS * H * HD;
         for (int e = tid; e < nh * HD / 8; e += NT) {
@@ -1674,7 +1358,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
 #pragma unroll
         for (int w = 0; w < NWV; w++) num = fmaf(fw[w], sO[w][h][d], num);
         const int hh = h0 + h;
-        if (S == 1 && !(FUSE && F.wom)) {
+        if (S == 1) {
             out[(size_t)hh * HD + d] = den > 0.f ? num * (1.0f / den) : 0.f;
         } else {
             const int po = (int)(((size_t)hh * maxs + sb) * (HD + 2)) * 4;
@@ -1685,7 +1369,7 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
             }
         }
     }
-    if (S > 1 && !(FUSE && F.wom) && (DBG == 0 || DBG == 4)) {
+    if (S > 1 && (DBG == 0 || DBG == 4)) {
         // the last of the S blocks of this kv head to finish merges the S partials of its
         // heads (the former k_attn_combine, one launch and its gap fewer per layer): stores
         // drained, one arrival count per (stream, kv head) just past the partials, reset by
@@ -2728,118 +2412,6 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
     }
 }
 
-// k_skl for the batched wo projection with the decode attention's merge as its prologue
-// (AttnFuse.wom): instead of loading planes, the block reads the NP key-range partials
-// {numerator[128], max, sum} of each (stream, head) its k range covers, merges them (factors
-// exp(m_s - M) in split order, the numerator over the summed denominator: the merging block's
-// arithmetic in k_attn_decode) and writes the three planes of the attention row into LDS --
-// one dependent load round as before, no merging block and no planes round trip through HBM.
-// A partial whose max is -inf (a block past the context) adds nothing.  Dead slots' rows read
-// stale partials; their results are never used (rows are independent columns of the MFMA).
-template <int WQ8, int NW, int KS, int NP>
-__global__ __launch_bounds__(NW * 64) void k_skl_attn(const float* __restrict__ apart, int apart_n, int maxs, int K,
-                                                      const uint8_t* __restrict__ W, const float* __restrict__ wscale,
-                                                      int N, int nb, float* __restrict__ part) {
-    __shared__ uint4 xb[KS * 6 * 64];  // [block][plane][half][lane]
-    constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
-    constexpr int NJ = KS * 2 / NW;  // merge jobs (row, 8 dims) per thread
-    static_assert(KS * 2 % NW == 0, "jobs split over the waves");
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int KB = K >> 6, S = KB / KS, X = N / (16 * NW);
-    const int u = blockIdx.x;
-    const int s = u / X, kb0 = s * KS;
-    const int g = (u % X) * NW + wave;
-    // job idx -> (block blk, half t, lane l): row j = l & 15, dims k .. k + 7 of head k >> 7,
-    // k = 64 blk + 16 (l >> 4) + 8 t (frag_off)
-    // a partial is 130 floats: 8-byte aligned numerators (float2 loads), not 16
-    float2 nv[NJ][NP][4];
-    float mv[NJ][NP], lv[NJ][NP];
-#pragma unroll
-    for (int i = 0; i < NJ; i++) {
-        const int idx = tid + i * NW * 64;
-        const int blk = idx >> 7, t = (idx >> 6) & 1, l = idx & 63;
-        const int j = min(l & 15, nb - 1);
-        const int k = (kb0 + blk) * 64 + (l >> 4) * 16 + t * 8;  // frag_off's layout of a 64-k block
-        const float* pb = apart + (size_t)j * apart_n + (size_t)(k >> 7) * maxs * 130;
-#pragma unroll
-        for (int q = 0; q < NP; q++) {
-#pragma unroll
-            for (int e = 0; e < 4; e++) nv[i][q][e] = *reinterpret_cast<const float2*>(pb + q * 130 + (k & 127) + 2 * e);
-            mv[i][q] = pb[q * 130 + 128];
-            lv[i][q] = pb[q * 130 + 129];
-        }
-    }
-    const __amdgpu_buffer_rsrc_t Wd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g * KB * FB, 0, KB * FB, 0x00020000);
-    u32x4 a[KS][NH];
-#pragma unroll
-    for (int kb = 0; kb < KS; kb++)
-#pragma unroll
-        for (int t = 0; t < NH; t++) a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(Wd, lane * 16 + t * 1024, (kb0 + kb) * FB, 2);
-#pragma unroll
-    for (int i = 0; i < NJ; i++) {
-        const int idx = tid + i * NW * 64;
-        const int blk = idx >> 7, t = (idx >> 6) & 1, l = idx & 63;
-        float M = -INFINITY;
-#pragma unroll
-        for (int q = 0; q < NP; q++) M = fmaxf(M, mv[i][q]);
-        float den = 0.f, o[8];
-#pragma unroll
-        for (int e = 0; e < 8; e++) o[e] = 0.f;
-#pragma unroll
-        for (int q = 0; q < NP; q++) {
-            const bool on = mv[i][q] > -INFINITY;
-            const float f = on ? expf(mv[i][q] - M) : 0.f;
-            den = on ? fmaf(f, lv[i][q], den) : den;
-            const float nn[8] = {nv[i][q][0].x, nv[i][q][0].y, nv[i][q][1].x, nv[i][q][1].y,
-                                 nv[i][q][2].x, nv[i][q][2].y, nv[i][q][3].x, nv[i][q][3].y};
-#pragma unroll
-            for (int e = 0; e < 8; e++) o[e] = on ? fmaf(f, nn[e], o[e]) : o[e];
-        }
-        const float inv = den > 0.f ? 1.0f / den : 0.f;
-        uint32_t hp[4], mp[4], lq[4];
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-            uint16_t a0, b0, c0, a1, b1, c1;
-            split3(den > 0.f ? o[e] * inv : 0.f, a0, b0, c0);
-            split3(den > 0.f ? o[e + 1] * inv : 0.f, a1, b1, c1);
-            hp[e / 2] = a0 | ((uint32_t)a1 << 16);
-            mp[e / 2] = b0 | ((uint32_t)b1 << 16);
-            lq[e / 2] = c0 | ((uint32_t)c1 << 16);
-        }
-        xb[((blk * 3 + 0) * 2 + t) * 64 + l] = make_uint4(hp[0], hp[1], hp[2], hp[3]);
-        xb[((blk * 3 + 1) * 2 + t) * 64 + l] = make_uint4(mp[0], mp[1], mp[2], mp[3]);
-        xb[((blk * 3 + 2) * 2 + t) * 64 + l] = make_uint4(lq[0], lq[1], lq[2], lq[3]);
-    }
-    __syncthreads();
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < KS; kb++)
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            bf16x8 af;
-            if (WQ8) {
-                const u32x4 q = a[kb][0];
-                af = t ? i8x8_bf16(q.z, q.w) : i8x8_bf16(q.x, q.y);
-            } else {
-                const u32x4 q = a[kb][t];
-                af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
-            }
-#pragma unroll
-            for (int p = 0; p < 3; p++)
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, xb[((kb * 3 + p) * 2 + t) * 64 + lane]),
-                                                             acc, 0, 0, 0);
-        }
-    const int j = lane & 15;
-    if (j < nb) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int row = g * 16 + (lane >> 4) * 4 + i;
-            part[((size_t)s * SK_ROWS + j) * N + row] = WQ8 ? acc[i] * wscale[row] : acc[i];
-        }
-    }
-}
-
 // Residual + the planes of an RMSNorm without its row reduction: x += the S slabs of the
 // previous projection (+ bias, summed in split order as k_resid_rmsnorm_fplanes), the row
 // written back, the planes of x * w (* (1 + ada)) -- the inverse RMS is applied by the next
@@ -3246,18 +2818,6 @@ hipError_t launch_rmsnorm_rows(const float* x, int ldx, float* y, int ldy, const
     return hipSuccess;
 }
 
-// K slices for a GEMM: enough blocks to cover the CUs twice when the (M, N) tiles alone do
-// not (prefill M = 38, the N = 1280 encoder projections), each slice >= 4 K steps, the
-// partials within the workspace.
-int gemm_ksplit(int M, int N, int K, size_t ws_elems) {
-    const int tiles = (N / GB_N) * ((M + GB_M - 1) / GB_M);
-    int s = 1;
-    while (tiles * s < 512 && K % (2 * s * GB_K) == 0 && K / (2 * s) >= 4 * GB_K &&
-           (size_t)(2 * s) * M * N <= ws_elems)
-        s *= 2;
-    return s;
-}
-
 // k_gemm2 split count: two 128x128 blocks per CU (LDS), so a launch of T tiles x S slices
 // runs ceil(T S / 512) rounds of K/(64 S) stages (~1.3 us each, two blocks sharing a CU);
 // a split adds the partial tiles' round trip (2 S M N 4 B at ~5 TB/s) and the reduce.
@@ -3318,62 +2878,37 @@ static hipError_t gemm2_launch(dim3 grid, hipStream_t st, const float* A, int ld
                               : gemm2_launch_np<E, Q, 3, 2>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
 }
 
-template <int EPI, int NS>
+template <int EPI>
 static hipError_t gemm_t(const float* A, int lda, const void* W, const float* wscale, int K, int M,
                          int N, const float* bias, float* C, int ldc, hipStream_t st, float* ws,
                          size_t ws_elems) {
-    if (NS == 3 && N % G2_N == 0 && K % G2_K == 0 && lda % 4 == 0) {
-        const int S = ws ? gemm2_ksplit(M, N, K, ws_elems, gemm_wide(M, N, wscale) ? 256 : G2_N) : 1;
-        if (S > 1) {
-            dim3 grid(N / G2_N, (M + G2_M - 1) / G2_M, S);
-            hipError_t e = wscale ? gemm2_launch<EPI_PARTIAL, 1>(grid, st, A, lda, W, K, M, N, wscale, nullptr, ws, N)
-                                  : gemm2_launch<EPI_PARTIAL, 0>(grid, st, A, lda, W, K, M, N, wscale, nullptr, ws, N);
-            if (e != hipSuccess) return e;
-            const size_t outs = (size_t)M * (EPI == EPI_SWIGLU ? N / 2 : N);
-            hipLaunchKernelGGL(k_splitk_reduce<EPI>, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, ws, S, M,
-                               N, wscale, bias, C, ldc);
-            LAUNCH_CHECK();
-            return hipSuccess;
-        }
-        dim3 grid(N / G2_N, (M + G2_M - 1) / G2_M, 1);
-        return wscale ? gemm2_launch<EPI, 1>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc)
-                      : gemm2_launch<EPI, 0>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
-    }
-    const int S = ws ? gemm_ksplit(M, N, K, ws_elems) : 1;
+    const int S = ws ? gemm2_ksplit(M, N, K, ws_elems, gemm_wide(M, N, wscale) ? 256 : G2_N) : 1;
     if (S > 1) {
-        dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M, S);
-        if (wscale)
-            hipLaunchKernelGGL((k_gemm<EPI_PARTIAL, NS, 1>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, nullptr, ws, N);
-        else
-            hipLaunchKernelGGL((k_gemm<EPI_PARTIAL, NS, 0>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, nullptr, ws, N);
-        LAUNCH_CHECK();
+        dim3 grid(N / G2_N, (M + G2_M - 1) / G2_M, S);
+        hipError_t e = wscale ? gemm2_launch<EPI_PARTIAL, 1>(grid, st, A, lda, W, K, M, N, wscale, nullptr, ws, N)
+                              : gemm2_launch<EPI_PARTIAL, 0>(grid, st, A, lda, W, K, M, N, wscale, nullptr, ws, N);
+        if (e != hipSuccess) return e;
         const size_t outs = (size_t)M * (EPI == EPI_SWIGLU ? N / 2 : N);
-        hipLaunchKernelGGL(k_splitk_reduce<EPI>, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, ws, S, M, N,
-                           wscale, bias, C, ldc);
+        hipLaunchKernelGGL(k_splitk_reduce<EPI>, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, st, ws, S, M,
+                           N, wscale, bias, C, ldc);
         LAUNCH_CHECK();
         return hipSuccess;
     }
-    dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M);
-    if (wscale)
-        hipLaunchKernelGGL((k_gemm<EPI, NS, 1>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
-    else
-        hipLaunchKernelGGL((k_gemm<EPI, NS, 0>), grid, dim3(256), 0, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
-    LAUNCH_CHECK();
-    return hipSuccess;
+    dim3 grid(N / G2_N, (M + G2_M - 1) / G2_M, 1);
+    return wscale ? gemm2_launch<EPI, 1>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc)
+                  : gemm2_launch<EPI, 0>(grid, st, A, lda, W, K, M, N, wscale, bias, C, ldc);
 }
 
 hipError_t launch_gemm(int epi, int nsplit, const float* A, int lda, const void* W,
                        const float* wscale, int K, int M, int N, const float* bias, float* C,
                        int ldc, hipStream_t st, float* ws, size_t ws_elems) {
     if (M <= 0) return hipSuccess;
-    if (N % GB_N || K % GB_K || lda % 4) return hipErrorInvalidValue;
-#define GEMM_CASE(E, S) \
-    if (epi == E && nsplit == S) return gemm_t<E, S>(A, lda, W, wscale, K, M, N, bias, C, ldc, st, ws, ws_elems);
-    GEMM_CASE(EPI_STORE, 1) GEMM_CASE(EPI_STORE, 2) GEMM_CASE(EPI_STORE, 3)
-    GEMM_CASE(EPI_RESID, 1) GEMM_CASE(EPI_RESID, 2) GEMM_CASE(EPI_RESID, 3)
-    GEMM_CASE(EPI_GELU, 1) GEMM_CASE(EPI_GELU, 2) GEMM_CASE(EPI_GELU, 3)
-    GEMM_CASE(EPI_GELU_ERF, 1) GEMM_CASE(EPI_GELU_ERF, 2) GEMM_CASE(EPI_GELU_ERF, 3)
-    GEMM_CASE(EPI_SWIGLU, 1) GEMM_CASE(EPI_SWIGLU, 2) GEMM_CASE(EPI_SWIGLU, 3)
+    // nsplit: the activation split of the reference-boundary callers; the planes are set by
+    // vox_hip_set_gemm_planes (2 or 3), shapes are padded by the callers to 128 / 64
+    if (nsplit != 3 || N % G2_N || K % G2_K || lda % 4) return hipErrorInvalidValue;
+#define GEMM_CASE(E) \
+    if (epi == E) return gemm_t<E>(A, lda, W, wscale, K, M, N, bias, C, ldc, st, ws, ws_elems);
+    GEMM_CASE(EPI_STORE) GEMM_CASE(EPI_RESID) GEMM_CASE(EPI_GELU) GEMM_CASE(EPI_GELU_ERF) GEMM_CASE(EPI_SWIGLU)
 #undef GEMM_CASE
     return hipErrorInvalidValue;
 }
@@ -3390,8 +2925,6 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
     return hipSuccess;
 }
 
-int g_attn_qt = 0;    // tools/kbench knob: queries per k_attn_tiled block (16 or 32; 0 = automatic)
-int g_attn_valu = 0;  // tools/kbench knob: 1 = the VALU k_attn_tiled instead of k_attn_mf
 int g_attn_blocks = 0;  // tools/kbench knob: target grid size of the key-range split (0 = 512)
 
 hipError_t launch_rope_kv_rows(const float* qkv, int N, int qd, int kvd, int hd, const float* rope_table,
@@ -3414,7 +2947,7 @@ hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, in
         keys = std::max(keys, er.pos0[b] + er.nr[b] - ks);
     }
     if (qbm == 0) return hipSuccess;
-    // key splits as launch_attn_tiled picks them, over every stream's (head, query block)s
+    // key splits as launch_attn_rows_mf picks them, over every stream's (head, query block)s
     int ns = 1;
     int nblk = 0;
     for (int b = 0; b < er.B; b++) nblk += H * ((er.nr[b] + 15) / 16);
@@ -3440,7 +2973,7 @@ hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, in
     return hipSuccess;
 }
 
-hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
+hipError_t launch_attn_rows_mf(int hd, const float* Q, int ldq, const float* Kc, const float* Vc,
                              int cap, float* O, int ldo, int M, int H, int KVH, int q_pos0,
                              int k_first, int window, float scale, hipStream_t st, float* ws, size_t ws_elems,
                              uint16_t* xs, int kv16) {
@@ -3448,8 +2981,8 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
     if (hd != 64 && hd != 128) return hipErrorInvalidValue;
     if (xs && (M > PLANE_MAX_ROWS || ldo != H * hd)) return hipErrorInvalidValue;
     // 16 queries per block: 32 (each K/V tile of a 25-row streaming chunk read once per head
-    // instead of twice) measured slower, 15.7 vs 14.6 us (tools/kbench)
-    const int QT = g_attn_qt ? g_attn_qt : 16;
+    // instead of twice) measured slower, 15.7 vs 14.6 us (tools/kbench, round 1)
+    const int QT = 16;
     const int qb = (M + QT - 1) / QT;
     // key-range splits when the (head, query block) grid cannot fill the chip: at least 64
     // keys per split, about 256 blocks in all (a 25-row streaming chunk over ~775 keys: 4)
@@ -3459,34 +2992,23 @@ hipError_t launch_attn_tiled(int hd, const float* Q, int ldq, const float* Kc, c
     int ns = 1;
     if (ws && H * qb < 256) {
         // (k_attn_mf, 25 rows x 775 keys: 256 blocks 10.4 us, 512 11.8, 128 13.9, 1024 12.0)
-        const int target = g_attn_blocks ? g_attn_blocks : (g_attn_valu ? 512 : 256);
+        const int target = g_attn_blocks ? g_attn_blocks : 256;
         ns = std::min((keys + 63) / 64, std::max(1, target / (H * qb)));
         while (ns > 1 && (size_t)H * M * ns * (hd + 2) > ws_elems) ns--;
     }
     dim3 grid(H, qb, ns);
-#define VOX_TILED(HD, QQ)                                                                                       \
-    hipLaunchKernelGGL((k_attn_tiled<HD, QQ>), grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, \
-                       q_pos0, k_first, window, scale, ns, ws)
     if (kv16) {
-        // the 16-bit decoder ring (prefill): the MFMA kernel only
-        if (hd != 128 || QT != 16) return hipErrorInvalidValue;
+        // the 16-bit decoder ring (prefill)
+        if (hd != 128) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_attn_mf<128, kvh_t>), grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH,
                            q_pos0, k_first, window, scale, ns, ws);
-    } else if (!g_attn_valu && QT == 16) {
-        if (hd == 64)
-            hipLaunchKernelGGL(k_attn_mf<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
-                               k_first, window, scale, ns, ws);
-        else
-            hipLaunchKernelGGL(k_attn_mf<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
-                               k_first, window, scale, ns, ws);
     } else if (hd == 64) {
-        if (QT == 32) VOX_TILED(64, 32);
-        else VOX_TILED(64, 16);
+        hipLaunchKernelGGL(k_attn_mf<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
+                           k_first, window, scale, ns, ws);
     } else {
-        if (QT == 32) VOX_TILED(128, 32);
-        else VOX_TILED(128, 16);
+        hipLaunchKernelGGL(k_attn_mf<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
+                           k_first, window, scale, ns, ws);
     }
-#undef VOX_TILED
     LAUNCH_CHECK();
     if (ns > 1) {
         // with xs the combine writes the wo planes itself
@@ -3620,9 +3142,8 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-// at least ATT_WOM_MAX: the batched step's wo-merge mode writes 2 x splits partials per head
-// even for windows shorter than two blocks
-int attn_maxch(int window) { return std::max(ATT_WOM_MAX, (window + ATT_MIN_BK - 1) / ATT_MIN_BK); }
+// partial slots per head (at least 4)
+int attn_maxch(int window) { return std::max(4, (window + ATT_MIN_BK - 1) / ATT_MIN_BK); }
 int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
 int g_attn_lw = 0;  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
 int g_attn_kvfast = 1;  // long-context grid with the kv heads of a key range adjacent (tools/kbench: 0 = off)
@@ -3689,11 +3210,10 @@ static hipError_t attn_launch(int hd, const AttnPtrs& p, int nb, int cap, int po
 // splits = key blocks provided per head group (>= the context's ceil(L / 256) for every
 // step the launch serves); 1 -> one block per query head, no combine kernel.
 int g_attn_short = -1;  // k_attn_short for one stream's contexts <= 256 keys (VOX_HIP_ATT_SHORT=0: off)
-// k_attn_short's keys 64..255 loaded after the position read (VOX_HIP_ATT_SHORT_LATE=8: keys
-// 128..255; =0: all 256 speculative).  C2 on one box: all speculative 655.3 / 655.4 / 655.7,
-// from wave 8 663.7 / 667.7 / 666.7 tok/s; on another, from wave 8 672.3 / 670.7 / 673.2,
-// from wave 4 676.6 / 676.7 / 676.2 (profiles/r4_attn_short_late_ab.txt)
-int g_attn_late = -1;
+// k_attn_short's keys 64..255 are loaded after the position read (waves 4..15): C2 on one
+// box, all 256 speculative 655.3 / 655.4 / 655.7 tok/s, from wave 8 663.7 / 667.7 / 666.7; on
+// another, from wave 8 672.3 / 670.7 / 673.2, from wave 4 676.6 / 676.7 / 676.2, from wave 2
+// within noise of wave 4 (profiles/r4_attn_short_late_ab.txt, r4_attn_short_late2_ab.txt)
 hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const float* Vc, int cap,
                               const int* state, int pos_host, int window, float scale, int H,
                               int KVH, float* part, float* out, int splits, hipStream_t st, int kv16) {
@@ -3701,35 +3221,17 @@ hipError_t launch_attn_decode(int hd, const float* q, const float* Kc, const flo
         const char* e = getenv("VOX_HIP_ATT_SHORT");
         g_attn_short = (e && atoi(e) == 0) ? 0 : 1;
     }
-    if (g_attn_late < 0) {
-        const char* e = getenv("VOX_HIP_ATT_SHORT_LATE");  // 0: off; 8 / 2: from wave 8 / 2 on; else 4
-        const int v = e ? atoi(e) : 4;
-        g_attn_late = (v == 0 || v == 2 || v == 8) ? v : 4;
-    }
     if (g_attn_short && splits == 1 && hd == 128 && window > ATT_BK && cap >= ATT_BK && H % KVH == 0) {
         // contexts of <= 256 keys (splits == 1) with a window of > 256: nothing has left the
         // window (lp < 256 < window) and the ring has not wrapped, so keys = slots 0..lp (a
         // window of exactly 256 would reach L = 256 again at lp >= 256 with wrapped slots)
-        if (kv16 && g_attn_late)
+        if (kv16)
             hipLaunchKernelGGL((k_attn_short<128, kvh_t, 4>), dim3(H), dim3(1024), 0, st, q,
                                reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
                                scale, H, KVH, out);
-        else if (kv16)
-            hipLaunchKernelGGL((k_attn_short<128, kvh_t>), dim3(H), dim3(1024), 0, st, q,
-                               reinterpret_cast<const kvh_t*>(Kc), reinterpret_cast<const kvh_t*>(Vc), state, pos_host,
-                               scale, H, KVH, out);
-        else if (g_attn_late == 4)
+        else
             hipLaunchKernelGGL((k_attn_short<128, float, 4>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
                                scale, H, KVH, out);
-        else if (g_attn_late == 2)
-            hipLaunchKernelGGL((k_attn_short<128, float, 2>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
-                               scale, H, KVH, out);
-        else if (g_attn_late)
-            hipLaunchKernelGGL((k_attn_short<128, float, 8>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host,
-                               scale, H, KVH, out);
-        else
-            hipLaunchKernelGGL((k_attn_short<128, float>), dim3(H), dim3(1024), 0, st, q, Kc, Vc, state, pos_host, scale,
-                               H, KVH, out);
         LAUNCH_CHECK();
         return hipSuccess;
     }
@@ -3756,7 +3258,7 @@ static hipError_t attn_batch_fused(const AttnPtrs& p, const AttnFuse& f, int nb,
     // contexts <= 256 keys: one 1024-thread block per (stream, kv head) -- unless those blocks
     // cannot fill the chip (16 streams x 8 kv heads = 128 blocks on 256 CUs): then the 128-key
     // blocks of the long path (two per (stream, kv head), last arriver merges)
-    if (splits == 1 && !f.wom && (!g_attn_bsplit || nb * KVH >= 256)) {
+    if (splits == 1 && (!g_attn_bsplit || nb * KVH >= 256)) {
         hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_WAVES, KT>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, 0,
                            window, scale, H, KVH, maxs, f);
         LAUNCH_CHECK();
@@ -4001,35 +3503,6 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
     return hipErrorInvalidValue;
 }
 
-template <int Q, int NW, int KS, int NP>
-static hipError_t skl_attn_launch(const float* apart, size_t apart_n, int maxs, int K, const void* W, const float* wscale,
-                                  int N, int nb, float* part, hipStream_t st) {
-    const int grid = (N / (16 * NW)) * (K / (64 * KS));
-    hipLaunchKernelGGL((k_skl_attn<Q, NW, KS, NP>), dim3(grid), dim3(NW * 64), 0, st, apart, (int)apart_n, maxs, K,
-                       static_cast<const uint8_t*>(W), wscale, N, nb, part);
-    return hipGetLastError();
-}
-
-hipError_t launch_gemm_skl_attn(const float* apart, size_t apart_n, int maxs, int np, int K, const void* Wf,
-                                const float* wscale, int N, int nb, float* part, hipStream_t st) {
-    const int S = skl_splits(K);
-    // one row block; K = heads x 128 in whole 64-k blocks; the waves as launch_gemm_skl picks them
-    if (!apart || nb < 1 || nb > SK_ROWS || K % 128 || !S || apart_n > 0x7fffffff || maxs < np ||
-        (np != 2 && np != 4))
-        return hipErrorInvalidValue;
-    const int ks = K / 64 / S;
-    const int nb8 = (N / 128) * S;
-    int nw = g_skl_nw ? g_skl_nw : (N % 128 == 0 && nb8 >= (N <= 4096 ? 128 : 384) ? 8 : 4);
-    if (N % (16 * nw)) nw = 4;
-    if (N % (16 * nw)) return hipErrorInvalidValue;
-#define SKA_X(Q, NWW, KSS, NPP)                                                                          \
-    if ((wscale != nullptr) == Q && nw == NWW && ks == KSS && np == NPP)                                 \
-        return skl_attn_launch<Q, NWW, KSS, NPP>(apart, apart_n, maxs, K, Wf, wscale, N, nb, part, st);
-    SKA_X(0, 8, 8, 2) SKA_X(0, 8, 8, 4) SKA_X(0, 4, 8, 2) SKA_X(0, 4, 8, 4)
-    SKA_X(1, 8, 8, 2) SKA_X(1, 8, 8, 4) SKA_X(1, 4, 8, 2) SKA_X(1, 4, 8, 4)
-#undef SKA_X
-    return hipErrorInvalidValue;
-}
 
 // tools/kbench: k_skl (bf16, 16 rows) at a given waves-per-block / 64-k blocks per split
 hipError_t launch_gemm_skl_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, int N, int nb, float* part,

@@ -1061,13 +1061,71 @@ void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {
 }
 
 static int sched_overlap(void) {
-    /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start */
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("VOX_HIP_SCHED_OVERLAP");
-        v = (e && atoi(e) == 0) ? 0 : 1;
+    /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start
+     * (read per run, so one process can serve both ways) */
+    const char *e = getenv("VOX_HIP_SCHED_OVERLAP");
+    return !(e && atoi(e) == 0);
+}
+
+/* the batched steps of one run: every stream whose decoder can run (ran[i]) goes into one
+ * vox_hip_batch_decode call per round, another round only when a stream hit the step cap;
+ * bounded: stream i reads only its first rows[i] adapter rows (an encoder pass may still be
+ * running on its queue) */
+static int sched_steps(vh_sched_t *q, int bounded, const int *rows, const int *ran, int *eos, int *total) {
+    for (int iter = 0;; iter++) {
+        vox_hip_stream_t *hs[VH_SCHED_MAX];
+        int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], gen0[VH_SCHED_MAX], brows[VH_SCHED_MAX], nb = 0;
+        for (int i = 0; i < q->n; i++) {
+            vh_stream_t *s = q->s[i];
+            if (!ran[i] || eos[i]) continue;
+            /* past a step cap only live-mode streams go on: their restart checks (step 4)
+             * belong after a full drain, as in the reference */
+            if (iter > 0 && q->step_cap > 0 && !s->continuous) continue;
+            int st6[6];
+            vox_hip_stream_state(s->st, st6);
+            if (st6[4]) continue;
+            if (st6[3] && rows[i] - st6[1] <= 0) continue;
+            gen0[nb] = st6[5];
+            brows[nb] = rows[i];
+            hs[nb] = s->st;
+            idx[nb++] = i;
+        }
+        if (!nb) break;
+        if (!q->batch) {
+            q->batch = vox_hip_batch_create(q->ctx->model, q->cap);
+            if (!q->batch) return fail("batch: %s", vox_hip_last_error());
+        }
+        const double t0 = now_ms();
+        const int cap = q->step_cap > 0 && q->step_cap < VH_SCHED_STEPS ? q->step_cap : VH_SCHED_STEPS;
+        const int r = bounded ? vox_hip_batch_decode_rows(q->batch, hs, nb, brows, cap, 1, q->tok, counts)
+                              : vox_hip_batch_decode(q->batch, hs, nb, cap, 1, q->tok, counts);
+        if (r < 0) return fail("batched decoder: %s", vox_hip_last_error());
+        const double dt = now_ms() - t0;
+        q->stats.batch_calls++;
+        q->stats.batch_ms += dt;
+        int more = 0;
+        for (int k = 0; k < nb; k++) {
+            vh_stream_t *s = q->s[idx[k]];
+            const int n = counts[k];
+            s->dec_ms += dt;
+            if (!n) continue;
+            if (!s->started_decoding) {
+                /* its prefill ran in this call (shared with the other new streams) */
+                s->started_decoding = 1;
+                s->prefill_ms += dt;
+                q->stats.prefills++;
+            }
+            memcpy(s->dec_buf, q->tok + (size_t)k * cap, sizeof(int) * (size_t)n);
+            if (fill_alt_records(s, gen0[k], n)) return -1;
+            consume_tokens(s, n, &eos[idx[k]]);
+            *total += n;
+            more |= n == cap;
+        }
+        q->stats.tokens += r;
+        /* with a step cap, a scheduled stream's rows beyond it wait for the next run */
+        if (r == 0 || !more) break;
     }
-    return v;
+    return 0;
 }
 
 int vh_sched_run(vh_sched_t *q) {
@@ -1148,63 +1206,21 @@ int vh_sched_run(vh_sched_t *q) {
             ran[i] = decoder_ready(q->s[i]);
             rows[i] = vox_hip_stream_adapter_tokens(q->s[i]->st);
         }
-    for (int iter = 0;; iter++) {
-        vox_hip_stream_t *hs[VH_SCHED_MAX];
-        int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], gen0[VH_SCHED_MAX], brows[VH_SCHED_MAX], nb = 0;
-        for (int i = 0; i < q->n; i++) {
-            vh_stream_t *s = q->s[i];
-            if (!ran[i] || eos[i]) continue;
-            /* past a step cap only live-mode streams go on: their restart checks (step 4)
-             * belong after a full drain, as in the reference */
-            if (iter > 0 && q->step_cap > 0 && !s->continuous) continue;
-            int st6[6];
-            vox_hip_stream_state(s->st, st6);
-            if (st6[4]) continue;
-            if (st6[3] && rows[i] - st6[1] <= 0) continue;
-            gen0[nb] = st6[5];
-            brows[nb] = rows[i];
-            hs[nb] = s->st;
-            idx[nb++] = i;
-        }
-        if (!nb) break;
-        if (!q->batch) {
-            q->batch = vox_hip_batch_create(q->ctx->model, q->cap);
-            if (!q->batch) return fail("batch: %s", vox_hip_last_error());
-        }
-        const double t0 = now_ms();
-        const int cap = q->step_cap > 0 && q->step_cap < VH_SCHED_STEPS ? q->step_cap : VH_SCHED_STEPS;
-        const int r = overlap ? vox_hip_batch_decode_rows(q->batch, hs, nb, brows, cap, 1, q->tok, counts)
-                              : vox_hip_batch_decode(q->batch, hs, nb, cap, 1, q->tok, counts);
-        if (r < 0) return fail("batched decoder: %s", vox_hip_last_error());
-        const double dt = now_ms() - t0;
-        q->stats.batch_calls++;
-        q->stats.batch_ms += dt;
-        int more = 0;
-        for (int k = 0; k < nb; k++) {
-            vh_stream_t *s = q->s[idx[k]];
-            const int n = counts[k];
-            s->dec_ms += dt;
-            if (!n) continue;
-            if (!s->started_decoding) {
-                /* its prefill ran in this call (shared with the other new streams) */
-                s->started_decoding = 1;
-                s->prefill_ms += dt;
-                q->stats.prefills++;
-            }
-            memcpy(s->dec_buf, q->tok + (size_t)k * cap, sizeof(int) * (size_t)n);
-            if (fill_alt_records(s, gen0[k], n)) return -1;
-            consume_tokens(s, n, &eos[idx[k]]);
-            total += n;
-            more |= n == cap;
-        }
-        q->stats.tokens += r;
-        /* with a step cap, a scheduled stream's rows beyond it wait for the next run */
-        if (r == 0 || !more) break;
-    }
+    if (sched_steps(q, overlap, rows, ran, eos, &total)) return -1;
     /* 3 (overlap). the pass beside the steps completes before the run returns */
-    if (overlap)
+    if (overlap) {
         for (int i = 0; i < q->n; i++)
             if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
+        /* without a step cap a run drains every stream (vh_sched_set_step_cap): the rows this
+         * run's pass produced are decoded now, after the pass, instead of by the next run */
+        if (q->step_cap <= 0) {
+            for (int i = 0; i < q->n; i++) {
+                ran[i] = decoder_ready(q->s[i]);
+                rows[i] = vox_hip_stream_adapter_tokens(q->s[i]->st);
+            }
+            if (sched_steps(q, 0, rows, ran, eos, &total)) return -1;
+        }
+    }
     /* 4. per-stream live-mode restarts (voxtral.c:1189-1239) */
     for (int i = 0; i < q->n; i++)
         if (ran[i] == 1 && after_drain(q->s[i], eos[i])) return -1;

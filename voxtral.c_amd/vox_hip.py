@@ -132,7 +132,7 @@ def _err(what):
 
 
 def set_gemm_planes(planes: int):
-    """bf16 activation planes of the M > 1 GEMMs: 2 (default) or 3 (exact f32 activations)"""
+    """bf16 activation planes of the M > 1 GEMMs: 3 (default, exact f32 activations) or 2 (hi + lo)"""
     if lib().vox_hip_set_gemm_planes(int(planes)) != 0:
         _err("set_gemm_planes")
 

@@ -1003,8 +1003,8 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
     if (model_enc_frag(m)) return -1;
     if (!s->exp_) {
         const int kmax = std::max(ED, std::max(EQ, EH));
-        const size_t slab = std::max(std::max((size_t)skl_splits(ED) * NQKV, (size_t)skl_splits(EQ) * ED),
-                                     std::max((size_t)skl_splits(ED) * 2 * EH, (size_t)skl_splits(EH) * ED));
+        const size_t slab = std::max(std::max((size_t)skl_splits(ED, NQKV) * NQKV, (size_t)skl_splits(EQ, ED) * ED),
+                                     std::max((size_t)skl_splits(ED, 2 * EH) * 2 * EH, (size_t)skl_splits(EH, ED) * ED));
         const int RB = ENC_SKINNY_MAX / SK_ROWS;
         CK(dalloc(&s->exp_, (size_t)RB * 3 * SK_ROWS * kmax));
         CK(dalloc(&s->eslab, (size_t)RB * SK_ROWS * slab));
@@ -1084,21 +1084,21 @@ static int run_encoder_rows_skinny(vox_hip_stream_t* s, float* x, int n, long lo
         float* Vc = s->ev + (size_t)l * s->ecap * EKV;
         // previous layer's w2 residual (+ bias) then RMSNorm -> planes (encoder.c:562-566, 680-684)
         CK(launch_rmsnorm_fplanes(x, n, ED, L.attn_norm, nullptr, c.enc_eps, xp, l ? sl : nullptr,
-                                  l ? skl_splits(EH) : 0, st, l ? m->enc[l - 1].b2 : nullptr));
+                                  l ? skl_splits(EH, ED) : 0, st, l ? m->enc[l - 1].b2 : nullptr));
         CK(launch_gemm_skl(xp, ED, F.wqkv, L.sqkv, NQKV, n, sl, st));
         // QKV slabs + biases -> RoPE -> K/V append (one pass), attention with its output
         // merged straight into the wo planes
-        CK(launch_slabs_rope_kv(sl, skl_splits(ED), n, L.bqkv, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
+        CK(launch_slabs_rope_kv(sl, skl_splits(ED, NQKV), n, L.bqkv, EQ, EKV, hd, rope, (int)pos0, s->q, Kc, Vc, s->ecap, st));
         CK(launch_attn_rows_mf(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, n, H, KVH, (int)pos0, 0, c.enc_window, scale, st,
                              s->gws, s->gws_n, xp));
         CK(launch_gemm_skl(xp, EQ, F.wo, L.so, ED, n, sl, st));
         // wo residual (+ bias) then the FFN RMSNorm -> planes (encoder.c:640-650)
-        CK(launch_rmsnorm_fplanes(x, n, ED, L.ffn_norm, nullptr, c.enc_eps, xp, sl, skl_splits(EQ), st, L.bo));
+        CK(launch_rmsnorm_fplanes(x, n, ED, L.ffn_norm, nullptr, c.enc_eps, xp, sl, skl_splits(EQ, ED), st, L.bo));
         CK(launch_gemm_skl(xp, ED, F.w13, L.s13, 2 * EH, n, sl, st));
-        CK(launch_swiglu_fplanes(sl, skl_splits(ED), EH, n, xp, st));
+        CK(launch_swiglu_fplanes(sl, skl_splits(ED, 2 * EH), EH, n, xp, st));
         CK(launch_gemm_skl(xp, EH, F.w2, L.s2, ED, n, sl, st));
     }
-    CK(launch_resid_slabs(x, n, ED, sl, skl_splits(EH), m->enc[c.enc_layers - 1].b2, st));
+    CK(launch_resid_slabs(x, n, ED, sl, skl_splits(EH, ED), m->enc[c.enc_layers - 1].b2, st));
     CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, n, ED, c.enc_eps, st));
     return 0;
 }
@@ -1174,6 +1174,59 @@ static int run_encoder_rows_gemmf(vox_hip_stream_t* s, float* x, int n, long lon
     return 0;
 }
 
+// A single new encoder row (the 1-frame final chunk of a one-shot clip, a live stream's odd
+// frame): the decode GEMVs -- every weight byte read once at the weight-streaming rate, with
+// the RMSNorm prologues and the bias / RoPE + K/V append / SwiGLU / residual epilogues
+// (encoder.c:562-684) -- and the M > 1 attention kernel for the one query row.  Five
+// launches per layer instead of the skinny chain's row blocks of 16.
+static bool enc_gemv_ok(const vox_hip_model_t* m) {
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, EQ = c.enc_heads * c.enc_head_dim, EKV = c.enc_kv_heads * c.enc_head_dim;
+    const bool q8 = m->enc[0].sqkv != nullptr;
+    return gemv_ok(EQ + 2 * EKV, ED, q8) && gemv_ok(ED, EQ, q8) && gemv_ok(2 * c.enc_hidden, ED, q8) &&
+           gemv_ok(ED, c.enc_hidden, q8) && c.enc_head_dim % 2 == 0 && c.enc_hidden % 16 == 0;
+}
+
+static int run_encoder_row_gemv(vox_hip_stream_t* s, float* x, long long pos0, const float* rope) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int ED = c.enc_dim, H = c.enc_heads, KVH = c.enc_kv_heads, hd = c.enc_head_dim;
+    const int EQ = H * hd, EKV = KVH * hd, EH = c.enc_hidden;
+    const float scale = 1.0f / sqrtf((float)hd);
+    hipStream_t st = s->st;
+    for (int l = 0; l < c.enc_layers; l++) {
+        const EncLayerD& L = m->enc[l];
+        float* Kc = s->ek + (size_t)l * s->ecap * EKV;
+        float* Vc = s->ev + (size_t)l * s->ecap * EKV;
+        GemvArgs a;
+        // RMSNorm -> QKV + bias -> RoPE -> K/V append (encoder.c:562-607)
+        memset(&a, 0, sizeof a);
+        a.x = x; a.K = ED; a.W = L.wqkv; a.wscale = L.sqkv; a.rows = EQ + 2 * EKV; a.bias = L.bqkv;
+        a.norm_w = L.attn_norm; a.eps = c.enc_eps; a.y = s->q;
+        a.qd = EQ; a.kvd = EKV; a.hd = hd; a.pos = (int)pos0; a.rope = rope - (size_t)pos0 * hd;
+        a.Kc = Kc; a.Vc = Vc; a.cap = s->ecap;
+        CK(launch_gemv(PRO_NORM, EPI_QKV_BIAS, a, st));
+        // windowed attention of the one query (encoder.c:609-638)
+        CK(launch_attn_rows_mf(hd, s->q, EQ, Kc, Vc, s->ecap, s->att, EQ, 1, H, KVH, (int)pos0, 0, c.enc_window, scale,
+                               st, s->gws, s->gws_n));
+        // wo + bias residual (encoder.c:640-644)
+        memset(&a, 0, sizeof a);
+        a.x = s->att; a.K = EQ; a.W = L.wo; a.wscale = L.so; a.rows = ED; a.bias = L.bo; a.y = x;
+        CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
+        // RMSNorm -> W1|W3 -> silu * up (encoder.c:646-676)
+        memset(&a, 0, sizeof a);
+        a.x = x; a.K = ED; a.W = L.w13; a.wscale = L.s13; a.rows = 2 * EH; a.norm_w = L.ffn_norm; a.eps = c.enc_eps;
+        a.y = s->gate;
+        CK(launch_gemv(PRO_NORM, EPI_SWIGLU, a, st));
+        // w2 + bias residual (encoder.c:678-684)
+        memset(&a, 0, sizeof a);
+        a.x = s->gate; a.K = EH; a.W = L.w2; a.wscale = L.s2; a.rows = ED; a.bias = L.b2; a.y = x;
+        CK(launch_gemv(PRO_NONE, EPI_RESID, a, st));
+    }
+    CK(launch_rmsnorm_rows(x, ED, x, ED, m->enc_norm, nullptr, 1, ED, c.enc_eps, st));
+    return 0;
+}
+
 static int enc_skinny_env() {
     static int v = -1;
     if (v < 0) {
@@ -1191,6 +1244,7 @@ static int run_encoder_rows(vox_hip_stream_t* s, float* x, int n, long long pos0
     const float scale = 1.0f / sqrtf((float)hd);
     hipStream_t st = s->st;
     if (n > ENC_SUB) return set_err("encoder pass of %d rows > %d", n, ENC_SUB);
+    if (n == 1 && enc_gemv_ok(m)) return run_encoder_row_gemv(s, x, pos0, rope);
     if (n <= enc_skinny_rows() && enc_skinny_env() && enc_skinny_ok(c)) return run_encoder_rows_skinny(s, x, n, pos0, rope);
     if (enc_gemmf_ok(m, n)) return run_encoder_rows_gemmf(s, x, n, pos0, rope);
     for (int l = 0; l < c.enc_layers; l++) {
@@ -2395,8 +2449,8 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     TRYH(dalloc(&b->x, S * D));
     {
         const size_t DQ = (size_t)c.dec_heads * c.dec_head_dim, DH = c.dec_hidden;
-        const size_t n = std::max(std::max(skl_splits(D) * QKV, skl_splits(DQ) * D),
-                                  std::max(skl_splits(D) * 2 * DH, skl_splits(DH) * D));
+        const size_t n = std::max(std::max(skl_splits(D, (int)QKV) * QKV, skl_splits(DQ, D) * D),
+                                  std::max(skl_splits(D, 2 * DH) * 2 * DH, skl_splits(DH, D) * D));
         if (!skl_splits(D) || !skl_splits(DQ) || !skl_splits(DH)) {
             set_err("batched decode needs dec_dim, heads*head_dim and dec_hidden divisible by 256");
             return fail();
@@ -2450,7 +2504,7 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         ap.part[i] = b->apart + (size_t)i * b->apart_n;
         ap.out[i] = b->att + (size_t)i * DQ;
     }
-    const int Sres = skl_splits(DH);  // slabs the previous layer's w2 left for the residual
+    const int Sres = skl_splits(DH, DD);  // slabs the previous layer's w2 left for the residual
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         const DecFragD& F = m->dfrag[l];
@@ -2466,11 +2520,11 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         // RoPE + KV append + attention of every live slot, output into the wo planes (one
         // launch; past 256 keys the last key-range block of a kv head merges the partials)
         AttnFuse af;
-        af.qkv = b->part; af.S = skl_splits(DD); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
+        af.qkv = b->part; af.S = skl_splits(DD, DQ + 2 * DKV); af.N = DQ + 2 * DKV; af.rope = m->rope_dec; af.xs = b->xp_q;
         CK(launch_attn_batch_fused(hd, ap, af, nb, cap, c.dec_window, scale, H, KVH, splits, st, kv16));
         CK(batch_gemm(b->xp_q, DQ, F.wo, L.so, DD, nb, b->part, st));
         CK(launch_resid_xw_fplanes(b->x, nb, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, b->xp_d, b->part,
-                                   skl_splits(DQ), nullptr, b->ssq, st));
+                                   skl_splits(DQ, DD), nullptr, b->ssq, st));
         if (!L.s13) {
             // W1|W3 with the SwiGLU folded in (k_sklx: the last block of each column slice
             // sums its slabs and writes the w2 planes)
@@ -2482,7 +2536,7 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
         } else {
             // Q8: the int8 projection, then the SwiGLU rows
             CK(batch_gemm(b->xp_d, DD, F.w13, L.s13, 2 * DH, nb, b->part, st, b->ssq, DD / 256, c.dec_eps));
-            CK(launch_swiglu_fplanes(b->part, skl_splits(DD), DH, nb, b->xp_h, st));
+            CK(launch_swiglu_fplanes(b->part, skl_splits(DD, 2 * DH), DH, nb, b->xp_h, st));
         }
         CK(batch_gemm(b->xp_h, DH, F.w2, L.s2, DD, nb, b->part, st));
     }

@@ -7,7 +7,8 @@ namespace vox {
 
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_GELU_ERF = 3, EPI_SWIGLU = 4, EPI_QKV = 5, EPI_LOGITS = 6,
        EPI_LOGITS_ALT = 7,
-       EPI_PARTIAL = 8 };  // split-K GEMM slice: raw f32 tile into a workspace, epilogue in k_splitk_reduce  // + softmax partials and top-4 text candidates (stream_fill_alts)
+       EPI_PARTIAL = 8,      // split-K GEMM slice: raw f32 tile into a workspace, epilogue in k_splitk_reduce
+       EPI_QKV_BIAS = 9 };   // EPI_QKV with the projection's bias added before RoPE (the encoder's)
 constexpr int ALT_TEXT_MIN = 1000;   // TOKEN_TEXT_MIN (voxtral.c:399)
 constexpr int ALT_PART = 10;         // per-block alt partial: m, s, 4 values, 4 ids
 constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3, pad
@@ -190,8 +191,9 @@ hipError_t launch_swiglu_fplanes(const float* part, int S, int H, int nb, uint16
 // C[j][n] = sum_k x_j[k] W[n][k] (LM head: k_skf)
 hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* C,
                            int ldc, hipStream_t st);
-// split-K slabs part[s][16][N], s < skl_splits(K) (projections: k_skl)
-int skl_splits(int K);
+// split-K slabs part[s][16][N], s < skl_splits(K, N) (projections: k_skl; k_sklx and the
+// encoder's skinny chain use skl_splits(K))
+int skl_splits(int K, int N = 0);
 // ssq: RMSNorm applied to the results (planes from launch_resid_xw_fplanes, nsl slices per row)
 constexpr int SKL_MAX_SLICES = 12;  // D <= 3072
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,

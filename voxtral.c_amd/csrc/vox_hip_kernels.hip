@@ -848,8 +848,9 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         }
     }
 
+    constexpr bool QKVE = (EPI == EPI_QKV || EPI == EPI_QKV_BIAS);
     int lp = 0;
-    if (EPI == EPI_QKV) lp = a.state ? a.state[0] : a.pos;
+    if (QKVE) lp = a.state ? a.state[0] : a.pos;
     float best = -INFINITY;
     int besti = 0x7fffffff;
     // EPI_LOGITS_ALT: online softmax partial (max, sum exp) and the 4 largest text logits
@@ -861,7 +862,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     // dependent round trip per row after the reduction.  The LM head keeps one lane (its
     // running argmax is sequential over ascending rows).
     constexpr bool LOGIT = (EPI == EPI_LOGITS || EPI == EPI_LOGITS_ALT);
-    constexpr bool PAIRED = (EPI == EPI_QKV || EPI == EPI_SWIGLU);
+    constexpr bool PAIRED = (QKVE || EPI == EPI_SWIGLU);
     constexpr int NL = LOGIT ? 1 : (PAIRED ? RB / 2 : RB);
     const bool owner = wave == 0 && lane < NL;
     const int i0 = PAIRED ? 2 * lane : lane;
@@ -870,7 +871,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         const int gcur = g;
         // epilogue inputs of this group (independent of the dot products)
         int er0 = 0, er1 = 0;
-        float ein0 = 0.f, ein1 = 0.f, esc0 = 1.f, esc1 = 1.f;
+        float ein0 = 0.f, ein1 = 0.f, esc0 = 1.f, esc1 = 1.f, eb0 = 0.f, eb1 = 0.f;
         if (!LOGIT && owner) {
             int rr[RB];
             gemv_rows<EPI, RB>(gcur, rr);
@@ -885,7 +886,11 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
             }
             if (EPI == EPI_RESID) ein0 = a.y[er0] + (a.bias ? a.bias[er0] : 0.f);
             if (EPI == EPI_STORE) ein0 = a.bias ? a.bias[er0] : 0.f;
-            if (EPI == EPI_QKV && er0 < a.qd + a.kvd) {
+            if (EPI == EPI_QKV_BIAS) {
+                eb0 = a.bias[er0];
+                eb1 = a.bias[er1];
+            }
+            if (QKVE && er0 < a.qd + a.kvd) {
                 const int col = er0 < a.qd ? er0 : er0 - a.qd;
                 const float* rp = a.rope + (size_t)lp * a.hd + ((col % a.hd) & ~1);
                 ein0 = rp[0];
@@ -944,11 +949,15 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 v0 *= esc0;
                 v1 *= esc1;
             }
+            if (EPI == EPI_QKV_BIAS) {
+                v0 += eb0;
+                v1 += eb1;
+            }
             if (EPI == EPI_STORE || EPI == EPI_RESID) {
                 a.y[er0] = ein0 + v0;  // RESID: residual + bias were read at the top
             } else if (EPI == EPI_SWIGLU) {
                 a.y[gcur * (RB / 2) + lane] = silu(v0) * v1;
-            } else if (EPI == EPI_QKV) {
+            } else if (QKVE) {
                 if (er0 < a.qd + a.kvd) {
                     const float o0 = v0 * ein0 - v1 * ein1, o1 = v0 * ein1 + v1 * ein0;
                     if (er0 < a.qd) {
@@ -3101,6 +3110,7 @@ const void* gemv_kernel(int pro, int epi, const GemvArgs& a) {
                        : (a.wscale ? gemv_fn<P, E, 4, 1>(kq) : gemv_fn<P, E, 4, 0>(kq));
     GEMV_FN(PRO_NONE, EPI_STORE) GEMV_FN(PRO_NONE, EPI_RESID) GEMV_FN(PRO_NORM, EPI_QKV)
     GEMV_FN(PRO_NORM_ADA, EPI_SWIGLU) GEMV_FN(PRO_NORM, EPI_LOGITS) GEMV_FN(PRO_NORM, EPI_LOGITS_ALT)
+    GEMV_FN(PRO_NORM, EPI_QKV_BIAS) GEMV_FN(PRO_NORM, EPI_SWIGLU)
 #undef GEMV_FN
     return nullptr;
 }
@@ -3132,12 +3142,15 @@ bool gemv_ok(int rows, int K, int q8) {
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
     const int rb = gemv_rb(a.rows);
     if (!gemv_ok(a.rows, a.K, a.wscale != nullptr)) return hipErrorInvalidValue;
+    if (epi == EPI_QKV_BIAS && !a.bias) return hipErrorInvalidValue;
     const int grid = gemv_grid(a.rows);
 #define GEMV_CASE(P, E) \
     if (pro == P && epi == E)                                                            \
         return rb == 8 ? gemv_q<P, E, 8>(a, grid, st) : rb == 2 ? gemv_q<P, E, 2>(a, grid, st) : gemv_q<P, E, 4>(a, grid, st);
     GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_QKV)
     GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS) GEMV_CASE(PRO_NORM, EPI_LOGITS_ALT)
+    // the encoder's single-row chunks (run_encoder_rows_gemv)
+    GEMV_CASE(PRO_NORM, EPI_QKV_BIAS) GEMV_CASE(PRO_NORM, EPI_SWIGLU)
 #undef GEMV_CASE
     return hipErrorInvalidValue;
 }
@@ -3475,30 +3488,48 @@ hipError_t launch_resid_xw_fplanes(float* x, int nb, int D, const float* w, cons
     return hipSuccess;
 }
 
-int skl_splits(int K) {
+// waves (row groups) per block of k_skl at S splits, by the 8-wave grid size (N / 128) * S:
+// narrow outputs take 8 from 128 blocks (decoder wo 3072 x 4096: 7.8 -> 7.1 us at 16 rows; the
+// encoder's wo / w2 at 40 / 100 blocks stay at 4), wide ones from 384 (decoder QKV 6144 x 3072
+// at 288: 11.4 -> 10.2 us with 4; encoder W1|W3 at 400 keeps 8)
+static int skl_nw_for(int N, int S) {
+    const int nb8 = (N / 128) * S;
+    int nw = g_skl_nw ? g_skl_nw : (N % 128 == 0 && nb8 >= (N <= 4096 ? 128 : 384) ? 8 : 4);
+    if (N % (16 * nw)) nw = 4;
+    return nw;
+}
+
+// k_skl split count.  K / 512 splits (8 64-k blocks each) by default; with N given, 6-block
+// splits on 4 waves where they spread the weight bytes more evenly over the CUs in one
+// residency round: the most bytes any CU streams is ceil(blocks / CUs) x the block's bytes
+// (decoder QKV 6144 x 3072: 576 blocks of 64 KiB, up to 3 per CU, against 768 of 48 KiB, 3
+// per CU -- kbench 10.46 -> 9.26 us at 16 rows, profiles/r4_kbench_skl_sweep.txt; the other
+// decoder and encoder shapes keep 8 or have no 6-block split)
+int skl_splits(int K, int N) {
     const int KB = K / 64;
-    return KB % 8 == 0 ? KB / 8 : KB % 4 == 0 ? KB / 4 : 0;
+    const int S8 = KB % 8 == 0 ? KB / 8 : KB % 4 == 0 ? KB / 4 : 0;
+    if (N <= 0 || !S8 || KB % 8 || KB % 6 || N % 64 || g_skl_nw) return S8;
+    const int cus = 256;
+    const int nw8 = skl_nw_for(N, S8);
+    const long long b8 = (long long)(N / (16 * nw8)) * S8, b6 = (long long)(N / 64) * (KB / 6);
+    if (b6 > 3LL * cus) return S8;
+    const long long c8 = (b8 + cus - 1) / cus * 8 * nw8, c6 = (b6 + cus - 1) / cus * 6 * 4;
+    return c6 < c8 ? KB / 6 : S8;
 }
 
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
                            float* part, hipStream_t st, const float* ssq, int nsl, float eps) {
-    const int S = skl_splits(K);
+    const int S = skl_splits(K, N);
     // ssq: one row block (its nsl x 16 sums ride with the planes: nsl * 16 <= the block's threads)
     if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S || (ssq && (nsl < 1 || nsl > SKL_MAX_SLICES || nb > SK_ROWS)))
         return hipErrorInvalidValue;
     const int ks = K / 64 / S;
-    // waves (row groups) per block, by the 8-wave grid size (N / 128) * S: narrow outputs take
-    // 8 from 128 blocks (decoder wo 3072 x 4096: 7.8 -> 7.1 us at 16 rows; the encoder's wo /
-    // w2 at 40 / 100 blocks stay at 4), wide ones from 384 (decoder QKV 6144 x 3072 at 288:
-    // 11.4 -> 10.2 us with 4; encoder W1|W3 at 400 keeps 8)
-    const int nb8 = (N / 128) * S;
-    int nw = g_skl_nw ? g_skl_nw : (N % 128 == 0 && nb8 >= (N <= 4096 ? 128 : 384) ? 8 : 4);
-    if (N % (16 * nw)) nw = 4;
+    const int nw = ks == 6 ? 4 : skl_nw_for(N, S);
     if (N % (16 * nw)) return hipErrorInvalidValue;
 #define SKL_X(Q, NWW, KSS) \
     if ((wscale != nullptr) == Q && nw == NWW && ks == KSS) return skl_launch<Q, NWW, KSS>(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
-    SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4)
-    SKL_X(1, 4, 8) SKL_X(1, 8, 8) SKL_X(1, 4, 4) SKL_X(1, 8, 4)
+    SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4) SKL_X(0, 4, 6)
+    SKL_X(1, 4, 8) SKL_X(1, 8, 8) SKL_X(1, 4, 4) SKL_X(1, 8, 4) SKL_X(1, 4, 6)
 #undef SKL_X
     return hipErrorInvalidValue;
 }
@@ -3516,12 +3547,8 @@ hipError_t launch_gemm_skl_cfg(int nw, int ks, const uint16_t* xs, int K, const 
 }
 
 static int sklx_nw(int N, int K) {
-    // waves per block as launch_gemm_skl picks them
-    const int S = skl_splits(K);
-    const int nb8 = (N / 128) * S;
-    int nw = g_skl_nw ? g_skl_nw : (N % 128 == 0 && nb8 >= (N <= 4096 ? 128 : 384) ? 8 : 4);
-    if (N % (16 * nw)) nw = 4;
-    return nw;
+    // waves per block as launch_gemm_skl picks them at K / 512 splits
+    return skl_nw_for(N, skl_splits(K));
 }
 
 int sklx_slices(int N, int K) { return N / (16 * sklx_nw(N, K)); }

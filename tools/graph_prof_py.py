@@ -5,6 +5,8 @@ ends in SIGSEGV under rocprofv3 inside hipGraphLaunch.)  One mode per process, T
             eagerly through hipExtLaunchKernel with dispatch-recorded events, as bench.py does
   batch  -- the batched decode's slot-table step graphs
   full   -- plain at the full Voxtral-4B shapes (synthetic weights, 200 graph-replayed steps)
+  fullbatch -- the batched decode at the full shapes: 16 streams of a 1355-frame chunk each,
+            148 graph-replayed batched steps (C4's pre-encoded step)
   fullprof -- full with Stream.set_profiling(True) (bench.py's roofline pass)
 Run: rocprofv3 --kernel-trace --stats -d DIR -o x -- python3 tools/graph_prof_py.py MODE"""
 import os
@@ -26,7 +28,8 @@ w = synth_weights(cfg, seed=1)
 m = vox_hip.Model(cfg, w)
 del w
 rng = np.random.default_rng(0)
-mels = [rng.uniform(-0.5, 1.5, size=(900, cfg.mel_bins)).astype(np.float32) for _ in range(4)]
+nst, nfr = (16, 1355) if mode == "fullbatch" else (4, 900)
+mels = [rng.uniform(-0.5, 1.5, size=(nfr, cfg.mel_bins)).astype(np.float32) for _ in range(nst)]
 
 
 def dump_maps():
@@ -36,12 +39,12 @@ def dump_maps():
 
 
 dump_maps()
-if mode == "batch":
+if mode in ("batch", "fullbatch"):
     ss = [vox_hip.Stream(m) for _ in mels]
     for s, mel in zip(ss, mels):
         s.encode_mel(mel)
-    b = vox_hip.Batch(m, 4)
-    n = sum(len(t) for t in b.decode(ss, max_steps=1000, stop_at_eos=False))
+    b = vox_hip.Batch(m, len(ss))
+    n = sum(len(t) for t in b.decode(ss, max_steps=148 if mode == "fullbatch" else 1000, stop_at_eos=False))
     b.close()
     for s in ss:
         s.close()

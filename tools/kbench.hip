@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -171,6 +171,29 @@ int main(int argc, char** argv) {
                 add(nm, timeit([&] { gemv(o.pro, o.epi, (*o.w)[layer++ % NL], o.K, o.rows); }, iters, st),
                     (double)o.rows * o.K * (o.q8 ? 1 : 2));
             }
+        g_gemv_maxb = 0;
+        qs = nullptr;
+        return 0;
+    }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "q8rb")) {
+        // Q8 decode GEMVs: rows per group (2 / 4 / 8) x grid cap: with 16 int8 per 16-B chunk a
+        // group keeps half the bf16 bytes in flight, so more rows per group (or more groups per
+        // CU) should cover the same HBM latency
+        struct O { const char* n; int pro, epi, K, rows; std::vector<uint16_t*>* w; };
+        for (O o : {O{"q8 qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, &wqkv}, O{"q8 wo", PRO_NONE, EPI_RESID, DQ, D, &wo},
+                    O{"q8 w13", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, &w13}, O{"q8 w2", PRO_NONE, EPI_RESID, DH, D, &w2}})
+            for (int rb : {4, 8, 2})
+                for (int mb : {1024, 2048}) {
+                    if (o.epi == EPI_SWIGLU && rb == 2) continue;
+                    g_gemv_rb = rb;
+                    g_gemv_maxb = mb;
+                    qs = wsc;
+                    char nm[96];
+                    snprintf(nm, sizeof nm, "gemv %-6s rb %d cap %4d (grid %4d)", o.n, rb, mb, gemv_grid(o.rows));
+                    add(nm, timeit([&] { gemv(o.pro, o.epi, (*o.w)[layer++ % NL], o.K, o.rows); }, iters, st),
+                        (double)o.rows * o.K);
+                }
+        g_gemv_rb = 0;
         g_gemv_maxb = 0;
         qs = nullptr;
         return 0;
@@ -539,24 +562,21 @@ int main(int argc, char** argv) {
         float* gc = (float*)dmalloc((size_t)1024 * 10240 * 4, 0);
         int epoch = 0;
         struct G { const char* n; int epi, N, K; const uint16_t* W; };
-        for (int M : {70, 677, 1024})
+        for (int M : {70, 256, 400, 512, 677, 800, 1024})
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
                         G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
-                for (int v = 0; v < 7; v++) {
-                    // np2 with the launcher's tile choice, np2 RB8, np2 RB4, np3 (RB4), then the
-                    // same np2 tiles with 16 waves per block (wr4: 4 row shares, 32 x 32 / 16 x 32
-                    // per wave); the wider per-wave tiles of round 4 are in profiles/r4_kbench_gemmf*.txt
-                    const int np = v == 3 ? 3 : 2;
-                    g_gemmf_rb = v == 1 || v == 5 ? 8 : v == 2 || v == 6 ? 4 : 0;
-                    g_gemmf_wr = v >= 4 ? 4 : 2;
+                for (int v = 0; v < 4; v++) {
+                    // np3 (RB4, 8 waves) in the row-tile-major and the column-tile-major unit
+                    // order, twice; earlier variants: profiles/r4_kbench_gemmf*.txt, r5_kbench_gemmf_order.txt
+                    const int np = 3;
+                    g_gemmf_order = v & 1;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
-                    printf("gemmf %-4s M=%4d %dx%d np%d rb%d%s minu%-2d %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
-                           g.K, np, g_gemmf_rb, g_gemmf_wr == 4 ? " wr4" : "", g_gemmf_minu, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                    printf("gemmf %-4s M=%4d %dx%d np%d %s %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
+                           g.K, np, g_gemmf_order ? "colmajor" : "rowmajor", us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
-                g_gemmf_rb = g_gemmf_minu = 0;
-                g_gemmf_wr = -1;
+                g_gemmf_order = 0;
             }
     }
     if (only_gemmf) return 0;

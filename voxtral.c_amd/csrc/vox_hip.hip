@@ -151,6 +151,8 @@ struct DecFragD {
     uint8_t *wqkv, *wo, *w13, *w2;
 };
 static int frag_copy(uint8_t** dst, const uint8_t* src, int N, int K, int q8);
+struct vox_hip_model;
+static int model_frag(vox_hip_model* m);
 
 struct vox_hip_model {
     vox_hip_config_t c;
@@ -504,6 +506,7 @@ struct vox_hip_stream {
     float* eslab;            // skinny encoder: split-K slabs [4][S][16][N]
     uint16_t* exp2;          // k_sklx: the second planes buffer (wo / w2 inputs)
     int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
+    int cus;                 // CUs of the stream's queue (vox_hip_stream_set_cu_share; 0 = all)
     int enc_async;           // vox_hip_stream_encode_mel returns without a stream sync
     float* xbatch;           // stacked encoder rows of a batched pass led by this stream
     float *abatch, *abatch_out;  // its stacked adapter input rows (4 x enc_dim) / adapter rows
@@ -511,6 +514,8 @@ struct vox_hip_stream {
     uint16_t *gpa, *gpc;     // k_gemmf planes: norm / attention rows (K <= max(enc_dim, heads x hd)), gate rows
     int* gflags;             // k_gemmf partial-tile flags + the recompute counter (gemmf_flag_ints())
     int gepoch;              // k_gemmf launch epoch on this stream
+    uint16_t *dpa, *dpc;     // decoder prefill planes on k_gemmf: [rb][3][16][max(dim, heads x hd)], [rb][3][16][hidden]
+    int dp_rows;             // rows they hold
     int n_alt;               // vox_stream_set_alt (voxtral.c:1329-1337); 1 = off
     float alt_cutoff;
     int graph_alt;           // alt mode the step graphs were captured with
@@ -641,6 +646,49 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     return s;
 }
 
+// a queue restricted to CUs [first, first + n) (n < 0: [first, last]; 0 or out of range: every
+// CU), as bits of the HIP CU mask
+static hipError_t queue_with_cus(hipStream_t* q, int first, int n, int prio_high) {
+    int dev = 0, ncu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    if (n < 0 && first > 0 && first < ncu) n = ncu - first;  // n < 0: CUs [first, last]
+    if (n <= 0 || first < 0 || first + n > ncu) {
+        if (prio_high) {
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+            return hipStreamCreateWithPriority(q, hipStreamNonBlocking, hi);
+        }
+        return hipStreamCreateWithFlags(q, hipStreamNonBlocking);
+    }
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int c = first; c < first + n; c++) mask[c / 32] |= 1u << (c % 32);
+    return hipExtStreamCreateWithCUMask(q, (uint32_t)mask.size(), mask.data());
+}
+
+// Serving policy (no reference counterpart): the stream's queue -- its encoder chunks, the
+// cross-stream encoder pass it leads, its own prefill / decode -- runs on CUs [first, first +
+// n) only, so kernels on other queues (the batched steps) never wait behind its k_gemmf blocks'
+// LDS; the encoder GEMM's stream-K grid is sized to n.  n <= 0: every CU again.  The stream's
+// queue is drained first.
+extern "C" int vox_hip_stream_set_cu_share(vox_hip_stream_t* s, int first, int n) {
+    if (!s) return set_err("set_cu_share: null stream");
+    CK(hipStreamSynchronize(s->st));
+    hipStream_t q = nullptr;
+    CK(queue_with_cus(&q, first, n, 0));
+    CK(hipStreamDestroy(s->st));
+    s->st = q;
+    if (n < 0 && first > 0) {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            n = ncu - first;
+    }
+    s->cus = n > 0 ? n : 0;
+    s->graph_ready = 0;
+    return 0;
+}
+
 extern "C" int vox_hip_stream_kv_fp16(const vox_hip_stream_t* s) { return s->kv16; }
 
 // layer l's decoder K or V ring (base = s->dk or s->dv) in the stream's element type
@@ -662,7 +710,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
     dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch); dfree(s->abatch); dfree(s->abatch_out);
-    dfree(s->gpa); dfree(s->gpc); dfree(s->gflags);
+    dfree(s->gpa); dfree(s->gpc); dfree(s->gflags); dfree(s->dpa); dfree(s->dpc);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
     if (s->sev) hipEventDestroy(s->sev);
@@ -1124,17 +1172,34 @@ static bool enc_gemmf_ok(const vox_hip_model_t* m, int n) {
            ED <= 4 * 512;
 }
 
-static int gemmf(vox_hip_stream_t* s, int epi, const uint16_t* xs, int K, int n, const uint8_t* W, int N,
-                 const float* bias, float* C, int ldc, uint16_t* xo) {
+// one k_gemmf launch on queue st with its split workspace, partial-tile flags and epoch
+// counter (a queue's own: two k_gemmf launches in flight on two queues must not share flags)
+struct GemmfQ {
+    hipStream_t st;
+    float* ws;
+    size_t ws_n;
+    int* flags;
+    int* epoch;
+    int cus;
+};
+
+static int gemmf_on(const GemmfQ& q, int epi, const uint16_t* xs, int K, int n, const uint8_t* W, int N,
+                    const float* bias, float* C, int ldc, uint16_t* xo) {
     // the hand-off epoch is a host counter baked into the launch: a captured (replayed)
     // k_gemmf would reuse it and read stale partial tiles, so capture is refused
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    CK(hipStreamIsCapturing(s->st, &cs));
+    CK(hipStreamIsCapturing(q.st, &cs));
     if (cs != hipStreamCaptureStatusNone) return set_err("k_gemmf launch while the stream is capturing");
-    if (++s->gepoch <= 0) s->gepoch = 1;
-    CK(launch_gemmf(epi, gemm_planes_np(), xs, K, n, W, N, bias, C, ldc, xo, s->gws, s->gws_n, s->gflags, s->gepoch,
-                    s->st));
+    if (++*q.epoch <= 0) *q.epoch = 1;
+    CK(launch_gemmf(epi, gemm_planes_np(), xs, K, n, W, N, bias, C, ldc, xo, q.ws, q.ws_n, q.flags, *q.epoch, q.st,
+                    q.cus));
     return 0;
+}
+
+static int gemmf(vox_hip_stream_t* s, int epi, const uint16_t* xs, int K, int n, const uint8_t* W, int N,
+                 const float* bias, float* C, int ldc, uint16_t* xo) {
+    return gemmf_on(GemmfQ{s->st, s->gws, s->gws_n, s->gflags, &s->gepoch, s->cus}, epi, xs, K, n, W, N, bias, C, ldc,
+                    xo);
 }
 
 static int run_encoder_rows_gemmf(vox_hip_stream_t* s, float* x, int n, long long pos0, const float* rope) {
@@ -1631,6 +1696,64 @@ static int stream_prefilled(vox_hip_stream_t* s, hipStream_t q) {
     return 0;
 }
 
+// Decoder prefill rows on k_gemmf (bf16 weights): the projections read the fragment-major
+// decoder copies of the batched path (model_frag) once per 64-row tile -- the 38-row prompt is
+// one tile, where k_gemm2's 128 x 128 tiles were mostly padding and split K eight ways --, with
+// the inputs written as planes by their producers (RMSNorm rows, the attention output, the
+// W1|W3 SwiGLU epilogue), as the encoder's long passes do.
+static bool dec_gemmf_ok(const vox_hip_model_t* m, int n) {
+    const vox_hip_config_t& c = m->c;
+    const int DD = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
+    return enc_gemmf_env() && !m->dec[0].sqkv && n >= 1 && n <= PLANE_MAX_ROWS && gemmf_ok(n, DQ + 2 * DKV, DD) &&
+           gemmf_ok(n, DD, DQ) && gemmf_ok(n, 2 * c.dec_hidden, DD) && gemmf_ok(n, DD, c.dec_hidden) &&
+           c.dec_hidden % 64 == 0;
+}
+
+static int stream_dec_planes(vox_hip_stream_t* s, int rows) {
+    if (rows <= s->dp_rows) return 0;
+    const vox_hip_config_t& c = s->m->c;
+    const int DD = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim;
+    // whole 128-row tiles: k_gemmf reads every row block of a tile (rows past n are computed
+    // and dropped)
+    const int r = (rows + 127) / 128 * 128;
+    dfree(s->dpa);
+    dfree(s->dpc);
+    s->dp_rows = 0;
+    CK(dalloc(&s->dpa, (size_t)r * 3 * std::max(DD, DQ)));
+    CK(dalloc(&s->dpc, (size_t)r * 3 * c.dec_hidden));
+    if (!s->gflags) CK(dalloc(&s->gflags, gemmf_flag_ints()));
+    s->dp_rows = r;
+    return 0;
+}
+
+// the prefill layers of rows x[0..n) with planes / scratch of s on queue q; attn(l) runs the
+// layer's RoPE + K/V append + attention into s->attd
+template <class Attn>
+static int dec_layers_gemmf(vox_hip_stream_t* s, const GemmfQ& q, float* x, int n, Attn attn) {
+    vox_hip_model_t* m = s->m;
+    const vox_hip_config_t& c = m->c;
+    const int DD = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
+    const int DH = c.dec_hidden;
+    if (model_frag(m) || stream_dec_planes(s, n)) return -1;
+    for (int l = 0; l < c.dec_layers; l++) {
+        const DecLayerD& L = m->dec[l];
+        const DecFragD& F = m->dfrag[l];
+        // RMSNorm -> planes, QKV (decoder.c:509-530)
+        CK(launch_rmsnorm_fplanes(x, n, DD, L.attn_norm, nullptr, c.dec_eps, s->dpa, nullptr, 0, q.st));
+        if (gemmf_on(q, EPI_STORE, s->dpa, DD, n, F.wqkv, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, nullptr)) return -1;
+        if (attn(l)) return -1;
+        // wo + residual (decoder.c:552-560)
+        CK(launch_split_fplanes(s->attd, n, DQ, s->dpa, q.st));
+        if (gemmf_on(q, EPI_RESID, s->dpa, DQ, n, F.wo, DD, nullptr, x, DD, nullptr)) return -1;
+        // RMSNorm * (1 + ada) -> planes, W1|W3 with SwiGLU into the w2 planes, w2 + residual (:562-606)
+        CK(launch_rmsnorm_fplanes(x, n, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, s->dpa, nullptr, 0,
+                                  q.st));
+        if (gemmf_on(q, EPI_SWIGLU, s->dpa, DD, n, F.w13, 2 * DH, nullptr, nullptr, DH, s->dpc)) return -1;
+        if (gemmf_on(q, EPI_RESID, s->dpc, DH, n, F.w2, DD, nullptr, x, DD, nullptr)) return -1;
+    }
+    return 0;
+}
+
 // M>1 rows (prefill) at logical positions pos0.. (voxtral_decoder.c:496-606)
 static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, const float* rope) {
     vox_hip_model_t* m = s->m;
@@ -1641,6 +1764,16 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
     hipStream_t st = s->st;
     if (stream_alloc_dec_rows(s, n)) return -1;
     if (n > DEC_SLACK + 1 && pos0 > 0) return set_err("prefill of %d rows on a non-empty cache", n);
+    if (n > 1 && dec_gemmf_ok(m, n)) {
+        return dec_layers_gemmf(s, GemmfQ{st, s->gws, s->gws_n, s->gflags, &s->gepoch, s->cus}, x, n, [&](int l) -> int {
+            float* Kc = dec_ring(s, s->dk, l);
+            float* Vc = dec_ring(s, s->dv, l);
+            CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st, s->kv16));
+            CK(launch_attn_rows_mf(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale,
+                                   st, s->gws, s->gws_n, nullptr, s->kv16));
+            return 0;
+        });
+    }
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         float* Kc = dec_ring(s, s->dk, l);
@@ -2360,8 +2493,11 @@ struct vox_hip_batch {
     int lnb;
     long long n_calls, n_replays, n_rows, n_captures, n_prefill_passes, n_prefilled;
     // split-K workspace of the stacked prefills (not the lead stream's: with an encoder pass
-    // running beside the batched steps, that stream's queue may be using its own)
+    // running beside the batched steps, that stream's queue may be using its own), and the
+    // k_gemmf partial-tile flags + epoch of the batch queue's prefill launches
     float* pgws;
+    int* gflags;
+    int gepoch;
 };
 
 static int* slot_toklog(BatchSlot* slots) { return reinterpret_cast<int*>(slots + VOX_MAX_BATCH); }
@@ -2412,7 +2548,7 @@ extern "C" void vox_hip_batch_free(vox_hip_batch_t* b) {
     if (b->st) hipStreamSynchronize(b->st);
     dfree(b->x); dfree(b->part); dfree(b->ssq); dfree(b->ticket); dfree(b->q); dfree(b->att);
     dfree(b->logits); dfree(b->pval); dfree(b->pidx); dfree(b->palt); dfree(b->apart);
-    dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h); dfree(b->pgws);
+    dfree(b->xp_d); dfree(b->xp_q); dfree(b->xp_h); dfree(b->pgws); dfree(b->gflags);
     if (b->slots) hipFree(b->slots);
     if (b->hslots) hipHostFree(b->hslots);
     batch_drop_graphs(b);
@@ -2439,13 +2575,9 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     const size_t S = VOX_MAX_BATCH;  // rows of the slot-indexed buffers (graphs of any bucket)
     auto fail = [&]() -> vox_hip_batch_t* { vox_hip_batch_free(b); return nullptr; };
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
-    {
-        // the batched steps' queue at the highest priority: beside a cross-stream encoder pass
-        // (vox_hip_batch_decode_rows) the latency-bound step kernels go first
-        int lo = 0, hi = 0;
-        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-        TRYH(hipStreamCreateWithPriority(&b->st, hipStreamNonBlocking, hi));
-    }
+    // the batched steps' queue at the highest priority: beside a cross-stream encoder pass
+    // (vox_hip_batch_decode_rows) the latency-bound step kernels go first
+    TRYH(queue_with_cus(&b->st, 0, 0, 1));
     TRYH(dalloc(&b->x, S * D));
     {
         const size_t DQ = (size_t)c.dec_heads * c.dec_head_dim, DH = c.dec_hidden;
@@ -2646,6 +2778,24 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B,
         er.nr[i] = np;
         er.pos0[i] = 0;
     }
+    if (dec_gemmf_ok(m, N)) {
+        if (!b->gflags) CK(dalloc(&b->gflags, gemmf_flag_ints()));
+        if (dec_layers_gemmf(lead, GemmfQ{st, gws, gws_n, b->gflags, &b->gepoch, 0}, X, N, [&](int l) -> int {
+                for (int i = 0; i < B; i++) {
+                    er.Kc[i] = dec_ring(ss[i], ss[i]->dk, l);
+                    er.Vc[i] = dec_ring(ss[i], ss[i]->dv, l);
+                }
+                CK(launch_rope_kv_rows(lead->qkvd, N, DQ, DKV, hd, m->rope_dec, er, lead->qd_, cap, st));
+                CK(launch_attn_rows(hd, lead->qd_, er, N, cap, lead->attd, H, KVH, c.dec_window, scale, gws, gws_n, st));
+                return 0;
+            }))
+            return -1;
+        for (int i = 0; i < B; i++)
+            if (stream_prefilled(ss[i], st)) return -1;
+        b->n_prefill_passes++;
+        b->n_prefilled += B;
+        return 0;
+    }
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         for (int i = 0; i < B; i++) {
@@ -2815,6 +2965,17 @@ extern "C" int vox_hip_batch_read_logits(vox_hip_batch_t* b, vox_hip_stream_t* s
             return 0;
         }
     return set_err("batch_read_logits: the stream was not advanced by the last batched step");
+}
+
+// the batched steps' queue on CUs [first, first + n) only (n <= 0: every CU, high priority)
+extern "C" int vox_hip_batch_set_cu_share(vox_hip_batch_t* b, int first, int n) {
+    if (!b) return set_err("batch_set_cu_share: null batch");
+    CK(hipStreamSynchronize(b->st));
+    hipStream_t q = nullptr;
+    CK(queue_with_cus(&q, first, n, 1));
+    CK(hipStreamDestroy(b->st));
+    b->st = q;
+    return 0;
 }
 
 extern "C" int vox_hip_batch_stats(const vox_hip_batch_t* b, long long* out6) {

@@ -73,6 +73,8 @@ struct GemmfArgs {
     int epoch;
     int S, NT, T;        // K stages, column tiles, tiles
     long long U;         // T * S work units
+    int MT;              // row tiles
+    int colmajor;        // tile order: 0 = t = mt NT + nt (row tile major), 1 = t = nt MT + mt
 };
 
 constexpr int GF_TIMEOUT_TICKS = 5000;  // s_memrealtime ticks (100 MHz): 50 us of waiting
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
     while (u < u1) {
         const int t = (int)(u / a.S), s0 = (int)(u % a.S);
         const int s1 = (int)min((long long)a.S, s0 + (u1 - u));
-        const int mt = t / a.NT, nt = t % a.NT;
+        const int mt = a.colmajor ? t % a.MT : t / a.NT, nt = a.colmajor ? t / a.MT : t % a.NT;
         f32x4 acc[RBW][NG];
 #pragma unroll
         for (int i = 0; i < RBW; i++)
@@ -377,6 +379,7 @@ static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = -1;     // row blocks per tile with two planes (0 = by shape; 4 or 8; -1: VOX_HIP_GEMMF_RB once)
 int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
+int g_gemmf_order = 0;   // tools/kbench knob: 1 = column-tile-major unit order (a weight tile's row tiles adjacent)
 // waves per block with two planes: 16 (4 row shares of a 128- or 64-row tile: 32 x 32 or 16 x
 // 32 per wave, four waves per SIMD) by default, 8 with VOX_HIP_GEMMF_WR=2 (64 x 32 per wave,
 // two per SIMD).  Same unit ranges, same per-output summation order: the same bits.  tools/
@@ -429,7 +432,7 @@ bool gemmf_ok(int M, int N, int K) { return M > 0 && M <= 1024 && K % 64 == 0 &&
 
 hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
                         float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
-                        hipStream_t st) {
+                        hipStream_t st, int max_blocks) {
     // tiles: 128 x 128 with two planes; 64 x 128 with three (a 3-slot ring of 8 row blocks'
     // three planes would not fit the 160 KB of LDS); 16 waves with two planes (g_gemmf_wr),
     // 8 with three
@@ -458,12 +461,15 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     a.wait_ticks = g_gemmf_wait;
     a.S = K / 64;
     a.NT = N / (64 * NGx);
-    a.T = ((M + 16 * RB - 1) / (16 * RB)) * a.NT;
+    a.MT = (M + 16 * RB - 1) / (16 * RB);
+    a.T = a.MT * a.NT;
+    a.colmajor = g_gemmf_order;
     a.U = (long long)a.T * a.S;
     // one block per CU, but every block at least half a tile's stages (and 4): a tile split
     // over many blocks costs its owner one partial-tile read per extra block
     const long long minu = g_gemmf_minu ? g_gemmf_minu : std::max(4, (a.S + 1) / 2);
     int G = gemmf_grid();
+    if (max_blocks > 0 && max_blocks < G) G = max_blocks;
     if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
     // one partial tile per block: (4 WR waves) x (RB / WR) x NGx x 64 lanes x 4 floats
     if ((size_t)G * 4 * RB * NGx * 256 > ws_floats) return hipErrorInvalidValue;

@@ -461,6 +461,9 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
     __shared__ float sm[4][16], sl[4][16];
     __shared__ __attribute__((aligned(16))) float so[4][16][HD + 4];
     const int zsplit = BAT ? (int)blockIdx.z % ns : (int)blockIdx.z;
+    // query blocks in reverse order: under the causal mask the last rows see the most keys,
+    // so the longest blocks are dispatched first and the short ones fill the tail
+    const int qbi = (int)gridDim.y - 1 - (int)blockIdx.y;
     int rbase = 0, Mr = M;  // first stacked row of this stream, its row count
     if (BAT) {
         const int zb = (int)blockIdx.z / ns;
@@ -469,9 +472,9 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
         q_pos0 = er.pos0[zb];
         Kc = er.Kc[zb];
         Vc = er.Vc[zb];
-        if ((int)blockIdx.y * 16 >= Mr) return;  // uniform per block
+        if (qbi * 16 >= Mr) return;  // uniform per block
     }
-    const int h = blockIdx.x, q0 = blockIdx.y * 16;
+    const int h = blockIdx.x, q0 = qbi * 16;
     const int kvh = h / (H / KVH), kvd = KVH * HD;
     const int nq = min(16, Mr - q0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -569,14 +569,14 @@ int main(int argc, char** argv) {
                     // np3 (RB4, 8 waves) in the row-tile-major and the column-tile-major unit
                     // order, twice; earlier variants: profiles/r4_kbench_gemmf*.txt, r5_kbench_gemmf_order.txt
                     const int np = 3;
-                    g_gemmf_order = v & 1;
+                    g_gemmf_order = (v & 1) ? 1 : 2;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
                     printf("gemmf %-4s M=%4d %dx%d np%d %s %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
-                           g.K, np, g_gemmf_order ? "colmajor" : "rowmajor", us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                           g.K, np, g_gemmf_order == 1 ? "colmajor" : "rowmajor", us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
-                g_gemmf_order = 0;
+                g_gemmf_order = 0;  // by shape
             }
     }
     if (only_gemmf) return 0;

@@ -1191,6 +1191,15 @@ static int gemmf_on(const GemmfQ& q, int epi, const uint16_t* xs, int K, int n, 
     CK(hipStreamIsCapturing(q.st, &cs));
     if (cs != hipStreamCaptureStatusNone) return set_err("k_gemmf launch while the stream is capturing");
     if (++*q.epoch <= 0) *q.epoch = 1;
+    // the launcher's shape / workspace checks, reported with the shape (launch_gemmf has one
+    // error code for all of them), and an error an earlier unchecked call left pending (the
+    // launcher's hipGetLastError would report it as this launch's)
+    if (!gemmf_ok(n, N, K) || !q.ws || !q.flags)
+        return set_err("k_gemmf: unsupported shape M %d N %d K %d (ws %p flags %p)", n, N, K, (void*)q.ws, (void*)q.flags);
+    {
+        const hipError_t pend = hipGetLastError();
+        if (pend != hipSuccess) return set_err("k_gemmf: HIP error pending before the launch: %s", hipGetErrorString(pend));
+    }
     CK(launch_gemmf(epi, gemm_planes_np(), xs, K, n, W, N, bias, C, ldc, xo, q.ws, q.ws_n, q.flags, *q.epoch, q.st,
                     q.cus));
     return 0;
@@ -1214,8 +1223,8 @@ static int run_encoder_rows_gemmf(vox_hip_stream_t* s, float* x, int n, long lon
         const size_t rb = PLANE_MAX_ROWS / SK_ROWS;
         CK(dalloc(&s->gpa, rb * 3 * SK_ROWS * std::max(ED, EQ)));
         CK(dalloc(&s->gpc, rb * 3 * SK_ROWS * EH));
-        CK(dalloc(&s->gflags, gemmf_flag_ints()));
     }
+    if (!s->gflags) CK(dalloc(&s->gflags, gemmf_flag_ints()));
     for (int l = 0; l < c.enc_layers; l++) {
         const EncLayerD& L = m->enc[l];
         const DecFragD& F = m->efrag[l];
@@ -1514,8 +1523,8 @@ static int run_encoder_rows_batch(vox_hip_stream_t* lead, float* X, int N, vox_h
             const size_t rb = PLANE_MAX_ROWS / SK_ROWS;
             CK(dalloc(&lead->gpa, rb * 3 * SK_ROWS * std::max(ED, EQ)));
             CK(dalloc(&lead->gpc, rb * 3 * SK_ROWS * EH));
-            CK(dalloc(&lead->gflags, gemmf_flag_ints()));
         }
+        if (!lead->gflags) CK(dalloc(&lead->gflags, gemmf_flag_ints()));
     }
     for (int l = 0; l < c.enc_layers; l++) {
         const EncLayerD& L = m->enc[l];
@@ -1765,6 +1774,9 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
     if (stream_alloc_dec_rows(s, n)) return -1;
     if (n > DEC_SLACK + 1 && pos0 > 0) return set_err("prefill of %d rows on a non-empty cache", n);
     if (n > 1 && dec_gemmf_ok(m, n)) {
+        // the hand-off flags before the queue descriptor copies the pointer (a stream whose
+        // encoder never ran a k_gemmf pass has none yet)
+        if (!s->gflags) CK(dalloc(&s->gflags, gemmf_flag_ints()));
         return dec_layers_gemmf(s, GemmfQ{st, s->gws, s->gws_n, s->gflags, &s->gepoch, s->cus}, x, n, [&](int l) -> int {
             float* Kc = dec_ring(s, s->dk, l);
             float* Vc = dec_ring(s, s->dv, l);

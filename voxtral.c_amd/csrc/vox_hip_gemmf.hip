@@ -379,7 +379,7 @@ static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = -1;     // row blocks per tile with two planes (0 = by shape; 4 or 8; -1: VOX_HIP_GEMMF_RB once)
 int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
-int g_gemmf_order = 0;   // tools/kbench knob: 1 = column-tile-major unit order (a weight tile's row tiles adjacent)
+int g_gemmf_order = -1;  // 1 = column-tile-major unit order (a weight tile's row tiles adjacent), 2 = row-tile-major, 0 = by shape (-1: VOX_HIP_GEMMF_ORDER once)
 // waves per block with two planes: 16 (4 row shares of a 128- or 64-row tile: 32 x 32 or 16 x
 // 32 per wave, four waves per SIMD) by default, 8 with VOX_HIP_GEMMF_WR=2 (64 x 32 per wave,
 // two per SIMD).  Same unit ranges, same per-output summation order: the same bits.  tools/
@@ -463,7 +463,17 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     a.NT = N / (64 * NGx);
     a.MT = (M + 16 * RB - 1) / (16 * RB);
     a.T = a.MT * a.NT;
-    a.colmajor = g_gemmf_order;
+    // unit order: with three planes (64-row tiles) a row-tile count that is not a multiple of
+    // 4 above 4 (M = 400 / 677 / 800: 7 / 11 / 13 tiles) runs the row-tile-major order 1.2-1.7x
+    // slower than the column-tile-major one (a weight tile's row tiles adjacent); at 2, 4, 8
+    // and 16 row tiles the row-tile-major order is 1-7 % faster (tools/kbench,
+    // profiles/r5_kbench_gemmf_order_m.txt).  VOX_HIP_GEMMF_ORDER / g_gemmf_order: 1 / 2 force either.
+    if (g_gemmf_order < 0) {
+        const char* e = getenv("VOX_HIP_GEMMF_ORDER");
+        const int v = e ? atoi(e) : 0;
+        g_gemmf_order = (v == 1 || v == 2) ? v : 0;
+    }
+    a.colmajor = g_gemmf_order ? g_gemmf_order == 1 : (np == 3 && a.MT > 4 && a.MT % 4 != 0);
     a.U = (long long)a.T * a.S;
     // one block per CU, but every block at least half a tile's stages (and 4): a tile split
     // over many blocks costs its owner one partial-tile read per extra block
@@ -472,7 +482,7 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     if (max_blocks > 0 && max_blocks < G) G = max_blocks;
     if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
     // one partial tile per block: (4 WR waves) x (RB / WR) x NGx x 64 lanes x 4 floats
-    if ((size_t)G * 4 * RB * NGx * 256 > ws_floats) return hipErrorInvalidValue;
+    if ((size_t)G * 4 * RB * NGx * 256 > ws_floats) return hipErrorInvalidConfiguration;  // workspace too small
 #define GF_EPI(E)                                                                               \
     if (epi == E)                                                                               \
         return np == 3 ? gemmf_launch<E, 3, 4, NG, WR>(a, G, st)                                \

@@ -126,13 +126,6 @@ vox_hip_stream_t *vox_hip_stream_create(vox_hip_model_t *m);
 void vox_hip_stream_free(vox_hip_stream_t *s);
 /* 1 if the stream's decoder KV rings hold IEEE half (vox_hip_model_set_kv_fp16), else 0 */
 int vox_hip_stream_kv_fp16(const vox_hip_stream_t *s);
-/* Serving policy (no reference counterpart; the Metal backend has one GPU queue): run the
- * stream's queue -- its encoder chunks and any cross-stream encoder pass it leads -- on CUs
- * [first, first + n) only (n < 0: [first, last CU]), and size the encoder GEMM's grid to that
- * count; n = 0: every CU.  With the
- * batch queue on the other CUs (vox_hip_batch_set_cu_share) the batched steps never share a CU
- * with an encoder pass.  Drains the stream's queue; returns 0 or <0. */
-int vox_hip_stream_set_cu_share(vox_hip_stream_t *s, int first, int n);
 /* stream_reset_full_state (voxtral.c:786-814) / stream_reset_decoder_state (:766-783) */
 int vox_hip_stream_reset(vox_hip_stream_t *s);
 int vox_hip_stream_reset_decoder(vox_hip_stream_t *s);
@@ -243,10 +236,6 @@ int vox_hip_batch_read_logits(vox_hip_batch_t *b, vox_hip_stream_t *s, float *ou
 /* Counters since creation: [0] calls, [1] step replays, [2] live rows over those steps,
  * [3] step-graph captures, [4] batched prefill passes, [5] prefilled streams. */
 int vox_hip_batch_stats(const vox_hip_batch_t *b, long long *out6);
-/* The batched steps' queue on CUs [first, first + n) only (n < 0: [first, last CU]; n = 0: every
- * CU, at the highest stream priority, the default); see vox_hip_stream_set_cu_share.  Returns
- * 0 or <0. */
-int vox_hip_batch_set_cu_share(vox_hip_batch_t *b, int first, int n);
 /* Decoder state snapshot: [0]=kv logical length, [1]=next adapter row, [2]=prev token,
  * [3]=started, [4]=eos_seen, [5]=tokens generated. */
 int vox_hip_stream_state(vox_hip_stream_t *s, int *out6);

@@ -109,18 +109,15 @@ def test_scheduler_step_cap_spreads_bursts(tiny_weights, jfk_samples):
     om.close()
 
 
-@pytest.mark.parametrize("overlap,enc_cus", [("1", "0"), ("0", "0"), ("1", "96")])
-def test_scheduler_finish_then_one_run_drains(tiny_weights, jfk_samples, monkeypatch, overlap, enc_cus):
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_scheduler_finish_then_one_run_drains(tiny_weights, jfk_samples, monkeypatch, overlap):
     """without a step cap one vh_sched_run drains every stream, including the rows
     of the chunk vh_stream_finish queued for that run's encoder pass (with the pass beside
     the steps, VOX_HIP_SCHED_OVERLAP=1, and sequentially): feed everything, finish, run once,
-    and every stream's ids equal its oracle session with nothing pending.  enc_cus: the
-    encoder queues on CUs [0, 96) and the batched steps on the rest
-    (vox_hip_stream_set_cu_share / vox_hip_batch_set_cu_share)."""
+    and every stream's ids equal its oracle session with nothing pending."""
     import vox_hip
     from vox_weights import TINY_LONG
     monkeypatch.setenv("VOX_HIP_SCHED_OVERLAP", overlap)
-    monkeypatch.setenv("VOX_HIP_SCHED_ENC_CUS", enc_cus)
     hm = vox_hip.Model(TINY_LONG, tiny_weights)
     import vox_oracle
     om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb, g_gemmw, g_gemmw_rb, g_gemmw_ngw; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -554,7 +554,7 @@ int main(int argc, char** argv) {
     }
     {
         // k_gemmf (stream-K, planes x fragment-major weights) at the encoder's shapes
-        const size_t wsn = 2 * gemmf_ws_floats(gemmf_grid());  // the NG4 RB8 tiles are twice the default
+        const size_t wsn = 2 * gemmf_ws_floats(gemmf_grid());
         float* gws = (float*)dmalloc(wsn * 4, 0);
         int* gfl = (int*)dmalloc(4096 * 4, 0);
         uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 5120 * 2, 1);
@@ -579,63 +579,34 @@ int main(int argc, char** argv) {
                 g_gemmf_order = 0;  // by shape
             }
     }
-    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmw")) {
-        // k_gemmw (weights in registers) against k_gemmf at the encoder / prefill shapes, np3;
-        // first a bit-level check on random operands (the same per-output MFMA order; only the
-        // stream-K split points differ, so outputs agree to f32 rounding of the partial sums)
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmfm")) {
+        // k_gemmf at small M (streaming chunks, prefills, the one-shot flush chunk): least
+        // stages per block (minu) = half a tile (default) / a quarter / an eighth / 4
         const size_t wsn = 2 * gemmf_ws_floats(gemmf_grid());
         float* gws = (float*)dmalloc(wsn * 4, 0);
         int* gfl = (int*)dmalloc(4096 * 4, 0);
-        const size_t pel = (size_t)64 * 3 * 16 * 5120;
-        uint16_t* gp = (uint16_t*)dmalloc(pel * 2, 1);
-        uint16_t* go = (uint16_t*)dmalloc(pel * 2, 0);
-        float* gc = (float*)dmalloc((size_t)1024 * 10240 * 4, 0);
-        float* gc2 = (float*)dmalloc((size_t)1024 * 10240 * 4, 0);
+        uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 1);
+        uint16_t* go = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 0);
+        float* gc = (float*)dmalloc((size_t)1024 * 18432 * 4, 0);
         int epoch = 0;
-        {
-            std::vector<uint16_t> h(pel);
-            uint32_t r = 12345;
-            for (auto& v : h) { r = r * 1664525u + 1013904223u; v = (uint16_t)(0x3c00u + ((r >> 16) & 0x1ff) - 0x100 + ((r >> 31) << 15)); }
-            CK(hipMemcpy(gp, h.data(), pel * 2, hipMemcpyHostToDevice));
-            std::vector<uint16_t> hw((size_t)10240 * 1280);
-            for (auto& v : hw) { r = r * 1664525u + 1013904223u; v = (uint16_t)(0x3c00u + ((r >> 16) & 0x1ff) - 0x100 + ((r >> 31) << 15)); }
-            CK(hipMemcpy(w13[1], hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
-            for (int M : {70, 677, 1024}) {
-                const int N = 10240, K = 1280;
-                g_gemmw = 0;
-                CK(launch_gemmf(EPI_STORE, 3, gp, K, M, w13[1], N, nullptr, gc, N, nullptr, gws, wsn, gfl, ++epoch, st));
-                CK(launch_gemmw(EPI_STORE, 3, gp, K, M, w13[1], N, nullptr, gc2, N, nullptr, gws, wsn, gfl, ++epoch, st));
-                CK(hipStreamSynchronize(st));
-                std::vector<float> a((size_t)M * N), b((size_t)M * N);
-                CK(hipMemcpy(a.data(), gc, a.size() * 4, hipMemcpyDeviceToHost));
-                CK(hipMemcpy(b.data(), gc2, b.size() * 4, hipMemcpyDeviceToHost));
-                double md = 0, mx = 0;
-                for (size_t i = 0; i < a.size(); i++) { md = std::max(md, (double)fabsf(a[i] - b[i])); mx = std::max(mx, (double)fabsf(a[i])); }
-                printf("gemmw check M=%d: max |gemmw - gemmf| %.3e of max |C| %.3e (rel %.2e)\n", M, md, mx, md / mx);
-            }
-        }
         struct G { const char* n; int epi, N, K; const uint16_t* W; };
-        for (int M : {70, 256, 400, 677, 1024})
+        for (int M : {25, 38, 70, 400, 677})
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
                         G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]},
                         G{"dqkv", EPI_STORE, 6144, 3072, wqkv[3]}, G{"dw13", EPI_SWIGLU, 18432, 3072, w13[3]},
                         G{"dwo", EPI_RESID, 3072, 4096, wo[3]}, G{"dw2", EPI_RESID, 3072, 9216, w2[3]}}) {
-                if (g.n[0] == 'd' && M > 400) continue;  // decoder shapes: prefill sizes only
-                auto run = [&](int w, int rb, int ngw, int order) {
-                    g_gemmw = w; g_gemmw_rb = rb; g_gemmw_ngw = ngw; g_gemmf_order = order;
+                if (g.n[0] == 'd' && M != 38 && M != 677) continue;
+                const int S = g.K / 64;
+                for (int mu : {0, std::max(4, S / 4), std::max(4, S / 8), 4}) {
+                    g_gemmf_minu = mu;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, 3, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
-                    printf("gemmw %-4s M=%4d %5dx%-4d %s rb%d ngw%d %s %9.2f us  %7.1f TF useful  %5.1f%% issued\n", g.n, M, g.N, g.K,
-                           w ? "gemmw" : "gemmf", rb, ngw, order == 1 ? "col" : order == 2 ? "row" : "auto", us,
-                           2.0 * M * g.N * g.K / us / 1e6, 100.0 * 3 * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                    printf("gemmfm %-4s M=%4d %5dx%-4d minu %3d %9.2f us  %7.1f GB/s weights\n", g.n, M, g.N, g.K, mu ? mu : std::max(4, (S + 1) / 2),
+                           us, 2.0 * g.N * g.K / us / 1e3);
                     fflush(stdout);
-                };
-                run(0, 0, 0, 0);
-                for (int rb : {8, 4})
-                    for (int ngw : {4, 2})
-                        for (int order : {2, 1}) run(1, rb, ngw, order);
+                }
+                g_gemmf_minu = 0;
             }
-        g_gemmw = 0; g_gemmw_rb = 0; g_gemmw_ngw = 0; g_gemmf_order = 0;
         return 0;
     }
     if (only_gemmf) return 0;

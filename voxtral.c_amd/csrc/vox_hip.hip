@@ -506,7 +506,6 @@ struct vox_hip_stream {
     float* eslab;            // skinny encoder: split-K slabs [4][S][16][N]
     uint16_t* exp2;          // k_sklx: the second planes buffer (wo / w2 inputs)
     int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
-    int cus;                 // CUs of the stream's queue (vox_hip_stream_set_cu_share; 0 = all)
     int enc_async;           // vox_hip_stream_encode_mel returns without a stream sync
     float* xbatch;           // stacked encoder rows of a batched pass led by this stream
     float *abatch, *abatch_out;  // its stacked adapter input rows (4 x enc_dim) / adapter rows
@@ -646,47 +645,15 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     return s;
 }
 
-// a queue restricted to CUs [first, first + n) (n < 0: [first, last]; 0 or out of range: every
-// CU), as bits of the HIP CU mask
-static hipError_t queue_with_cus(hipStream_t* q, int first, int n, int prio_high) {
-    int dev = 0, ncu = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    if (n < 0 && first > 0 && first < ncu) n = ncu - first;  // n < 0: CUs [first, last]
-    if (n <= 0 || first < 0 || first + n > ncu) {
-        if (prio_high) {
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-            return hipStreamCreateWithPriority(q, hipStreamNonBlocking, hi);
-        }
-        return hipStreamCreateWithFlags(q, hipStreamNonBlocking);
+// the batched steps' queue: the highest stream priority, so beside a cross-stream encoder pass
+// (vox_hip_batch_decode_rows) the latency-bound step kernels go first
+static hipError_t queue_high_priority(hipStream_t* q) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) {
+        (void)hipGetLastError();  // not left pending for the next launch check
+        hi = 0;
     }
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int c = first; c < first + n; c++) mask[c / 32] |= 1u << (c % 32);
-    return hipExtStreamCreateWithCUMask(q, (uint32_t)mask.size(), mask.data());
-}
-
-// Serving policy (no reference counterpart): the stream's queue -- its encoder chunks, the
-// cross-stream encoder pass it leads, its own prefill / decode -- runs on CUs [first, first +
-// n) only, so kernels on other queues (the batched steps) never wait behind its k_gemmf blocks'
-// LDS; the encoder GEMM's stream-K grid is sized to n.  n <= 0: every CU again.  The stream's
-// queue is drained first.
-extern "C" int vox_hip_stream_set_cu_share(vox_hip_stream_t* s, int first, int n) {
-    if (!s) return set_err("set_cu_share: null stream");
-    CK(hipStreamSynchronize(s->st));
-    hipStream_t q = nullptr;
-    CK(queue_with_cus(&q, first, n, 0));
-    CK(hipStreamDestroy(s->st));
-    s->st = q;
-    if (n < 0 && first > 0) {
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-            n = ncu - first;
-    }
-    s->cus = n > 0 ? n : 0;
-    s->graph_ready = 0;
-    return 0;
+    return hipStreamCreateWithPriority(q, hipStreamNonBlocking, hi);
 }
 
 extern "C" int vox_hip_stream_kv_fp16(const vox_hip_stream_t* s) { return s->kv16; }
@@ -1180,7 +1147,6 @@ struct GemmfQ {
     size_t ws_n;
     int* flags;
     int* epoch;
-    int cus;
 };
 
 static int gemmf_on(const GemmfQ& q, int epi, const uint16_t* xs, int K, int n, const uint8_t* W, int N,
@@ -1200,14 +1166,13 @@ static int gemmf_on(const GemmfQ& q, int epi, const uint16_t* xs, int K, int n, 
         const hipError_t pend = hipGetLastError();
         if (pend != hipSuccess) return set_err("k_gemmf: HIP error pending before the launch: %s", hipGetErrorString(pend));
     }
-    CK(launch_gemmf(epi, gemm_planes_np(), xs, K, n, W, N, bias, C, ldc, xo, q.ws, q.ws_n, q.flags, *q.epoch, q.st,
-                    q.cus));
+    CK(launch_gemmf(epi, gemm_planes_np(), xs, K, n, W, N, bias, C, ldc, xo, q.ws, q.ws_n, q.flags, *q.epoch, q.st));
     return 0;
 }
 
 static int gemmf(vox_hip_stream_t* s, int epi, const uint16_t* xs, int K, int n, const uint8_t* W, int N,
                  const float* bias, float* C, int ldc, uint16_t* xo) {
-    return gemmf_on(GemmfQ{s->st, s->gws, s->gws_n, s->gflags, &s->gepoch, s->cus}, epi, xs, K, n, W, N, bias, C, ldc,
+    return gemmf_on(GemmfQ{s->st, s->gws, s->gws_n, s->gflags, &s->gepoch}, epi, xs, K, n, W, N, bias, C, ldc,
                     xo);
 }
 
@@ -1777,7 +1742,7 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
         // the hand-off flags before the queue descriptor copies the pointer (a stream whose
         // encoder never ran a k_gemmf pass has none yet)
         if (!s->gflags) CK(dalloc(&s->gflags, gemmf_flag_ints()));
-        return dec_layers_gemmf(s, GemmfQ{st, s->gws, s->gws_n, s->gflags, &s->gepoch, s->cus}, x, n, [&](int l) -> int {
+        return dec_layers_gemmf(s, GemmfQ{st, s->gws, s->gws_n, s->gflags, &s->gepoch}, x, n, [&](int l) -> int {
             float* Kc = dec_ring(s, s->dk, l);
             float* Vc = dec_ring(s, s->dv, l);
             CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st, s->kv16));
@@ -2587,9 +2552,7 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     const size_t S = VOX_MAX_BATCH;  // rows of the slot-indexed buffers (graphs of any bucket)
     auto fail = [&]() -> vox_hip_batch_t* { vox_hip_batch_free(b); return nullptr; };
 #define TRYH(x) do { hipError_t e__ = (x); if (e__ != hipSuccess) { set_err("%s: %s", #x, hipGetErrorString(e__)); return fail(); } } while (0)
-    // the batched steps' queue at the highest priority: beside a cross-stream encoder pass
-    // (vox_hip_batch_decode_rows) the latency-bound step kernels go first
-    TRYH(queue_with_cus(&b->st, 0, 0, 1));
+    TRYH(queue_high_priority(&b->st));
     TRYH(dalloc(&b->x, S * D));
     {
         const size_t DQ = (size_t)c.dec_heads * c.dec_head_dim, DH = c.dec_hidden;
@@ -2792,7 +2755,7 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B,
     }
     if (dec_gemmf_ok(m, N)) {
         if (!b->gflags) CK(dalloc(&b->gflags, gemmf_flag_ints()));
-        if (dec_layers_gemmf(lead, GemmfQ{st, gws, gws_n, b->gflags, &b->gepoch, 0}, X, N, [&](int l) -> int {
+        if (dec_layers_gemmf(lead, GemmfQ{st, gws, gws_n, b->gflags, &b->gepoch}, X, N, [&](int l) -> int {
                 for (int i = 0; i < B; i++) {
                     er.Kc[i] = dec_ring(ss[i], ss[i]->dk, l);
                     er.Vc[i] = dec_ring(ss[i], ss[i]->dv, l);
@@ -2977,17 +2940,6 @@ extern "C" int vox_hip_batch_read_logits(vox_hip_batch_t* b, vox_hip_stream_t* s
             return 0;
         }
     return set_err("batch_read_logits: the stream was not advanced by the last batched step");
-}
-
-// the batched steps' queue on CUs [first, first + n) only (n <= 0: every CU, high priority)
-extern "C" int vox_hip_batch_set_cu_share(vox_hip_batch_t* b, int first, int n) {
-    if (!b) return set_err("batch_set_cu_share: null batch");
-    CK(hipStreamSynchronize(b->st));
-    hipStream_t q = nullptr;
-    CK(queue_with_cus(&q, first, n, 1));
-    CK(hipStreamDestroy(b->st));
-    b->st = q;
-    return 0;
 }
 
 extern "C" int vox_hip_batch_stats(const vox_hip_batch_t* b, long long* out6) {

@@ -77,6 +77,7 @@ struct GemmfArgs {
     int colmajor;        // tile order: 0 = t = mt NT + nt (row tile major), 1 = t = nt MT + mt
 };
 
+
 constexpr int GF_TIMEOUT_TICKS = 5000;  // s_memrealtime ticks (100 MHz): 50 us of waiting
 static int g_gemmf_wait = GF_TIMEOUT_TICKS;  // vox_hip_set_gemmf_wait (tests force the backstop)
 
@@ -281,7 +282,8 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
     using C = GfCfg<NP, RB, NG, WR>;
     constexpr int RBW = C::RBW;
     extern __shared__ __attribute__((aligned(16))) uint16_t gf_lds[];
-    int* s_ok = reinterpret_cast<int*>(gf_lds + 3 * C::SLOT);   // one word past the ring (same array)
+    // the owner's flag mask, one 8-byte word past the ring (the same array)
+    unsigned long long* s_okm = reinterpret_cast<unsigned long long*>(gf_lds + 3 * C::SLOT);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wc = wave & 3, r0 = (wave >> 2) * RBW;
     const int G = gridDim.x, b = blockIdx.x;
@@ -318,49 +320,57 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
             if (tid == 0) __hip_atomic_store(&a.flags[b], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             continue;
         }
-        // stage 0 is ours: add the later parts in block order, then the epilogue
+        // stage 0 is ours: add the later parts in block order, then the epilogue.  The lanes of
+        // wave 0 poll the later blocks' flags together (bounded), so the owner waits for the
+        // last of them once instead of one flag round trip per block
         const long long tend = (long long)(t + 1) * a.S;
-        for (int pb = b + 1; pb < G && gf_bound(a.U, G, pb) < tend; pb++) {
-            if (tid == 0) {
-                int ok = 0;
+        int npb = 0;
+        while (b + 1 + npb < G && gf_bound(a.U, G, b + 1 + npb) < tend) npb++;
+        if (npb > 64) npb = 64;  // unreachable: a block holds >= 4 stages and a tile <= 144
+        if (npb > 0) {
+            if (wave == 0) {
+                const bool mine = lane < npb;
+                bool ok = !mine;
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 while (a.wait_ticks >= 0) {
-                    if (__hip_atomic_load(&a.flags[pb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch) {
-                        ok = 1;
-                        break;
-                    }
+                    if (!ok) ok = __hip_atomic_load(&a.flags[b + 1 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+                    if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > (unsigned long long)a.wait_ticks) break;
                     __builtin_amdgcn_s_sleep(2);
                 }
                 // every recompute is counted (vox_hip_stream_profile): a timeout that fires in
                 // production costs the owner the whole stage range, so it must not stay silent
-                if (!ok) __hip_atomic_fetch_add(a.recomputes, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                *s_ok = ok;
+                if (mine && !ok) __hip_atomic_fetch_add(a.recomputes, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long okm = __builtin_amdgcn_ballot_w64(mine && ok);
+                if (lane == 0) *s_okm = okm;
             }
             __syncthreads();
-            const int ok = *s_ok;
+            const unsigned long long okm = *s_okm;
             __syncthreads();
-            f32x4 part[RBW][NG];
-            if (ok) {
+            for (int k = 0; k < npb; k++) {
+                const int pb = b + 1 + k;
+                f32x4 part[RBW][NG];
+                if ((okm >> k) & 1) {
+#pragma unroll
+                    for (int i = 0; i < RBW; i++)
+#pragma unroll
+                        for (int g = 0; g < NG; g++)
+                            part[i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Ws, poff(pb, i, g), 0, 16));
+                } else {
+                    // the publishing block has not run: its stage range of this tile, computed here
+#pragma unroll
+                    for (int i = 0; i < RBW; i++)
+#pragma unroll
+                        for (int g = 0; g < NG; g++) part[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const int q0 = (int)(gf_bound(a.U, G, pb) - (long long)t * a.S);
+                    const int q1 = (int)(min(gf_bound(a.U, G, pb + 1), tend) - (long long)t * a.S);
+                    gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, q0, q1, part);
+                }
 #pragma unroll
                 for (int i = 0; i < RBW; i++)
 #pragma unroll
-                    for (int g = 0; g < NG; g++)
-                        part[i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Ws, poff(pb, i, g), 0, 16));
-            } else {
-                // the publishing block has not run: its stage range of this tile, computed here
-#pragma unroll
-                for (int i = 0; i < RBW; i++)
-#pragma unroll
-                    for (int g = 0; g < NG; g++) part[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-                const int q0 = (int)(gf_bound(a.U, G, pb) - (long long)t * a.S);
-                const int q1 = (int)(min(gf_bound(a.U, G, pb + 1), tend) - (long long)t * a.S);
-                gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, q0, q1, part);
+                    for (int g = 0; g < NG; g++) acc[i][g] += part[i][g];
             }
-#pragma unroll
-            for (int i = 0; i < RBW; i++)
-#pragma unroll
-                for (int g = 0; g < NG; g++) acc[i][g] += part[i][g];
         }
         // epilogue: lane holds outputs n = group * 16 + (lane >> 4) * 4 + e for row m = rb * 16 + (lane & 15)
 #pragma unroll
@@ -372,255 +382,6 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
 #pragma unroll
             for (int g = 0; g < NG; g += (EPI == EPI_SWIGLU ? 2 : 1))
                 gf_out<EPI>(a, m, (nt * 4 + wc) * NG + g, lane, acc[i][g], acc[i][EPI == EPI_SWIGLU ? g + 1 : g]);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_gemmw: k_gemmf's stream-K GEMM with the weight operand in registers.  k_gemmf stages both
-// operands through LDS-DMA (40 1-KiB pieces a stage for 192 MFMAs) and pays, per stage, the
-// DMA issue (~100 cycles a piece beside MFMAs, MI355X_MICROARCH.md), 20 ds_read_b128 per wave
-// and a barrier; its MFMA pipes run ~30 % busy.  Here:
-//   * tile 16 RB rows x 64 NGW columns over 8 waves, wave (wm, wn) = (wave >> 2, wave & 3) owning
-//     RB / 2 row blocks x NGW column groups (64 x 64 at RB = 8, NGW = 4: 96 MFMAs a stage with
-//     three planes, against 24 in k_gemmf);
-//   * weights: each wave loads its NGW groups' fragments of the next stage straight into VGPRs
-//     (1 KiB MFMA-ready runs, buffer loads), the two waves of a column slot both (L2 hits);
-//   * planes: ordinary 16-B loads into VGPRs one stage ahead, written to a 2-slot LDS ring
-//     (RB x NP x 2 pieces a stage) at the top of the stage, one barrier per stage.  No LDS-DMA
-//     is in flight anywhere, so hipcc's counted vmcnt waits stay partial (beside a DMA it
-//     drains to 0 at any VGPR-load use, cdna_hip_programming.md "Pipelining across barriers").
-// Stream-K units, the owner's fix-up of later parts (write-through partial tiles, epoch flags,
-// bounded wait, recompute backstop) and the epilogues are k_gemmf's.
-// ---------------------------------------------------------------------------
-template <int NP, int RB, int NGW>
-struct GwCfg {
-    static constexpr int NWV = 8;
-    static constexpr int RBW = RB / 2;                  // row blocks per wave
-    static constexpr int CH = RB * NP * 2;              // 1 KiB plane pieces per stage
-    static constexpr int NA = CH / NWV;                 // plane pieces per wave
-    static constexpr int SLOT = CH * 512;               // bf16 elements per LDS slot
-    static constexpr int TILE = NWV * RBW * NGW * 256;  // floats of one partial tile
-    static_assert(CH % NWV == 0 && RB % 2 == 0 && NGW % 2 == 0, "k_gemmw tile");
-};
-
-template <int NP, int RB, int NGW>
-struct GwRegs {
-    u32x4 a[GwCfg<NP, RB, NGW>::NA];  // plane pieces (to LDS)
-    u32x4 b[NGW][2];                  // weight fragments, halves k 0..31 / 32..63
-};
-
-// one stage's loads: plane piece c = wave + 8 i is (row block c / 2NP, plane (c / 2) % NP, half
-// c % 2) of the tile's row blocks; past the range the descriptors have no records (loads
-// return 0, no traffic), so the loads need no branch
-template <int NP, int RB, int NGW>
-__device__ __forceinline__ void gw_load(GwRegs<NP, RB, NGW>& r, __amdgpu_buffer_rsrc_t X, __amdgpu_buffer_rsrc_t W,
-                                        int pbytes, int KB, int s, int wave, int lane) {
-    using C = GwCfg<NP, RB, NGW>;
-#pragma unroll
-    for (int i = 0; i < C::NA; i++) {
-        const int c = wave + C::NWV * i;
-        const int rb = c / (NP * 2), p = (c >> 1) % NP, t = c & 1;
-        r.a[i] = __builtin_amdgcn_raw_buffer_load_b128(X, lane * 16, (rb * 3 + p) * pbytes + (s * 2 + t) * 1024, 0);
-    }
-#pragma unroll
-    for (int g = 0; g < NGW; g++)
-#pragma unroll
-        for (int t = 0; t < 2; t++)
-            r.b[g][t] = __builtin_amdgcn_raw_buffer_load_b128(W, lane * 16 + t * 1024, (g * KB + s) * 2048, 2);
-}
-
-// one stage's MFMAs: 2 RB / 2 steps (half t, row block i), each NGW x NP MFMAs on the weight
-// registers and NP plane fragments read from the LDS slot; the next step's fragments are read
-// under the current step's MFMAs (two fragment sets: the compiler would otherwise hoist every
-// read of the stage and hold 24 fragments)
-template <int NP, int RB, int NGW>
-__device__ __forceinline__ void gw_read(const uint16_t* slot, int wm, int lane, int k, bf16x8 (&x)[NP]) {
-    using C = GwCfg<NP, RB, NGW>;
-    const int t = k / C::RBW, rb = wm * C::RBW + k % C::RBW;
-#pragma unroll
-    for (int p = 0; p < NP; p++) x[p] = *reinterpret_cast<const bf16x8*>(slot + ((rb * NP + p) * 2 + t) * 512 + lane * 8);
-}
-
-template <int NP, int RB, int NGW>
-__device__ __forceinline__ void gw_mma(const uint16_t* slot, const GwRegs<NP, RB, NGW>& r, int wm, int lane,
-                                       f32x4 (&acc)[GwCfg<NP, RB, NGW>::RBW][NGW]) {
-    using C = GwCfg<NP, RB, NGW>;
-    constexpr int STEPS = 2 * C::RBW;
-    bf16x8 xa[NP], xb[NP];
-    gw_read<NP, RB, NGW>(slot, wm, lane, 0, xa);
-#pragma unroll
-    for (int k = 0; k < STEPS; k++) {
-        bf16x8(&cur)[NP] = (k & 1) ? xb : xa;
-        bf16x8(&nxt)[NP] = (k & 1) ? xa : xb;
-        if (k + 1 < STEPS) gw_read<NP, RB, NGW>(slot, wm, lane, k + 1, nxt);
-        __builtin_amdgcn_sched_barrier(0);
-        const int t = k / C::RBW, i = k % C::RBW;
-#pragma unroll
-        for (int g = 0; g < NGW; g++)
-#pragma unroll
-            for (int p = 0; p < NP; p++)
-                acc[i][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.b[g][t]), cur[p], acc[i][g],
-                                                                     0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// stages [s0, s1) of tile (mt, nt) into acc: loads one stage ahead, planes through the 2-slot
-// ring (stage s0 + j in slot j % 2), one barrier per stage
-template <int NP, int RB, int NGW>
-__device__ __forceinline__ void gw_stages(const GemmfArgs& a, uint16_t* lds, int mt, int nt, int s0, int s1,
-                                          f32x4 (&acc)[GwCfg<NP, RB, NGW>::RBW][NGW]) {
-    using C = GwCfg<NP, RB, NGW>;
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int KB = a.K >> 6;
-    const int pbytes = SK_ROWS * a.K * 2;  // one plane of a row block
-    const __amdgpu_buffer_rsrc_t X = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(a.xs) + (size_t)mt * RB * 3 * SK_ROWS * a.K, 0, RB * 3 * pbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t W = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(a.W) + (size_t)(nt * 4 + wn) * NGW * KB * 2048, 0, NGW * KB * 2048, 0x00020000);
-    const __amdgpu_buffer_rsrc_t Xz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.xs), 0, 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t Wz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.W), 0, 0, 0x00020000);
-    GwRegs<NP, RB, NGW> R0, R1;
-    gw_load<NP, RB, NGW>(R0, X, W, pbytes, KB, s0, wave, lane);
-    for (int s = s0; s < s1; s += 2) {
-        // stage s (registers R0, slot 0): planes into LDS, then every wave's pieces are in
-#pragma unroll
-        for (int i = 0; i < C::NA; i++)
-            *reinterpret_cast<u32x4*>(lds + (wave + C::NWV * i) * 512 + lane * 8) = R0.a[i];
-        wait_lgkm0();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        {
-            const bool in = s + 1 < s1;
-            gw_load<NP, RB, NGW>(R1, in ? X : Xz, in ? W : Wz, pbytes, KB, in ? s + 1 : 0, wave, lane);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        gw_mma<NP, RB, NGW>(lds, R0, wm, lane, acc);
-        __builtin_amdgcn_sched_barrier(0);
-        if (s + 1 >= s1) break;
-        // stage s + 1 (R1, slot 1)
-#pragma unroll
-        for (int i = 0; i < C::NA; i++)
-            *reinterpret_cast<u32x4*>(lds + C::SLOT + (wave + C::NWV * i) * 512 + lane * 8) = R1.a[i];
-        wait_lgkm0();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        {
-            const bool in = s + 2 < s1;
-            gw_load<NP, RB, NGW>(R0, in ? X : Xz, in ? W : Wz, pbytes, KB, in ? s + 2 : 0, wave, lane);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        gw_mma<NP, RB, NGW>(lds + C::SLOT, R1, wm, lane, acc);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // the ring is reused by the next range: every wave done reading before anyone writes
-    wait_lgkm0();
-    __builtin_amdgcn_s_barrier();
-}
-
-template <int EPI, int NP, int RB, int NGW>
-__global__ __launch_bounds__(512, 1) void k_gemmw(const GemmfArgs a) {
-    using C = GwCfg<NP, RB, NGW>;
-    constexpr int RBW = C::RBW, TILE = C::TILE;
-    extern __shared__ __attribute__((aligned(16))) uint16_t gw_lds[];
-    int* s_ok = reinterpret_cast<int*>(gw_lds + 2 * C::SLOT);  // one word past the ring (same array)
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int G = gridDim.x, b = blockIdx.x;
-    const long long u0 = gf_bound(a.U, G, b), u1 = gf_bound(a.U, G, b + 1);
-    const int rbm = (a.M + 15) >> 4;
-    const __amdgpu_buffer_rsrc_t Ws = __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, 0x7fffffff, 0x00020000);
-    auto poff = [&](int slotb, int i, int g) {
-        return (int)(((size_t)slotb * TILE + ((size_t)(wave * RBW + i) * NGW + g) * 256 + lane * 4) * 4);
-    };
-    long long u = u0;
-    while (u < u1) {
-        const int t = (int)(u / a.S), s0 = (int)(u % a.S);
-        const int s1 = (int)min((long long)a.S, s0 + (u1 - u));
-        const int mt = a.colmajor ? t % a.MT : t / a.NT, nt = a.colmajor ? t / a.MT : t % a.NT;
-        f32x4 acc[RBW][NGW];
-#pragma unroll
-        for (int i = 0; i < RBW; i++)
-#pragma unroll
-            for (int g = 0; g < NGW; g++) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        gw_stages<NP, RB, NGW>(a, gw_lds, mt, nt, s0, s1, acc);
-        u += s1 - s0;
-        if (s0 > 0) {
-#pragma unroll
-            for (int i = 0; i < RBW; i++)
-#pragma unroll
-                for (int g = 0; g < NGW; g++)
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][g]), Ws, poff(b, i, g), 0, 16);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(&a.flags[b], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            continue;
-        }
-        const long long tend = (long long)(t + 1) * a.S;
-        for (int pb = b + 1; pb < G && gf_bound(a.U, G, pb) < tend; pb++) {
-            if (tid == 0) {
-                int ok = 0;
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                while (a.wait_ticks >= 0) {
-                    if (__hip_atomic_load(&a.flags[pb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch) {
-                        ok = 1;
-                        break;
-                    }
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > (unsigned long long)a.wait_ticks) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (!ok) __hip_atomic_fetch_add(a.recomputes, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                *s_ok = ok;
-            }
-            __syncthreads();
-            const int ok = *s_ok;
-            __syncthreads();
-            if (ok) {
-                f32x4 part[RBW][NGW];
-#pragma unroll
-                for (int i = 0; i < RBW; i++)
-#pragma unroll
-                    for (int g = 0; g < NGW; g++)
-                        part[i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Ws, poff(pb, i, g), 0, 16));
-#pragma unroll
-                for (int i = 0; i < RBW; i++)
-#pragma unroll
-                    for (int g = 0; g < NGW; g++) acc[i][g] += part[i][g];
-            } else {
-                // the publishing block has not run: its stage range computed here.  acc waits in
-                // this block's own partial-tile slot (owners never publish), so one accumulator
-                // set is live through the stages; acc + part, the bits of the published path
-#pragma unroll
-                for (int i = 0; i < RBW; i++)
-#pragma unroll
-                    for (int g = 0; g < NGW; g++) {
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][g]), Ws, poff(b, i, g), 0, 0);
-                        acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const int q0 = (int)(gf_bound(a.U, G, pb) - (long long)t * a.S);
-                const int q1 = (int)(min(gf_bound(a.U, G, pb + 1), tend) - (long long)t * a.S);
-                gw_stages<NP, RB, NGW>(a, gw_lds, mt, nt, q0, q1, acc);
-#pragma unroll
-                for (int i = 0; i < RBW; i++)
-#pragma unroll
-                    for (int g = 0; g < NGW; g++)
-                        acc[i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Ws, poff(b, i, g), 0, 0)) + acc[i][g];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < RBW; i++) {
-            const int rb = mt * RB + wm * RBW + i;
-            if (rb >= rbm) break;
-            const int m = rb * 16 + (lane & 15);
-            if (m >= a.M) continue;
-#pragma unroll
-            for (int g = 0; g < NGW; g += (EPI == EPI_SWIGLU ? 2 : 1))
-                gf_out<EPI>(a, m, (nt * 4 + wn) * NGW + g, lane, acc[i][g], acc[i][EPI == EPI_SWIGLU ? g + 1 : g]);
         }
     }
 }
@@ -653,28 +414,7 @@ static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int EPI, int NP, int RB, int NGW>
-static hipError_t gemmw_launch(const GemmfArgs& a, int G, hipStream_t st) {
-    using C = GwCfg<NP, RB, NGW>;
-    static bool attr = false;
-    const size_t lds = (size_t)2 * C::SLOT * 2 + 16;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemmw<EPI, NP, RB, NGW>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    hipLaunchKernelGGL((k_gemmw<EPI, NP, RB, NGW>), dim3(G), dim3(512), lds, st, a);
-    return hipGetLastError();
-}
-
-// k_gemmw (weights in registers) in place of k_gemmf: -1 reads VOX_HIP_GEMMW once (1 = on);
-// g_gemmw_rb / g_gemmw_ngw (tools/kbench): force the tile (0 = by shape)
-int g_gemmw = -1, g_gemmw_rb = 0, g_gemmw_ngw = 0;
-
-// one partial tile per block: k_gemmf's (4 WR x RB / WR x 2 x 256 floats) or k_gemmw's 128 x 256
-// (8 x 4 x 4 x 256), whichever is larger
-size_t gemmf_ws_floats(int blocks) { return (size_t)blocks * (8 * 4 * 4 * 256); }
+size_t gemmf_ws_floats(int blocks) { return (size_t)blocks * (8 * 2 * 4 * 256); }
 
 int gemmf_grid() {
     if (!g_cus) {
@@ -702,64 +442,12 @@ int set_gemmf_wait(int ticks) {
 
 bool gemmf_ok(int M, int N, int K) { return M > 0 && M <= 1024 && K % 64 == 0 && N % 128 == 0; }
 
-// k_gemmw's tile by shape: 128 rows (RB 8) unless the rows fit 64, 256 columns (NGW 4) when N
-// allows; the unit order, the stream-K grid and the owner rule as in k_gemmf
-hipError_t launch_gemmw(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
-                        float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
-                        hipStream_t st, int max_blocks) {
-    if (!gemmf_ok(M, N, K) || (np != 2 && np != 3) || !ws || !flags) return hipErrorInvalidValue;
-    const int RB = g_gemmw_rb ? g_gemmw_rb : (M > 64 ? 8 : 4);
-    const int NGW = g_gemmw_ngw ? g_gemmw_ngw : (N % 256 == 0 ? 4 : 2);
-    if ((RB != 4 && RB != 8) || (NGW != 2 && NGW != 4) || N % (64 * NGW)) return hipErrorInvalidValue;
-    GemmfArgs a;
-    a.xs = xs; a.K = K; a.M = M; a.W = static_cast<const uint8_t*>(Wf); a.N = N; a.bias = bias; a.C = C; a.ldc = ldc;
-    a.xo = xo; a.ws = ws; a.flags = flags; a.epoch = epoch;
-    a.recomputes = flags + gemmf_grid();
-    a.wait_ticks = g_gemmf_wait;
-    a.S = K / 64;
-    a.NT = N / (64 * NGW);
-    a.MT = (M + 16 * RB - 1) / (16 * RB);
-    a.T = a.MT * a.NT;
-    if (g_gemmf_order < 0) {
-        const char* e = getenv("VOX_HIP_GEMMF_ORDER");
-        const int v = e ? atoi(e) : 0;
-        g_gemmf_order = (v == 1 || v == 2) ? v : 0;
-    }
-    a.colmajor = g_gemmf_order == 1;
-    a.U = (long long)a.T * a.S;
-    const long long minu = g_gemmf_minu ? g_gemmf_minu : std::max(4, (a.S + 1) / 2);
-    int G = gemmf_grid();
-    if (max_blocks > 0 && max_blocks < G) G = max_blocks;
-    if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
-    if ((size_t)G * 8 * (RB / 2) * NGW * 256 > ws_floats) return hipErrorInvalidConfiguration;  // workspace too small
-#define GW_CFG(E, P)                                                                      \
-    if (RB == 8 && NGW == 4) return gemmw_launch<E, P, 8, 4>(a, G, st);                   \
-    if (RB == 8 && NGW == 2) return gemmw_launch<E, P, 8, 2>(a, G, st);                   \
-    if (RB == 4 && NGW == 4) return gemmw_launch<E, P, 4, 4>(a, G, st);                   \
-    return gemmw_launch<E, P, 4, 2>(a, G, st);
-#define GW_EPI(E)                                                                         \
-    if (epi == E) {                                                                       \
-        if (np == 3) { GW_CFG(E, 3) }                                                     \
-        GW_CFG(E, 2)                                                                      \
-    }
-    GW_EPI(EPI_STORE) GW_EPI(EPI_RESID) GW_EPI(EPI_GELU) GW_EPI(EPI_GELU_ERF) GW_EPI(EPI_SWIGLU)
-#undef GW_EPI
-#undef GW_CFG
-    return hipErrorInvalidValue;
-}
-
 hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
                         float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
-                        hipStream_t st, int max_blocks) {
+                        hipStream_t st) {
     // tiles: 128 x 128 with two planes; 64 x 128 with three (a 3-slot ring of 8 row blocks'
     // three planes would not fit the 160 KB of LDS); 16 waves with two planes (g_gemmf_wr),
     // 8 with three
-    if (g_gemmw < 0) {
-        const char* e = getenv("VOX_HIP_GEMMW");
-        g_gemmw = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    if (g_gemmw && gemmf_ok(M, N, K) && (np == 2 || np == 3) && ws && flags)
-        return launch_gemmw(epi, np, xs, K, M, Wf, N, bias, C, ldc, xo, ws, ws_floats, flags, epoch, st, max_blocks);
     constexpr int NG = 2, WR = 2;
     if (g_gemmf_rb < 0) {
         // VOX_HIP_GEMMF_RB=4: 64-row tiles on every shape (a 96 KB LDS ring instead of 144 KB,
@@ -787,23 +475,23 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     a.NT = N / (64 * NGx);
     a.MT = (M + 16 * RB - 1) / (16 * RB);
     a.T = a.MT * a.NT;
-    // unit order: with three planes (64-row tiles) a row-tile count that is not a multiple of
-    // 4 above 4 (M = 400 / 677 / 800: 7 / 11 / 13 tiles) runs the row-tile-major order 1.2-1.7x
-    // slower than the column-tile-major one (a weight tile's row tiles adjacent); at 2, 4, 8
-    // and 16 row tiles the row-tile-major order is 1-7 % faster (tools/kbench,
-    // profiles/r5_kbench_gemmf_order_m.txt).  VOX_HIP_GEMMF_ORDER / g_gemmf_order: 1 / 2 force either.
+    // unit order: with three planes (64-row tiles) and more than 4 row tiles the row-tile-major
+    // order runs 1.2-2.2x slower than the column-tile-major one (a weight tile's row tiles
+    // adjacent) on the encoder shapes at 7 / 11 / 13 row tiles (M = 400 / 677 / 800) and on the
+    // decoder's (K >= 3072, the stacked prefills) at 7 and 11; at 8 and 16 row tiles of the
+    // encoder shapes it is 1-7 % faster (tools/kbench, profiles/r5_kbench_gemmf_order_m.txt,
+    // r5_kbench_gemmfx.txt).  VOX_HIP_GEMMF_ORDER / g_gemmf_order: 1 / 2 force either.
     if (g_gemmf_order < 0) {
         const char* e = getenv("VOX_HIP_GEMMF_ORDER");
         const int v = e ? atoi(e) : 0;
         g_gemmf_order = (v == 1 || v == 2) ? v : 0;
     }
-    a.colmajor = g_gemmf_order ? g_gemmf_order == 1 : (np == 3 && a.MT > 4 && a.MT % 4 != 0);
+    a.colmajor = g_gemmf_order ? g_gemmf_order == 1 : (np == 3 && a.MT > 4 && (a.MT % 4 != 0 || K > 2048));
     a.U = (long long)a.T * a.S;
     // one block per CU, but every block at least half a tile's stages (and 4): a tile split
     // over many blocks costs its owner one partial-tile read per extra block
     const long long minu = g_gemmf_minu ? g_gemmf_minu : std::max(4, (a.S + 1) / 2);
     int G = gemmf_grid();
-    if (max_blocks > 0 && max_blocks < G) G = max_blocks;
     if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
     // one partial tile per block: (4 WR waves) x (RB / WR) x NGx x 64 lanes x 4 floats
     if ((size_t)G * 4 * RB * NGx * 256 > ws_floats) return hipErrorInvalidConfiguration;  // workspace too small

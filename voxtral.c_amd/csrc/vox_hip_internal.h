@@ -242,23 +242,16 @@ hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const v
                             const SklFused& f, hipStream_t st);
 // k_gemmf (vox_hip_gemmf.hip): stream-K MFMA GEMM, planes x fragment-major bf16 weights;
 // epi in {STORE, RESID, GELU, GELU_ERF, SWIGLU}; SWIGLU with xo writes the gate rows as
-// planes [rb][3][16][N / 2].  ws: gemmf_ws_floats(gemmf_grid()) floats of partial tiles (either kernel),
+// planes [rb][3][16][N / 2].  ws: gemmf_ws_floats(gemmf_grid()) floats of partial tiles,
 // flags: gemmf_grid() ints (zeroed once), epoch: > 0, new for every launch on the stream.
 bool gemmf_ok(int M, int N, int K);
 int gemmf_grid();
 size_t gemmf_flag_ints();      // flags buffer: gemmf_grid() flags, then the recompute counter
 int set_gemmf_wait(int ticks); // owner's wait per partial in 100 MHz ticks (< 0: always recompute); returns the old
 size_t gemmf_ws_floats(int blocks);
-// max_blocks > 0: the stream-K grid is at most that many blocks (a queue restricted to that
-// many CUs, vox_hip_stream_set_cu_share)
 hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
                         float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
-                        hipStream_t st, int max_blocks = 0);
-// k_gemmw: the same GEMM with the weight operand in registers (128 x 256 tiles by default);
-// launch_gemmf routes here when VOX_HIP_GEMMW=1
-hipError_t launch_gemmw(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,
-                        float* C, int ldc, uint16_t* xo, float* ws, size_t ws_floats, int* flags, int epoch,
-                        hipStream_t st, int max_blocks = 0);
+                        hipStream_t st);
 int gemm_planes_np();  // activation planes of the M > 1 GEMMs (2, or 3 with VOX_HIP_GEMM_PLANES=3)
 int set_gemm_planes(int np);  // 2 or 3 (vox_hip_set_gemm_planes); -1 otherwise
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,

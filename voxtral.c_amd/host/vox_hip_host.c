@@ -1009,11 +1009,6 @@ void vh_sched_free(vh_sched_t *q) {
     free(q);
 }
 
-static int sched_enc_cus(void) {
-    const char *e = getenv("VOX_HIP_SCHED_ENC_CUS");
-    return e ? atoi(e) : 0;
-}
-
 int vh_sched_attach(vh_sched_t *q, vh_stream_t *s) {
     if (!q || !s || s->ctx->model != q->ctx->model) return fail("vh_sched_attach: stream of another model");
     if (s->sched == q) return 0;
@@ -1024,11 +1019,6 @@ int vh_sched_attach(vh_sched_t *q, vh_stream_t *s) {
     const char *ae = getenv("VOX_HIP_SCHED_ASYNC");
     if (vox_hip_stream_set_async_encode(s->st, !(ae && atoi(ae) == 0)))
         return fail("async encode: %s", vox_hip_last_error());
-    /* VOX_HIP_SCHED_ENC_CUS=n: the attached streams' queues (their encoder chunks and the
-     * cross-stream encoder pass) on CUs [0, n), the batched steps on the others */
-    const int ecus = sched_enc_cus();
-    if (ecus > 0 && vox_hip_stream_set_cu_share(s->st, 0, ecus))
-        return fail("cu share: %s", vox_hip_last_error());
     q->s[q->n++] = s;
     s->sched = q;
     return 0;
@@ -1041,8 +1031,6 @@ int vh_sched_detach(vh_sched_t *q, vh_stream_t *s) {
             q->s[i] = q->s[--q->n];
             s->sched = NULL;
             if (rc) return -1;
-            if (sched_enc_cus() > 0 && vox_hip_stream_set_cu_share(s->st, 0, 0))
-                return fail("cu share: %s", vox_hip_last_error());
             return vox_hip_stream_set_async_encode(s->st, 0) ? fail("async encode: %s", vox_hip_last_error()) : 0;
         }
     return fail("vh_sched_detach: stream not attached");
@@ -1106,12 +1094,6 @@ static int sched_steps(vh_sched_t *q, int bounded, const int *rows, const int *r
         if (!q->batch) {
             q->batch = vox_hip_batch_create(q->ctx->model, q->cap);
             if (!q->batch) return fail("batch: %s", vox_hip_last_error());
-            /* the batched steps on the CUs the encoder queues do not use (VOX_HIP_SCHED_ENC_CUS;
-             * VOX_HIP_SCHED_BATCH_ALL_CUS=1 leaves them every CU) */
-            const char *ba = getenv("VOX_HIP_SCHED_BATCH_ALL_CUS");
-            if (sched_enc_cus() > 0 && !(ba && atoi(ba) == 1) &&
-                vox_hip_batch_set_cu_share(q->batch, sched_enc_cus(), -1))
-                return fail("batch cu share: %s", vox_hip_last_error());
         }
         const double t0 = now_ms();
         const int cap = q->step_cap > 0 && q->step_cap < VH_SCHED_STEPS ? q->step_cap : VH_SCHED_STEPS;

@@ -38,7 +38,6 @@ EXPORTS = [
     "vox_hip_last_error", "vox_hip_clear_error", "vox_hip_set_device", "vox_hip_config_voxtral_4b",
     "vox_hip_model_create", "vox_hip_model_free", "vox_hip_model_set_delay",
     "vox_hip_model_ada_scale", "vox_hip_model_set_kv_fp16", "vox_hip_stream_kv_fp16",
-    "vox_hip_stream_set_cu_share", "vox_hip_batch_set_cu_share",
     "vox_hip_set_gemm_planes", "vox_hip_gemm_planes", "vox_hip_set_gemmf_wait",
     "vox_hip_stream_create", "vox_hip_stream_free",
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
@@ -77,7 +76,6 @@ def lib():
         "vox_hip_model_create": (P, [P, P, I]), "vox_hip_model_free": (None, [P]),
         "vox_hip_model_set_delay": (I, [P, I]), "vox_hip_model_ada_scale": (I, [P, fp]),
         "vox_hip_model_set_kv_fp16": (I, [P, I]), "vox_hip_stream_kv_fp16": (I, [P]),
-        "vox_hip_stream_set_cu_share": (I, [P, I, I]), "vox_hip_batch_set_cu_share": (I, [P, I, I]),
         "vox_hip_set_gemm_planes": (I, [I]), "vox_hip_gemm_planes": (I, []),
         "vox_hip_set_gemmf_wait": (I, [I]),
         "vox_hip_stream_create": (P, [P]), "vox_hip_stream_free": (None, [P]),

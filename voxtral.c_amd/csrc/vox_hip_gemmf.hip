@@ -489,8 +489,14 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     a.colmajor = g_gemmf_order ? g_gemmf_order == 1 : (np == 3 && a.MT > 4 && (a.MT % 4 != 0 || K > 2048));
     a.U = (long long)a.T * a.S;
     // one block per CU, but every block at least half a tile's stages (and 4): a tile split
-    // over many blocks costs its owner one partial-tile read per extra block
-    const long long minu = g_gemmf_minu ? g_gemmf_minu : std::max(4, (a.S + 1) / 2);
+    // over many blocks costs its owner one partial-tile read per extra block.  One or two row
+    // tiles (M <= 128 with three planes: prefills, the flush chunk) leave too few tiles for
+    // that: an eighth of a tile (and 6) spreads the weights over 2-4x the CUs -- decoder prefill
+    // M = 38: wo 25.3 -> 15.8, w2 48.6 -> 22.3, QKV 20.5 -> 15.6 us; encoder M = 25-70: wo 15.3
+    // -> 11.5-12.9, w2 28.9 -> 16.2-17.5 us; at 7+ row tiles the half-tile rule stays faster
+    // (tools/kbench VOX_KB_ONLY=gemmfm, profiles/r5_kbench_gemmf_minu.txt)
+    const long long minu = g_gemmf_minu ? g_gemmf_minu
+                           : a.MT <= 2 ? std::max(6, a.S / 8) : std::max(4, (a.S + 1) / 2);
     int G = gemmf_grid();
     if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
     // one partial tile per block: (4 WR waves) x (RB / WR) x NGx x 64 lanes x 4 floats

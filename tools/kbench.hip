@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb, g_gemmf_wr3; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -566,16 +566,17 @@ int main(int argc, char** argv) {
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
                         G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
                 for (int v = 0; v < 4; v++) {
-                    // np3 (RB4, 8 waves) in the row-tile-major and the column-tile-major unit
-                    // order, twice; earlier variants: profiles/r4_kbench_gemmf*.txt, r5_kbench_gemmf_order.txt
+                    // np3 (RB4), 8 or 16 waves, unit order by shape, twice; earlier variants:
+                    // profiles/r4_kbench_gemmf*.txt, r5_kbench_gemmf_order*.txt
                     const int np = 3;
-                    g_gemmf_order = (v & 1) ? 1 : 2;
+                    g_gemmf_wr3 = (v & 1) ? 4 : 2;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
-                    printf("gemmf %-4s M=%4d %dx%d np%d %s %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
-                           g.K, np, g_gemmf_order == 1 ? "colmajor" : "rowmajor", us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                    printf("gemmf %-4s M=%4d %dx%d np%d %d waves %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
+                           g.K, np, 4 * g_gemmf_wr3, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
+                g_gemmf_wr3 = 2;
                 g_gemmf_order = 0;  // by shape
             }
     }

@@ -11,7 +11,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb, g_gemmf_wr3; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -557,26 +557,29 @@ int main(int argc, char** argv) {
         const size_t wsn = 2 * gemmf_ws_floats(gemmf_grid());
         float* gws = (float*)dmalloc(wsn * 4, 0);
         int* gfl = (int*)dmalloc(4096 * 4, 0);
-        uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 5120 * 2, 1);
-        uint16_t* go = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 5120 * 2, 0);
-        float* gc = (float*)dmalloc((size_t)1024 * 10240 * 4, 0);
+        uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 1);
+        uint16_t* go = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 0);
+        float* gc = (float*)dmalloc((size_t)1024 * 18432 * 4, 0);
         int epoch = 0;
         struct G { const char* n; int epi, N, K; const uint16_t* W; };
-        for (int M : {70, 256, 400, 512, 677, 800, 1024})
+        for (int M : {256, 400, 512, 677, 1024})
             for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
-                        G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]}}) {
-                for (int v = 0; v < 4; v++) {
-                    // np3 (RB4), 8 or 16 waves, unit order by shape, twice; earlier variants:
-                    // profiles/r4_kbench_gemmf*.txt, r5_kbench_gemmf_order*.txt
+                        G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]},
+                        G{"dqkv", EPI_STORE, 6144, 3072, wqkv[3]}, G{"dw13", EPI_SWIGLU, 18432, 3072, w13[3]}}) {
+                if (g.n[0] == 'd' && M != 400 && M != 677) continue;
+                for (int v = 0; v < 6; v++) {
+                    // np3 (RB4): unit order by shape / column-major / row-major, twice (XCD-grouped
+                    // tiles: profiles/r5_kbench_gemmf_xcdgrp.txt);
+                    // earlier: profiles/r4_kbench_gemmf*.txt, r5_kbench_gemmf_order*.txt
                     const int np = 3;
-                    g_gemmf_wr3 = (v & 1) ? 4 : 2;
+                    g_gemmf_order = v % 3;
                     double us = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, g.epi == EPI_SWIGLU ? g.N / 2 : g.N,
                                                              g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
-                    printf("gemmf %-4s M=%4d %dx%d np%d %d waves %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
-                           g.K, np, 4 * g_gemmf_wr3, us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
+                    static const char* on[3] = {"auto", "col", "row"};
+                    printf("gemmf %-4s M=%4d %dx%d np%d %-6s %9.2f us  %8.1f TFLOP/s (useful)  %6.1f%% of bf16 peak (issued)\n", g.n, M, g.N,
+                           g.K, np, on[v % 3], us, 2.0 * M * g.N * g.K / us / 1e6, 100.0 * np * 2.0 * M * g.N * g.K / us / 1e6 / 2500.0);
                     fflush(stdout);
                 }
-                g_gemmf_wr3 = 2;
                 g_gemmf_order = 0;  // by shape
             }
     }

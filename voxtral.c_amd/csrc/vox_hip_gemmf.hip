@@ -90,20 +90,11 @@ struct GfCfg {
     static constexpr int RBW = RB / WR;             // row blocks per wave
     static constexpr int CH = RB * NP * 2;          // 1 KiB plane chunks per stage
     static constexpr int CW = 4 * NG * 2;           // 1 KiB weight chunks per stage (4 column slots)
-    static constexpr int NA = (CH + NWV - 1) / NWV; // plane chunks per wave (waves >= CH % NWV take one
-    static constexpr int NAX = CH % NWV;            //  fewer when CH % NWV != 0: three planes on 16 waves)
+    static constexpr int NA = CH / NWV;             // plane chunks per wave
     static constexpr int NB = CW / NWV;             // weight chunks per wave
     static constexpr int SLOT = (CH + CW) * 512;    // bf16 elements per LDS slot: planes, then weights
-    static_assert(CW % NWV == 0 && RB % WR == 0, "weight chunks must split over the waves");
+    static_assert(CH % NWV == 0 && CW % NWV == 0 && RB % WR == 0, "chunks must split over the waves");
 };
-
-// s_waitcnt vmcnt(K stages of this wave's loads): a wave past C::NAX issues one plane chunk
-// fewer per stage (wave-uniform branch)
-template <class C, int K>
-__device__ __forceinline__ void wait_stages(int wave) {
-    if (C::NAX && wave >= C::NAX) wait_vm<K * (C::NA - 1 + C::NB)>();
-    else wait_vm<K * (C::NA + C::NB)>();
-}
 
 // one stage's loads into ring slot SL, all LDS-DMA (no VGPR-destination load in the loop:
 // hipcc waits vmcnt(0) at the use of one, which would drain the DMA ring every stage)
@@ -116,7 +107,6 @@ __device__ __forceinline__ void gf_issue(const uint16_t* xb, size_t plane, const
 #pragma unroll
     for (int i = 0; i < C::NA; i++) {
         const int c = wave + C::NWV * i;  // chunk: row block c / (2 NP), plane (c / 2) % NP, half c % 2
-        if (C::NAX && c >= C::CH) break;  // wave-uniform
         const int rb = c / (NP * 2), p = (c >> 1) % NP, t = c & 1;
         const uint16_t* src = xb + ((size_t)rb * 3 + p) * plane + (size_t)(s * 2 + t) * 512 + lane * 8;
         __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(dst + c * 512), 16, 0, 0);
@@ -197,8 +187,8 @@ __device__ __forceinline__ void gf_stages(const GemmfArgs& a, uint16_t* lds, int
     if (s0 + 2 < s1) gf_issue<NP, RB, NG, WR, 2>(xb, plane, wt, KB, s0 + 2, lds, wave, lane);
     // stage s0's DMA landed (stages s0 + 1, s0 + 2 may stay in flight)
     if (VOX_GF_DIAG == 2) {
-    } else if (s0 + 2 < s1) wait_stages<C, 2>(wave);
-    else if (s0 + 1 < s1) wait_stages<C, 1>(wave);
+    } else if (s0 + 2 < s1) wait_vm<2 * (C::NA + C::NB)>();
+    else if (s0 + 1 < s1) wait_vm<C::NA + C::NB>();
     else wait_vm<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -214,7 +204,7 @@ __device__ __forceinline__ void gf_stages(const GemmfArgs& a, uint16_t* lds, int
         wait_lgkm0();                                                                                            \
         if (s + J + 1 < s1) {                                                                                    \
             if (VOX_GF_DIAG == 2) {                                                                              \
-            } else if (s + J + 2 < s1) wait_stages<C, 1>(wave);                                                  \
+            } else if (s + J + 2 < s1) wait_vm<C::NA + C::NB>();                                                 \
             else wait_vm<0>();                                                                                   \
             asm volatile("" ::: "memory");                                                                       \
             __builtin_amdgcn_s_barrier();                                                                        \
@@ -408,10 +398,6 @@ int g_gemmf_order = -1;  // 1 = column-tile-major unit order (a weight tile's ro
 // kbench (profiles/r4_kbench_gemmf_wr4.txt): M = 677 W1|W3 47.9 -> 44.6, W2 25.6 -> 23.8 us,
 // QKV / wo equal; M = 1024 W1|W3 54.5 -> 48.4 us.  Three planes keep 8 (24 chunks a stage).
 int g_gemmf_wr = -1;
-// three planes: 8 waves (2 per SIMD, 64 x 32 per wave) by default; 4 = 16 waves (4 per SIMD,
-// 16 x 32 per wave, the 24 plane chunks of a stage spread 2 / 1 over the waves); -1 reads
-// VOX_HIP_GEMMF_WR3 once
-int g_gemmf_wr3 = -1;
 
 template <int EPI, int NP, int RB, int NG, int WR>
 static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
@@ -517,8 +503,7 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     if ((size_t)G * 4 * RB * NGx * 256 > ws_floats) return hipErrorInvalidConfiguration;  // workspace too small
 #define GF_EPI(E)                                                                               \
     if (epi == E)                                                                               \
-        return np == 3 ? (g_gemmf_wr3 == 4 ? gemmf_launch<E, 3, 4, NG, 4>(a, G, st)              \
-                                           : gemmf_launch<E, 3, 4, NG, WR>(a, G, st))            \
+        return np == 3 ? gemmf_launch<E, 3, 4, NG, WR>(a, G, st)                                \
                : g_gemmf_wr == 4 ? (RB == 8 ? gemmf_launch<E, 2, 8, NG, 4>(a, G, st)             \
                                             : gemmf_launch<E, 2, 4, NG, 4>(a, G, st))            \
                : RB == 8 ? gemmf_launch<E, 2, 8, NG, WR>(a, G, st) : gemmf_launch<E, 2, 4, NG, WR>(a, G, st);
@@ -526,10 +511,7 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
         const char* e = getenv("VOX_HIP_GEMMF_WR");
         g_gemmf_wr = (e && atoi(e) == 2) ? 2 : 4;
     }
-    if (g_gemmf_wr3 < 0) {
-        const char* e = getenv("VOX_HIP_GEMMF_WR3");
-        g_gemmf_wr3 = (e && atoi(e) == 4) ? 4 : 2;
-    }
+
     GF_EPI(EPI_STORE) GF_EPI(EPI_RESID) GF_EPI(EPI_GELU) GF_EPI(EPI_GELU_ERF) GF_EPI(EPI_SWIGLU)
 #undef GF_EPI
     return hipErrorInvalidValue;

@@ -3045,6 +3045,10 @@ hipError_t launch_slabs_rope_kv(const float* part, int S, int M, const float* bi
     return hipSuccess;
 }
 
+#ifdef VOX_GEMV_STAMPS
+// diagnostic build only (tools/kbench_stamps): where k_gemv's per-block stamps go (null: off)
+hipError_t gemv_set_stamps(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_gemv_stamps), &p, sizeof p); }
+#endif
 int g_gemv_rb = 0;  // tools/kbench knob: force 4- or 8-row groups (0 = automatic)
 // Rows per group: each block should stream at least two groups, so that the next group's
 // loads overlap this group's reduction and epilogue (one group per block left every block

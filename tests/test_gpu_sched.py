@@ -355,3 +355,52 @@ def test_host_stream_reset_reuses_like_fresh(tiny_weights, jfk_samples):
     ctx.close()
     hm.close()
     om.close()
+
+
+def _single_stream_ids(ctx, audio, interval):
+    """The same pieces through one vh_stream_t with no scheduler: its own encoder chunks and the
+    single-stream decode path (vox_hip_stream_decode, pinned to the oracle by test_gpu_full)."""
+    import vox_hip
+    s = vox_hip.HostStream(ctx, interval_s=interval)
+    ids = []
+    for i in range(0, len(audio), PIECE):
+        s.feed(audio[i:i + PIECE])
+        ids += s.get()
+    s.finish()
+    ids += s.get()
+    s.close()
+    return ids
+
+
+def test_scheduler_full_size_16_streams_match_single_stream(jfk_samples):
+    """The served mix the C4 bench runs, at full Voxtral-4B shapes (the
+    full-size served parity had covered 3 short streams): 16 streams of 6-22 s, starts staggered
+    by one tick, a step cap of 8 (bench.py --stagger), cross-stream encoder passes beside the
+    slot-table batched steps; every stream's ids equal the same audio run alone through the
+    single-stream path -- itself pinned to the CPU oracle at full size -- so the batched,
+    stacked-prefill and overlapped machinery adds nothing of its own at this scale (an oracle
+    run of ~200 s of audio would take the CPU most of an hour)."""
+    import vox_hip
+    from vox_weights import VOXTRAL_4B, synth_weights
+    w = synth_weights(VOXTRAL_4B, seed=0)
+    hm = vox_hip.Model(VOXTRAL_4B, w)
+    del w
+    long = np.concatenate([jfk_samples] * 3)
+    rng = np.random.default_rng(5)
+    audios = []
+    for k in range(16):
+        n = int(16000 * (6 + (k * 7) % 17))
+        off = int(rng.integers(0, len(long) - n))
+        sign = -1.0 if k % 3 == 1 else 1.0
+        audios.append(np.ascontiguousarray(sign * long[off:off + n] * (0.6 + 0.05 * (k % 8))))
+    ids, st = _serve(hm, audios, list(range(16)), 0.5, max_streams=16, step_cap=8)
+    ctx = vox_hip.HostCtx(hm)
+    for k, au in enumerate(audios):
+        ref = _single_stream_ids(ctx, au, 0.5)
+        assert len(ref) > 40, (k, len(ref))
+        assert ids[k] == ref, (k, len(ids[k]), len(ref), next((i for i in range(min(len(ref), len(ids[k])))
+                                                               if ids[k][i] != ref[i]), None))
+    ctx.close()
+    hm.close()
+    assert st["steps"] > 0 and st["tokens"] / st["steps"] > 4, st
+    print("16-stream full-size scheduler stats", st)

@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
 static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = -1;     // row blocks per tile with two planes (0 = by shape; 4 or 8; -1: VOX_HIP_GEMMF_RB once)
-int g_gemmf_minu = 0;    // tools/kbench knob: least stages per block (0 = max(4, half a tile))
+VOX_KB_KNOB(g_gemmf_minu, 0);  // tools/kbench knob: least stages per block (0 = max(4, half a tile))
 int g_gemmf_order = -1;  // 1 = column-tile-major unit order (a weight tile's row tiles adjacent), 2 = row-tile-major, 0 = by shape (-1: VOX_HIP_GEMMF_ORDER once)
 // waves per block with two planes: 16 (4 row shares of a 128- or 64-row tile: 32 x 32 or 16 x
 // 32 per wave, four waves per SIMD) by default, 8 with VOX_HIP_GEMMF_WR=2 (64 x 32 per wave,

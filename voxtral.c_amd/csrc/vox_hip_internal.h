@@ -173,6 +173,13 @@ hipError_t launch_argmax_batch(const float* logits, int nb, int V, float* pval, 
                                float* x, hipStream_t st);
 // Batched decode GEMMs for M <= 16 rows held as three bf16 planes xs[3][16][K] (hi/mid/lo =
 // the exact f32 rows) in MFMA fragment order; weights packed by launch_frag_pack.
+// tools/kbench sweep knobs: variables in a kbench build (-DVOX_KBENCH), compile-time constants
+// (the product's own choice) in the library
+#ifdef VOX_KBENCH
+#define VOX_KB_KNOB(name, v) int name = v
+#else
+#define VOX_KB_KNOB(name, v) constexpr int name = v
+#endif
 constexpr int SK_ROWS = 16;
 constexpr int SK_MAX_ROWS = 96;  // rows of one skinny launch: up to 6 row blocks of 16
                                  // (planes [rb][3][16][K], slabs [rb][S][16][N])

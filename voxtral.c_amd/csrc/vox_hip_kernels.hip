@@ -2937,7 +2937,7 @@ hipError_t launch_rope_kv(const float* qkv, int M, int qd, int kvd, int hd, cons
     return hipSuccess;
 }
 
-int g_attn_blocks = 0;  // tools/kbench knob: target grid size of the key-range split (0 = 512)
+VOX_KB_KNOB(g_attn_blocks, 0);  // tools/kbench knob: target grid size of the key-range split (0 = 512)
 
 hipError_t launch_rope_kv_rows(const float* qkv, int N, int qd, int kvd, int hd, const float* rope_table,
                                const EncRows& er, float* q, int cap, hipStream_t st) {
@@ -3049,7 +3049,7 @@ hipError_t launch_slabs_rope_kv(const float* part, int S, int M, const float* bi
 // diagnostic build only (tools/kbench_stamps): where k_gemv's per-block stamps go (null: off)
 hipError_t gemv_set_stamps(unsigned long long* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_gemv_stamps), &p, sizeof p); }
 #endif
-int g_gemv_rb = 0;  // tools/kbench knob: force 4- or 8-row groups (0 = automatic)
+VOX_KB_KNOB(g_gemv_rb, 0);  // tools/kbench knob: force 4- or 8-row groups (0 = automatic)
 // Rows per group: each block should stream at least two groups, so that the next group's
 // loads overlap this group's reduction and epilogue (one group per block left every block
 // idle at its tail).  tools/kbench, bf16 / 768 blocks: QKV 10.2 -> 8.5 us with 4-row
@@ -3062,7 +3062,7 @@ static int gemv_rb(int rows) {
     return 2;
 }
 
-int g_gemv_maxb = 0;  // tools/kbench knob: grid cap other than GEMV_MAX_BLOCKS (no LM head)
+VOX_KB_KNOB(g_gemv_maxb, 0);  // tools/kbench knob: grid cap other than GEMV_MAX_BLOCKS (no LM head)
 int gemv_grid(int rows) {
     // the largest divisor of the group count that fits 4 blocks per CU: every block then
     // runs the same number of groups (no tail); tools/kbench VOX_KB_ONLY=grid: 1536-2304
@@ -3165,8 +3165,8 @@ hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
 // partial slots per head (at least 4)
 int attn_maxch(int window) { return std::max(4, (window + ATT_MIN_BK - 1) / ATT_MIN_BK); }
 int attn_maxsplits(int window) { return (window + ATT_BK - 1) / ATT_BK; }
-int g_attn_lw = 0;  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
-int g_attn_kvfast = 1;  // long-context grid with the kv heads of a key range adjacent (tools/kbench: 0 = off)
+VOX_KB_KNOB(g_attn_lw, 0);  // tools/kbench knob: waves per long-context block (2 or 4; 0 = ATT_LWAVES)
+VOX_KB_KNOB(g_attn_kvfast, 1);  // long-context grid with the kv heads of a key range adjacent (tools/kbench: 0 = off)
 // batched step, <= 256 keys: 128-key blocks when (stream, kv head) blocks < 256 (16 streams
 // 6582 -> 6695 tok/s, 8 streams 3556 -> 3632; VOX_HIP_ATT_BSPLIT=0: off)
 int g_attn_bsplit = -1;
@@ -3438,7 +3438,10 @@ hipError_t launch_swiglu_fplanes(const float* part, int S, int H, int nb, uint16
 
 // tuning knobs (tools/kbench; 0 = automatic): k_skf row groups per block, waves per block,
 // ring depth; k_skl waves per block
-int g_skf_r = 0, g_skf_nw = 0, g_skf_d = 0, g_skl_nw = 0;
+VOX_KB_KNOB(g_skf_r, 0);
+VOX_KB_KNOB(g_skf_nw, 0);
+VOX_KB_KNOB(g_skf_d, 0);
+VOX_KB_KNOB(g_skl_nw, 0);
 
 template <int Q, int R, int NW, int D>
 static hipError_t skf_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,

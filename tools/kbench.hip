@@ -65,6 +65,78 @@ __global__ __launch_bounds__(256) void k_touch_rows(const uint16_t* __restrict__
     if (acc == 0x9e3779b9u) sink[0] = (int)acc;
 }
 
+// VOX_KB_ONLY=bar: what a launch boundary between dependent weight streams costs.  One decode
+// layer's four weight reads (QKV, wo, W1|W3, W2 sizes) as (A) four launches of a plain streaming
+// kernel in a graph, (B) one launch whose 768 blocks meet at a grid barrier between the reads
+// (a relaxed agent-scope arrival counter, reset by a memset node per replay; 3 blocks per CU,
+// all resident), (C) as B with each block's first loads of the next read issued before it
+// waits at the barrier.
+constexpr int BAR_U = 4;  // 16-B loads per thread in flight per iteration
+typedef unsigned int bar_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 bar_ld(const uint4* p) {
+    const bar_v4 t = __builtin_nontemporal_load(reinterpret_cast<const bar_v4*>(p));
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+struct BarStreams {
+    const uint4* w[4];
+    size_t n16[4];
+};
+__device__ __forceinline__ void bar_first(const uint4* W, size_t n16, int b, int G, uint4 (&v)[BAR_U]) {
+    const size_t per = (n16 + G - 1) / G, s0 = (size_t)b * per, e = min(n16, s0 + per);
+#pragma unroll
+    for (int k = 0; k < BAR_U; k++) {
+        const size_t i = s0 + threadIdx.x + (size_t)k * 256;
+        v[k] = i < e ? bar_ld(W + i) : make_uint4(0, 0, 0, 0);
+    }
+}
+__device__ __forceinline__ unsigned bar_rest(const uint4* W, size_t n16, int b, int G, const uint4 (&v0)[BAR_U]) {
+    const size_t per = (n16 + G - 1) / G, s0 = (size_t)b * per, e = min(n16, s0 + per);
+    unsigned acc = 0;
+#pragma unroll
+    for (int k = 0; k < BAR_U; k++) acc ^= v0[k].x ^ v0[k].y ^ v0[k].z ^ v0[k].w;
+    for (size_t i0 = s0 + BAR_U * 256; i0 < e; i0 += BAR_U * 256) {
+        uint4 v[BAR_U];
+#pragma unroll
+        for (int k = 0; k < BAR_U; k++) {
+            const size_t i = i0 + threadIdx.x + (size_t)k * 256;
+            v[k] = i < e ? bar_ld(W + i) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < BAR_U; k++) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    return acc;
+}
+__global__ __launch_bounds__(256) void k_bar_one(const uint4* W, size_t n16, int* sink) {
+    uint4 v[BAR_U];
+    bar_first(W, n16, blockIdx.x, gridDim.x, v);
+    const unsigned acc = bar_rest(W, n16, blockIdx.x, gridDim.x, v);
+    if (acc == 0x9e3779b9u) sink[0] = (int)acc;
+}
+template <int PF>
+__global__ __launch_bounds__(256) void k_bar_chain(const BarStreams S, int* ctr, int* sink) {
+    const int G = gridDim.x, b = blockIdx.x;
+    unsigned acc = 0;
+    uint4 v[BAR_U];
+    bar_first(S.w[0], S.n16[0], b, G, v);
+    for (int j = 0; j < 4; j++) {
+        acc ^= bar_rest(S.w[j], S.n16[j], b, G, v);
+        if (j == 3) break;
+        if (PF) bar_first(S.w[j + 1], S.n16[j + 1], b, G, v);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int target = (j + 1) * G;
+            long long spins = 0;
+            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++spins < (1 << 22))
+                __builtin_amdgcn_s_sleep(1);
+            if (spins >= (1 << 22)) sink[1] = 1;  // bounded: a missing block is reported, not waited for
+        }
+        __syncthreads();
+        if (!PF) bar_first(S.w[j + 1], S.n16[j + 1], b, G, v);
+    }
+    if (acc == 0x9e3779b9u) sink[0] = (int)acc;
+}
+
 int main(int argc, char** argv) {
     int iters = argc > 1 ? atoi(argv[1]) : 200;
     hipStream_t st;
@@ -129,6 +201,47 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "bar")) {
+        int* ctr = (int*)dmalloc(64, 0);
+        int* sink = (int*)dmalloc(64, 0);
+        const size_t nb[4] = {(size_t)(DQ + 2 * DKV) * D * 2 / 16, (size_t)D * DQ * 2 / 16, (size_t)2 * DH * D * 2 / 16,
+                              (size_t)D * DH * 2 / 16};
+        const double bytes = 16.0 * (nb[0] + nb[1] + nb[2] + nb[3]);
+        for (int G : {768, 512}) {
+            std::vector<hipGraphExec_t> ga(NL), gb(NL), gc(NL);
+            for (int l = 0; l < NL; l++) {
+                const uint4* w[4] = {(const uint4*)wqkv[l], (const uint4*)wo[l], (const uint4*)w13[l], (const uint4*)w2[l]};
+                BarStreams S;
+                for (int j = 0; j < 4; j++) { S.w[j] = w[j]; S.n16[j] = nb[j]; }
+                for (int v = 0; v < 3; v++) {
+                    hipGraph_t g;
+                    CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+                    if (v == 0) {
+                        for (int j = 0; j < 4; j++) hipLaunchKernelGGL(k_bar_one, dim3(G), dim3(256), 0, st, w[j], nb[j], sink);
+                    } else {
+                        CK(hipMemsetAsync(ctr, 0, 4, st));
+                        if (v == 1) hipLaunchKernelGGL(k_bar_chain<0>, dim3(G), dim3(256), 0, st, S, ctr, sink);
+                        else hipLaunchKernelGGL(k_bar_chain<1>, dim3(G), dim3(256), 0, st, S, ctr, sink);
+                    }
+                    CK(hipStreamEndCapture(st, &g));
+                    CK(hipGraphInstantiate(v == 0 ? &ga[l] : v == 1 ? &gb[l] : &gc[l], g, nullptr, nullptr, 0));
+                    CK(hipGraphDestroy(g));
+                }
+            }
+            const char* nm[3] = {"4 launches (graph)", "1 launch, grid barriers", "1 launch, barriers + next loads first"};
+            for (int rep = 0; rep < 2; rep++)
+                for (int v = 0; v < 3; v++) {
+                    std::vector<hipGraphExec_t>& gx = v == 0 ? ga : v == 1 ? gb : gc;
+                    char n[96];
+                    snprintf(n, sizeof n, "bar G=%d %s", G, nm[v]);
+                    add(n, timeit([&] { CK(hipGraphLaunch(gx[layer++ % NL], st)); }, iters, st), bytes);
+                }
+            int flag[2];
+            CK(hipMemcpy(flag, sink, 8, hipMemcpyDeviceToHost));
+            printf("barrier timeouts: %d\n", flag[1]);
+        }
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "pf")) {
         // does an L2-hot first row group shorten a decode GEMV?  A: GEMV alone (26 rotating
         // layers, cold); B: touch kernel + GEMV; C: touch kernel alone.  GEMV with a hot first

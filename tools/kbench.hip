@@ -112,7 +112,9 @@ __global__ __launch_bounds__(256) void k_bar_one(const uint4* W, size_t n16, int
     const unsigned acc = bar_rest(W, n16, blockIdx.x, gridDim.x, v);
     if (acc == 0x9e3779b9u) sink[0] = (int)acc;
 }
-template <int PF>
+// HIER: arrivals counted per XCD group (block b % 8, 64-B apart) and only each group's last
+// arrival bumps the global phase counter ctr[0] (8 adds per barrier instead of G)
+template <int PF, int HIER = 0>
 __global__ __launch_bounds__(256) void k_bar_chain(const BarStreams S, int* ctr, int* sink) {
     const int G = gridDim.x, b = blockIdx.x;
     unsigned acc = 0;
@@ -124,8 +126,15 @@ __global__ __launch_bounds__(256) void k_bar_chain(const BarStreams S, int* ctr,
         if (PF) bar_first(S.w[j + 1], S.n16[j + 1], b, G, v);
         __syncthreads();
         if (threadIdx.x == 0) {
-            __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int target = (j + 1) * G;
+            int target = (j + 1) * G;
+            if (HIER) {
+                const int grp = b & 7, gn = G / 8;  // G % 8 == 0
+                if (__hip_atomic_fetch_add(ctr + 16 * (1 + grp), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (j + 1) * gn - 1)
+                    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                target = (j + 1) * 8;
+            } else {
+                __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             long long spins = 0;
             while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++spins < (1 << 22))
                 __builtin_amdgcn_s_sleep(1);
@@ -202,36 +211,38 @@ int main(int argc, char** argv) {
     };
     const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "bar")) {
-        int* ctr = (int*)dmalloc(64, 0);
+        int* ctr = (int*)dmalloc(16 * 9 * 4, 0);
         int* sink = (int*)dmalloc(64, 0);
         const size_t nb[4] = {(size_t)(DQ + 2 * DKV) * D * 2 / 16, (size_t)D * DQ * 2 / 16, (size_t)2 * DH * D * 2 / 16,
                               (size_t)D * DH * 2 / 16};
         const double bytes = 16.0 * (nb[0] + nb[1] + nb[2] + nb[3]);
         for (int G : {768, 512}) {
-            std::vector<hipGraphExec_t> ga(NL), gb(NL), gc(NL);
+            std::vector<hipGraphExec_t> ga(NL), gb(NL), gc(NL), gd(NL);
             for (int l = 0; l < NL; l++) {
                 const uint4* w[4] = {(const uint4*)wqkv[l], (const uint4*)wo[l], (const uint4*)w13[l], (const uint4*)w2[l]};
                 BarStreams S;
                 for (int j = 0; j < 4; j++) { S.w[j] = w[j]; S.n16[j] = nb[j]; }
-                for (int v = 0; v < 3; v++) {
+                for (int v = 0; v < 4; v++) {
                     hipGraph_t g;
                     CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
                     if (v == 0) {
                         for (int j = 0; j < 4; j++) hipLaunchKernelGGL(k_bar_one, dim3(G), dim3(256), 0, st, w[j], nb[j], sink);
                     } else {
-                        CK(hipMemsetAsync(ctr, 0, 4, st));
+                        CK(hipMemsetAsync(ctr, 0, 16 * 9 * 4, st));
                         if (v == 1) hipLaunchKernelGGL(k_bar_chain<0>, dim3(G), dim3(256), 0, st, S, ctr, sink);
-                        else hipLaunchKernelGGL(k_bar_chain<1>, dim3(G), dim3(256), 0, st, S, ctr, sink);
+                        else if (v == 2) hipLaunchKernelGGL(k_bar_chain<1>, dim3(G), dim3(256), 0, st, S, ctr, sink);
+                        else hipLaunchKernelGGL((k_bar_chain<1, 1>), dim3(G), dim3(256), 0, st, S, ctr, sink);
                     }
                     CK(hipStreamEndCapture(st, &g));
-                    CK(hipGraphInstantiate(v == 0 ? &ga[l] : v == 1 ? &gb[l] : &gc[l], g, nullptr, nullptr, 0));
+                    CK(hipGraphInstantiate(v == 0 ? &ga[l] : v == 1 ? &gb[l] : v == 2 ? &gc[l] : &gd[l], g, nullptr, nullptr, 0));
                     CK(hipGraphDestroy(g));
                 }
             }
-            const char* nm[3] = {"4 launches (graph)", "1 launch, grid barriers", "1 launch, barriers + next loads first"};
+            const char* nm[4] = {"4 launches (graph)", "1 launch, grid barriers", "1 launch, barriers + next loads first",
+                                 "1 launch, per-XCD barriers + next loads first"};
             for (int rep = 0; rep < 2; rep++)
-                for (int v = 0; v < 3; v++) {
-                    std::vector<hipGraphExec_t>& gx = v == 0 ? ga : v == 1 ? gb : gc;
+                for (int v = 0; v < 4; v++) {
+                    std::vector<hipGraphExec_t>& gx = v == 0 ? ga : v == 1 ? gb : v == 2 ? gc : gd;
                     char n[96];
                     snprintf(n, sizeof n, "bar G=%d %s", G, nm[v]);
                     add(n, timeit([&] { CK(hipGraphLaunch(gx[layer++ % NL], st)); }, iters, st), bytes);

@@ -251,6 +251,36 @@ int main(int argc, char** argv) {
             CK(hipMemcpy(flag, sink, 8, hipMemcpyDeviceToHost));
             printf("barrier timeouts: %d\n", flag[1]);
         }
+        // the Q8 layer's bytes (int8 rows: half of each read) and single reads of each size: the
+        // floor a streaming kernel with the decode step's launch structure reaches
+        for (int G : {768, 512, 384}) {
+            std::vector<hipGraphExec_t> gq(NL);
+            for (int l = 0; l < NL; l++) {
+                const uint4* w[4] = {(const uint4*)wqkv[l], (const uint4*)wo[l], (const uint4*)w13[l], (const uint4*)w2[l]};
+                hipGraph_t g;
+                CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+                for (int j = 0; j < 4; j++) hipLaunchKernelGGL(k_bar_one, dim3(G), dim3(256), 0, st, w[j], nb[j] / 2, sink);
+                CK(hipStreamEndCapture(st, &g));
+                CK(hipGraphInstantiate(&gq[l], g, nullptr, nullptr, 0));
+                CK(hipGraphDestroy(g));
+            }
+            char n[96];
+            snprintf(n, sizeof n, "bar G=%d Q8 layer bytes, 4 launches", G);
+            add(n, timeit([&] { CK(hipGraphLaunch(gq[layer++ % NL], st)); }, iters, st), bytes / 2);
+            const char* rn[4] = {"qkv", "wo", "w13", "w2"};
+            for (int q8 = 0; q8 < 2; q8++)
+                for (int j = 0; j < 4; j++) {
+                    const uint4* w[4] = {(const uint4*)wqkv[0], (const uint4*)wo[0], (const uint4*)w13[0], (const uint4*)w2[0]};
+                    std::vector<const uint4*> ws(NL);
+                    for (int l = 0; l < NL; l++)
+                        ws[l] = j == 0 ? (const uint4*)wqkv[l] : j == 1 ? (const uint4*)wo[l] : j == 2 ? (const uint4*)w13[l] : (const uint4*)w2[l];
+                    (void)w;
+                    snprintf(n, sizeof n, "bar G=%d one read %s%s", G, rn[j], q8 ? " (Q8 bytes)" : "");
+                    const size_t m = q8 ? nb[j] / 2 : nb[j];
+                    add(n, timeit([&] { hipLaunchKernelGGL(k_bar_one, dim3(G), dim3(256), 0, st, ws[layer++ % NL], m, sink); }, iters, st),
+                        16.0 * m);
+                }
+        }
         return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "pf")) {

@@ -803,6 +803,13 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     }
 
     float4 xr[KQ][XPC];
+    // bf16: the RMSNorm weights (and ada) go out with x -- independent of the row sum, so the
+    // prologue waits for one L2 round trip instead of two (C2 +0.7 %, W1|W3 21.0 -> 20.8 us);
+    // Q8 (16 x values per chunk) keeps them after the sum: the early registers cost it 0.5 %
+    // (profiles/r5_gemv_prologue_ab.txt)
+    constexpr bool EARLY = PRO != PRO_NONE && !WQ8;
+    constexpr int NXP = EARLY ? XPC : 1;
+    float4 nwr[KQ][NXP], adr[KQ][NXP];
     float ss = 0.f;
 #pragma unroll
     for (int j = 0; j < KQ; j++) {
@@ -813,6 +820,16 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         for (int h = 0; h < XPC; h++) {
             const float4 xv = xp[h];
             xr[j][h] = c < KC ? xv : z;
+        }
+        if (EARLY) {
+            const int cc = c < KC ? c : 0;
+            const float4* wp = reinterpret_cast<const float4*>(a.norm_w) + XPC * cc;
+            const float4* ap = reinterpret_cast<const float4*>(PRO == PRO_NORM_ADA ? a.ada : a.norm_w) + XPC * cc;
+#pragma unroll
+            for (int h = 0; h < NXP; h++) {
+                nwr[j][h] = wp[h];
+                if (PRO == PRO_NORM_ADA) adr[j][h] = ap[h];
+            }
         }
         if (PRO != PRO_NONE) {
 #pragma unroll
@@ -838,11 +855,11 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
 #pragma unroll
             for (int h = 0; h < XPC; h++) {
                 float4 v = xr[j][h];
-                const float4 nw = wp[h];
+                const float4 nw = EARLY ? nwr[j][h % NXP] : wp[h];
                 v.x = v.x * inv * nw.x; v.y = v.y * inv * nw.y;
                 v.z = v.z * inv * nw.z; v.w = v.w * inv * nw.w;
                 if (PRO == PRO_NORM_ADA) {
-                    const float4 ad = ap[h];
+                    const float4 ad = EARLY ? adr[j][h % NXP] : ap[h];
                     v.x *= (1.0f + ad.x); v.y *= (1.0f + ad.y);
                     v.z *= (1.0f + ad.z); v.w *= (1.0f + ad.w);
                 }

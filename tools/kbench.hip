@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../voxtral.c_amd/csrc/vox_hip_internal.h"
+#include "../voxtral.c_amd/csrc/vox_hip_dev.h"
 
 using namespace vox;
 namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
@@ -146,6 +147,83 @@ __global__ __launch_bounds__(256) void k_bar_chain(const BarStreams S, int* ctr,
     if (acc == 0x9e3779b9u) sink[0] = (int)acc;
 }
 
+// VOX_KB_ONLY=gw: a wave-independent decode GEMV prototype (STORE epilogue only).  Each wave
+// owns RB whole rows per group (no cross-wave reduction, no per-group block barrier), x sits
+// in LDS (one barrier at the start), and the wave's next U rounds of 16-B weight chunks are in
+// flight while it computes the current ones (flattened group x round-block steps).
+template <int RB, int WQ8, int U>
+__global__ __launch_bounds__(256) void k_gemv_wave(const void* __restrict__ W, const float* __restrict__ x, int K, int rows,
+                                                   float* __restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) float sx[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int rowbytes = WQ8 ? K : 2 * K, NC = rowbytes / 16, NR = (NC + 63) / 64, NB = (NR + U - 1) / U;
+    const int WS = gridDim.x * 4, ngroups = rows / RB;
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W), 0, rows * rowbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wz = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W), 0, 0, 0x00020000);
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    auto issue = [&](int g, int rb, uint4 (&wv)[U][RB]) {
+        const bool ok = g < ngroups;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int c = (rb * U + u) * 64 + lane;
+            const int cc = c < NC ? c : 0;
+#pragma unroll
+            for (int i = 0; i < RB; i++) {
+                const v4u v = __builtin_amdgcn_raw_buffer_load_b128(ok ? wr : wz, cc * 16, (ok ? g * RB + i : 0) * rowbytes, 2);
+                wv[u][i] = make_uint4(v.x, v.y, v.z, v.w);
+            }
+        }
+    };
+    float acc[RB];
+#pragma unroll
+    for (int i = 0; i < RB; i++) acc[i] = 0.f;
+    auto compute = [&](int rb, const uint4 (&wv)[U][RB]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int c = (rb * U + u) * 64 + lane;
+            const bool in = c < NC;
+            if (WQ8) {
+                float4 xv[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) xv[h] = in ? reinterpret_cast<const float4*>(sx)[c * 4 + h] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int i = 0; i < RB; i++) acc[i] = dot16q(wv[u][i], xv, acc[i]);
+            } else {
+                const float4 x0 = in ? reinterpret_cast<const float4*>(sx)[c * 2] : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 x1 = in ? reinterpret_cast<const float4*>(sx)[c * 2 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int i = 0; i < RB; i++) acc[i] = dot8(wv[u][i], x0, x1, acc[i]);
+            }
+        }
+    };
+    int g = blockIdx.x * 4 + wave, rb = 0;
+    uint4 A[U][RB], B[U][RB];
+    issue(g, 0, A);
+    for (int i = threadIdx.x; i < K / 4; i += 256) reinterpret_cast<float4*>(sx)[i] = reinterpret_cast<const float4*>(x)[i];
+    __syncthreads();
+    auto step = [&](const uint4 (&cur)[U][RB], uint4 (&nxt)[U][RB]) {
+        int gn = g, rn = rb + 1;
+        if (rn == NB) { rn = 0; gn += WS; }
+        issue(gn, rn, nxt);
+        compute(rb, cur);
+        if (rb == NB - 1) {
+#pragma unroll
+            for (int i = 0; i < RB; i++) {
+                const float v = wave_sum(acc[i]);
+                if (lane == 0) y[g * RB + i] = v;
+                acc[i] = 0.f;
+            }
+        }
+        g = gn;
+        rb = rn;
+    };
+    while (g < ngroups) {
+        step(A, B);
+        if (g >= ngroups) break;
+        step(B, A);
+    }
+}
+
 int main(int argc, char** argv) {
     int iters = argc > 1 ? atoi(argv[1]) : 200;
     hipStream_t st;
@@ -210,6 +288,56 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gw")) {
+        // the current k_gemv (PRO_NONE / EPI_STORE) against the wave-independent prototype,
+        // bf16 and Q8, the four decode shapes, 26 rotating layers; results compared
+        float* y2 = (float*)dmalloc(V * 4, 0);
+        struct S { const char* n; int K, rows; int which; };
+        std::vector<float> h1(2 * DH), h2(2 * DH);
+        for (int q8 = 0; q8 < 2; q8++) {
+            qs = q8 ? wsc : nullptr;
+            for (S sh : {S{"qkv", D, DQ + 2 * DKV, 0}, S{"wo", DQ, D, 1}, S{"w13", D, 2 * DH, 2}, S{"w2", DH, D, 3}}) {
+                auto wl = [&](int l) -> const uint16_t* { return sh.which == 0 ? wqkv[l] : sh.which == 1 ? wo[l] : sh.which == 2 ? w13[l] : w2[l]; };
+                char n[96];
+                const double bytes = (double)sh.rows * sh.K * (q8 ? 1 : 2);
+                snprintf(n, sizeof n, "gemv %s%s k_gemv", sh.n, q8 ? " q8" : "");
+                add(n, timeit([&] { gemv(PRO_NONE, EPI_STORE, wl(layer++ % NL), sh.K, sh.rows); }, iters, st), bytes);
+                gemv(PRO_NONE, EPI_STORE, wl(0), sh.K, sh.rows);
+                CK(hipStreamSynchronize(st));
+                CK(hipMemcpy(h1.data(), y, sh.rows * 4, hipMemcpyDeviceToHost));
+                for (int G : {768, 512}) {
+                    for (int v = 0; v < 3; v++) {
+                        auto launch = [&](const void* Wp) {
+                            const size_t lds = (size_t)sh.K * 4;
+                            if (q8) {
+                                if (v == 0) hipLaunchKernelGGL((k_gemv_wave<4, 1, 2>), dim3(G), dim3(256), lds, st, Wp, x, sh.K, sh.rows, y2);
+                                else if (v == 1) hipLaunchKernelGGL((k_gemv_wave<2, 1, 4>), dim3(G), dim3(256), lds, st, Wp, x, sh.K, sh.rows, y2);
+                                else hipLaunchKernelGGL((k_gemv_wave<4, 1, 1>), dim3(G), dim3(256), lds, st, Wp, x, sh.K, sh.rows, y2);
+                            } else {
+                                if (v == 0) hipLaunchKernelGGL((k_gemv_wave<4, 0, 2>), dim3(G), dim3(256), lds, st, Wp, x, sh.K, sh.rows, y2);
+                                else if (v == 1) hipLaunchKernelGGL((k_gemv_wave<2, 0, 4>), dim3(G), dim3(256), lds, st, Wp, x, sh.K, sh.rows, y2);
+                                else hipLaunchKernelGGL((k_gemv_wave<4, 0, 1>), dim3(G), dim3(256), lds, st, Wp, x, sh.K, sh.rows, y2);
+                            }
+                        };
+                        static const char* vn[3] = {"RB4 U2", "RB2 U4", "RB4 U1"};
+                        snprintf(n, sizeof n, "gemv %s%s wave-indep G=%d %s", sh.n, q8 ? " q8" : "", G, vn[v]);
+                        add(n, timeit([&] { launch(wl(layer++ % NL)); }, iters, st), bytes);
+                        launch(wl(0));
+                        CK(hipStreamSynchronize(st));
+                        CK(hipMemcpy(h2.data(), y2, sh.rows * 4, hipMemcpyDeviceToHost));
+                        double md = 0, mx = 0;
+                        for (int r = 0; r < sh.rows; r++) {
+                            md = std::max(md, (double)fabsf(h1[r] - h2[r]));
+                            mx = std::max(mx, (double)fabsf(h1[r]));
+                        }
+                        printf("   max |diff| %.3g of max |y| %.3g\n", md, mx);
+                    }
+                }
+            }
+        }
+        qs = nullptr;
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "bar")) {
         int* ctr = (int*)dmalloc(16 * 9 * 4, 0);
         int* sink = (int*)dmalloc(64, 0);

@@ -288,6 +288,26 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gpe")) {
+        // where the fused prologue / epilogue cost of the W1|W3 and QKV GEMVs sits: each
+        // prologue x epilogue combination of the same weights, bf16 and Q8
+        for (int q8 = 0; q8 < 2; q8++) {
+            qs = q8 ? wsc : nullptr;
+            struct C { const char* n; int pro, epi, K, rows, which; };
+            // (the instantiated pairs: NONE with STORE / RESID, NORM with SWIGLU / QKV, NORM_ADA with SWIGLU)
+            for (C cc : {C{"w13 none/store", PRO_NONE, EPI_STORE, D, 2 * DH, 2}, C{"w13 norm/swiglu", PRO_NORM, EPI_SWIGLU, D, 2 * DH, 2},
+                         C{"w13 norm_ada/swiglu", PRO_NORM_ADA, EPI_SWIGLU, D, 2 * DH, 2},
+                         C{"qkv none/store", PRO_NONE, EPI_STORE, D, DQ + 2 * DKV, 0}, C{"qkv none/resid", PRO_NONE, EPI_RESID, D, DQ + 2 * DKV, 0},
+                         C{"qkv norm/qkv", PRO_NORM, EPI_QKV, D, DQ + 2 * DKV, 0}}) {
+                char n[96];
+                snprintf(n, sizeof n, "gemv %s%s", cc.n, q8 ? " q8" : "");
+                add(n, timeit([&] { gemv(cc.pro, cc.epi, cc.which == 2 ? w13[layer++ % NL] : wqkv[layer++ % NL], cc.K, cc.rows); }, iters, st),
+                    (double)cc.rows * cc.K * (q8 ? 1 : 2));
+            }
+        }
+        qs = nullptr;
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gw")) {
         // the current k_gemv (PRO_NONE / EPI_STORE) against the wave-independent prototype,
         // bf16 and Q8, the four decode shapes, 26 rotating layers; results compared

@@ -1,6 +1,7 @@
 # decode GEMV prologue: RMSNorm weights (and ada) loaded with x (one L2 round trip before the
 # norm instead of two).  Parity (tiny, full jfk, Q8), then C2 and C5 alternating the new
 # library with the previous one (tools/ab/libvoxtral_hip_base.so via VOX_HIP_LIB) on one box
+# (tools/ab/libvoxtral_hip_base.so: the library built from the commit before the change, copied aside; not kept in the tree)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 400 --timeout-method thread tests/test_gpu_tiny.py tests/test_gpu_q8.py tests/test_gpu_full.py -k "not long_clip and not 60s" > gpurun_out/r5i_test.log 2>&1 || { tail -30 gpurun_out/r5i_test.log; exit 1; }

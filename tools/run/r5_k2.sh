@@ -1,6 +1,7 @@
 # decode GEMV prologue order: x (and the norm weights) issued before the first group's weights,
 # so the row sum waits for x alone (B: Q8 keeps late norm-weight loads; C: Q8 early too), against
 # the previous library (A); parity of B, then C2 and C5 alternating A / B / C on one box
+# (tools/ab/libvoxtral_hip_base.so: the library built from the commit before the change, copied aside; not kept in the tree)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 400 --timeout-method thread tests/test_gpu_tiny.py tests/test_gpu_q8.py tests/test_gpu_full.py -k "not long_clip and not 60s" > gpurun_out/r5k2_test.log 2>&1 || { tail -30 gpurun_out/r5k2_test.log; exit 1; }

@@ -2716,7 +2716,9 @@ static void stream_steps_done(vox_hip_stream_t* s, int produced, int last_token)
 // encoder's row-offset kernels), scratch of ss[0].  One stream, or 16-bit rings, take the
 // single-stream prefill.  The member queues must be idle.
 // bounded (vox_hip_batch_decode_rows): a single new stream takes the stacked path too, on the
-// batch queue -- its own queue may be busy with an encoder pass the steps overlap
+// batch queue -- its own queue may be busy with an encoder pass the steps overlap; 16-bit rings and
+// stacks past ENC_SUB rows still take the per-stream prefill on the member's own queue and
+// wait there for any encoder pass queued on it (correct; the overlap is lost for them)
 static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B, bool bounded) {
     vox_hip_model_t* m = b->m;
     const vox_hip_config_t& c = m->c;

@@ -2453,7 +2453,9 @@ __global__ __launch_bounds__(64) void k_resid_xw_fplanes(float* __restrict__ x, 
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ ada,
                                                          uint16_t* __restrict__ xs, float* __restrict__ ssq) {
-    constexpr int CH = 8;  // slabs per load round
+    // slabs per load round: 24 covers the batched step's wo (8 splits) and W2 (18) in one
+    // round of loads instead of 1 and 3 dependent ones
+    constexpr int CH = 24;
     const int sl = blockIdx.x, j = blockIdx.y, lane = threadIdx.x;
     const int k = sl * 256 + lane * 4;
     float* xr = x + (size_t)j * D + k;

@@ -35,6 +35,7 @@ CASES = [
     (25, 775, 32, 32, 64, 750, 750),   # streaming encoder chunk: key-range splits + combine
     (26, 800, 8, 8, 64, 750, 774),     # ragged rows, window cut
     (70, 300, 8, 8, 64, 750, 230),     # several 16-query blocks
+    (70, 819, 4, 4, 64, 750, 749),     # 70 rows over a full 750 window: the most key splits (12) + combine
     (38, 38, 32, 8, 128, 8192, 0),     # decoder prefill shape (head_dim 128, GQA 4)
     (17, 600, 32, 8, 128, 0, 583),     # head_dim 128 with splits
     (200, 200, 4, 4, 64, 24, 0),       # window much shorter than the rows

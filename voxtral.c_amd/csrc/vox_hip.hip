@@ -169,7 +169,7 @@ struct vox_hip_model {
     float *rope_enc, *rope_dec;    // device tables [rope_positions][hd]
     int rope_positions;
     int rope_gen;                  // bumped when the tables are reallocated (graphs hold the pointer)
-    std::vector<DecFragD> dfrag;   // fragment-major decoder matrices (empty until a batch exists)
+    std::vector<DecFragD> dfrag;   // fragment-major decoder matrices (empty until a batch or a bf16 prefill)
     std::vector<DecFragD> efrag;   // fragment-major encoder matrices (empty until a short chunk)
     uint8_t* lm_frag;              // fragment-major LM head (tied embeddings)
     int kv16;                      // decoder KV rings of streams created from now on in IEEE half
@@ -1675,10 +1675,21 @@ static int stream_prefilled(vox_hip_stream_t* s, hipStream_t q) {
 // one tile, where k_gemm2's 128 x 128 tiles were mostly padding and split K eight ways --, with
 // the inputs written as planes by their producers (RMSNorm rows, the attention output, the
 // W1|W3 SwiGLU epilogue), as the encoder's long passes do.
+static int dec_gemmf_env() {
+    // VOX_HIP_PREFILL_GEMMF=0: decoder prefills on k_gemm2 over the row-major weights (A/B, and
+    // no fragment-major copies for a process that never batches)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VOX_HIP_PREFILL_GEMMF");
+        v = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return v;
+}
+
 static bool dec_gemmf_ok(const vox_hip_model_t* m, int n) {
     const vox_hip_config_t& c = m->c;
     const int DD = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
-    return enc_gemmf_env() && !m->dec[0].sqkv && n >= 1 && n <= PLANE_MAX_ROWS && gemmf_ok(n, DQ + 2 * DKV, DD) &&
+    return enc_gemmf_env() && dec_gemmf_env() && !m->dec[0].sqkv && n >= 1 && n <= PLANE_MAX_ROWS && gemmf_ok(n, DQ + 2 * DKV, DD) &&
            gemmf_ok(n, DD, DQ) && gemmf_ok(n, 2 * c.dec_hidden, DD) && gemmf_ok(n, DD, c.dec_hidden) &&
            c.dec_hidden % 64 == 0;
 }
@@ -1738,7 +1749,16 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
     hipStream_t st = s->st;
     if (stream_alloc_dec_rows(s, n)) return -1;
     if (n > DEC_SLACK + 1 && pos0 > 0) return set_err("prefill of %d rows on a non-empty cache", n);
-    if (n > 1 && dec_gemmf_ok(m, n)) {
+    // k_gemmf needs the fragment-major decoder copies (6.86 GB, made here on the first
+    // prefill unless a batch made them) and the stream's plane buffers; when either cannot be
+    // allocated the prefill takes the k_gemm2 layers below (same arithmetic, row-major weights)
+    bool gf = n > 1 && dec_gemmf_ok(m, n);
+    if (gf && (model_frag(m) || stream_dec_planes(s, n))) {
+        vox_hip_clear_error();
+        (void)hipGetLastError();  // the failed hipMalloc, so no later launch check reports it
+        gf = false;
+    }
+    if (gf) {
         // the hand-off flags before the queue descriptor copies the pointer (a stream whose
         // encoder never ran a k_gemmf pass has none yet)
         if (!s->gflags) CK(dalloc(&s->gflags, gemmf_flag_ints()));
@@ -2488,24 +2508,32 @@ static int frag_copy(uint8_t** dst, const uint8_t* src, int N, int K, int q8) {
     return 0;
 }
 
-// fragment-major copies of the decoder matrices and the LM head, made once per model
-// (6.86 GB bf16 / 3.83 GB Q8 beside the row-major weights the single-stream GEMVs read)
+// fragment-major copies of the decoder matrices and the LM head, made once per model, on the
+// first batch or the first bf16 prefill of more than one row (6.86 GB bf16 / 3.83 GB Q8 beside
+// the row-major weights the single-stream GEMVs read).  All or nothing: a failed copy frees
+// what it had made, so the model holds either every copy or none.
 static int model_frag(vox_hip_model_t* m) {
     if (m->lm_frag) return 0;
     const vox_hip_config_t& c = m->c;
     const int DD = c.dec_dim, DQ = c.dec_heads * c.dec_head_dim, DKV = c.dec_kv_heads * c.dec_head_dim;
     const int DH = c.dec_hidden;
-    m->dfrag.assign(c.dec_layers, DecFragD{});
-    for (int l = 0; l < c.dec_layers; l++) {
-        const DecLayerD& L = m->dec[l];
-        DecFragD& F = m->dfrag[l];
-        if (frag_copy(&F.wqkv, L.wqkv, DQ + 2 * DKV, DD, L.sqkv != nullptr)) return -1;
-        if (frag_copy(&F.wo, L.wo, DD, DQ, L.so != nullptr)) return -1;
-        if (frag_copy(&F.w13, L.w13, 2 * DH, DD, L.s13 != nullptr)) return -1;
-        if (frag_copy(&F.w2, L.w2, DD, DH, L.s2 != nullptr)) return -1;
-    }
+    std::vector<DecFragD> F(c.dec_layers, DecFragD{});
     uint8_t* lm = nullptr;
-    if (frag_copy(&lm, m->tok_emb, c.vocab, DD, m->tok_emb_s != nullptr)) { dfree(lm); return -1; }
+    bool ok = true;
+    for (int l = 0; l < c.dec_layers && ok; l++) {
+        const DecLayerD& L = m->dec[l];
+        ok = !frag_copy(&F[l].wqkv, L.wqkv, DQ + 2 * DKV, DD, L.sqkv != nullptr) &&
+             !frag_copy(&F[l].wo, L.wo, DD, DQ, L.so != nullptr) &&
+             !frag_copy(&F[l].w13, L.w13, 2 * DH, DD, L.s13 != nullptr) &&
+             !frag_copy(&F[l].w2, L.w2, DD, DH, L.s2 != nullptr);
+    }
+    if (ok) ok = !frag_copy(&lm, m->tok_emb, c.vocab, DD, m->tok_emb_s != nullptr);
+    if (!ok) {
+        for (auto& f : F) { dfree(f.wqkv); dfree(f.wo); dfree(f.w13); dfree(f.w2); }
+        dfree(lm);
+        return -1;
+    }
+    m->dfrag.swap(F);
     m->lm_frag = lm;
     return 0;
 }

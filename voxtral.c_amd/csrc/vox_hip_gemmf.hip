@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
         const long long tend = (long long)(t + 1) * a.S;
         int npb = 0;
         while (b + 1 + npb < G && gf_bound(a.U, G, b + 1 + npb) < tend) npb++;
-        if (npb > 64) npb = 64;  // unreachable: a block holds >= 4 stages and a tile <= 144
+        // npb <= 62: launch_gemmf refuses a minimum stage count that would let more blocks touch a tile
         if (npb > 0) {
             if (wave == 0) {
                 const bool mine = lane < npb;
@@ -497,6 +497,9 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     // (tools/kbench VOX_KB_ONLY=gemmfm, profiles/r5_kbench_gemmf_minu.txt)
     const long long minu = g_gemmf_minu ? g_gemmf_minu
                            : a.MT <= 2 ? std::max(6, a.S / 8) : std::max(4, (a.S + 1) / 2);
+    // the owner polls the flags of its tile's later blocks with the lanes of one wave: a tile
+    // may span at most 64 of them (ceil(S / minu) + 1 blocks touch a tile)
+    if ((a.S + minu - 1) / minu + 2 > 64) return hipErrorInvalidConfiguration;
     int G = gemmf_grid();
     if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
     // one partial tile per block: (4 WR waves) x (RB / WR) x NGx x 64 lanes x 4 floats

@@ -1133,8 +1133,9 @@ int vh_sched_run(vh_sched_t *q) {
     int total = 0;
     int eos[VH_SCHED_MAX] = {0}, ran[VH_SCHED_MAX] = {0};
     /* Overlap: the batched steps decode the adapter rows that exist when the run starts while
-     * this run's encoder pass (enqueued first, on the streams' queues) computes the next ones;
-     * those are decoded by the next run.  Greedy ids do not depend on when a row is decoded, so
+     * this run's encoder pass (enqueued first, on the streams' queues) computes the next ones.
+     * With a step cap set, those rows are decoded by the next run; with no cap (step_cap <= 0)
+     * this run waits for the pass and drains them in a second round of steps.  Greedy ids do not depend on when a row is decoded, so
      * a stream's ids are unchanged.  Live-mode streams keep the sequential order: their restart
      * checks belong after a drain of every row of the chunk (voxtral.c:1189-1239). */
     int overlap = sched_overlap() && sched_batch_encode();

@@ -500,6 +500,30 @@ int main(int argc, char** argv) {
         qs = nullptr;
         return 0;
     }
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "sknb")) {
+        // batched decode projections at 16 / 32 / 48 rows (1-3 row blocks; the blocks of one
+        // weight slice on one XCD): what a step of more than 16 streams costs per GEMM
+        uint16_t* xp = (uint16_t*)dmalloc((size_t)3 * 3 * 16 * 9216 * 2, 1);
+        float* part = (float*)dmalloc((size_t)3 * 36 * 16 * 18432 * 4, 0);
+        float* Cs = (float*)dmalloc((size_t)48 * 131072 * 4, 0);
+        struct S { const char* n; int N, K; uint16_t* const* W; double bytes; };
+        const S shapes[] = {S{"qkv 6144x3072", DQ + 2 * DKV, D, wqkv.data(), (DQ + 2.0 * DKV) * D * 2},
+                            S{"wo  3072x4096", D, DQ, wo.data(), (double)D * DQ * 2},
+                            S{"w13 18432x3072", 2 * DH, D, w13.data(), 2.0 * DH * D * 2},
+                            S{"w2  3072x9216", D, DH, w2.data(), (double)D * DH * 2}};
+        for (const S& g : shapes)
+            for (int nb : {16, 32, 48}) {
+                char nm[96];
+                snprintf(nm, sizeof nm, "skl %s nb%d", g.n, nb);
+                add(nm, timeit([&] { CK(launch_gemm_skl(xp, g.K, g.W[layer++ % NL], nullptr, g.N, nb, part, st)); }, iters, st), g.bytes);
+            }
+        for (int nb : {16}) {
+            char nm[96];
+            snprintf(nm, sizeof nm, "skf lm 131072x3072 nb%d", nb);
+            add(nm, timeit([&] { CK(launch_gemm_skf(xp, D, emb, nullptr, V, nb, Cs, V, st)); }, iters / 4 + 1, st), (double)V * D * 2);
+        }
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "sklks")) {
         // batched decode projections at 16 rows: k_skl waves per block x 64-k blocks per split
         uint16_t* xp = (uint16_t*)dmalloc((size_t)3 * 16 * 9216 * 2, 1);

@@ -22,4 +22,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace -d $O/tr16 -o run --output-format csv
 timeout -k 10 400 rocprofv3 --kernel-trace -d $O/tr8 -o run --output-format csv -- python3 bench.py --stagger --streams 8 --steps 1 --warmup 0 --no-cpu-baseline > $O/tr8.log 2>&1 || { tail -20 $O/tr8.log; exit 1; }
 python3 tools/serve_timeline.py $(find $O/tr16 -name "*kernel_trace.csv" | head -1) > $O/timeline16.txt 2>&1; cat $O/timeline16.txt
 python3 tools/serve_timeline.py $(find $O/tr8 -name "*kernel_trace.csv" | head -1) > $O/timeline8.txt 2>&1; cat $O/timeline8.txt
+
+VOX_KB_ONLY=sknb timeout -k 10 200 tools/kb_run 100 > $O/kb_sknb.txt 2>&1 || { tail -20 $O/kb_sknb.txt; exit 1; }
+cat $O/kb_sknb.txt
 echo rc=0

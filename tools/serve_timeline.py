@@ -14,8 +14,10 @@ import collections
 import csv
 import sys
 
-PREFILL_NAMES = ("k_gemmf", "k_rope_kv_rows", "k_embed_rows", "k_attn_mf", "k_split_fplanes", "k_rmsnorm_fplanes",
-                 "k_attn_tiled_combine")
+# kernels only the batched step launches: on the batch queue a stacked prefill runs from a
+# k_embed_rows to the next of these
+STEP_NAMES = ("k_embed_batch", "k_resid_xw_fplanes", "k_skl", "k_sklx", "k_attn_decode", "k_skf", "k_argmax_rows",
+              "k_argmax_batch_final", "k_swiglu_fplanes")
 
 
 def short(name):
@@ -78,19 +80,20 @@ def main():
     rows = [r for r in rows if r[1] > first and r[0] < last]
     cls = collections.defaultdict(list)
     per = collections.defaultdict(lambda: collections.Counter())
-    # a stacked prefill = the batch-queue kernels between a k_embed_rows and the next step kernel
+    queues = collections.defaultdict(collections.Counter)
     in_prefill = False
     for a, b, q, n in rows:
         if q == batch_q:
             if n.startswith("k_embed_rows"):
                 in_prefill = True
-            elif not n.startswith(PREFILL_NAMES):
+            elif n.startswith(STEP_NAMES):
                 in_prefill = False
             c = "prefill" if in_prefill else "step"
         else:
             c = "encoder"
         cls[c].append((a, b))
         per[c][n] += b - a
+        queues[c][q] += 1
     wall = last - first
     allv = [iv for v in cls.values() for iv in v]
     busy = union(allv)
@@ -129,6 +132,21 @@ def main():
             v.sort()
             print(f"  step span {k:15s} n={len(v):5d}  p50 {v[len(v) // 2] / 1e3:8.1f} us  mean {sum(v) / len(v) / 1e3:8.1f} us"
                   f"  sum {sum(v) / 1e6:8.1f} ms")
+    for c in ("step", "prefill", "encoder"):
+        print(f"  {c} launches by queue id: {dict(queues[c])}")
+    if "--dump" in sys.argv:
+        # every kernel of the first few step spans that had encoder kernels in them
+        shown = 0
+        for e0, e1 in zip(ends, ends[1:]):
+            if not touches(enc, e0, e1) or touches(pre, e0, e1):
+                continue
+            print(f"  -- step span {(e1 - e0) / 1e3:.1f} us with encoder kernels (t = 0 at the previous step's end)")
+            for a, b, q, n in rows:
+                if b > e0 and a < e1:
+                    print(f"     q{q:<3d} {(a - e0) / 1e3:9.1f} .. {(b - e0) / 1e3:9.1f} us  {n[:60]}")
+            shown += 1
+            if shown >= 2:
+                break
     for c in ("step", "prefill", "encoder"):
         tot = sum(per[c].values())
         print(f"  {c}: top kernels")

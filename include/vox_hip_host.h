@@ -122,7 +122,7 @@ vh_ctx_t *vh_ctx_wrap(vox_hip_model_t *model, const vox_hip_config_t *cfg, int d
  * in the batch (the batched argmax keeps their candidates); a live-mode stream drains on its
  * own path inside vh_stream_flush (and so inside vh_stream_finish), where the reference's
  * restart checks run between the flush and the final chunk. */
-#define VH_SCHED_MAX 16
+#define VH_SCHED_MAX 32
 typedef struct vh_sched vh_sched_t;
 typedef struct {
     int runs, prefills, batch_calls;

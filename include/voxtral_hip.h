@@ -206,7 +206,7 @@ int vox_hip_stream_set_alt(vox_hip_stream_t *s, int n_alt, float cutoff);
 int vox_hip_stream_read_alts(vox_hip_stream_t *s, int first, int n, int *ids_out, float *probs_out);
 /* Cross-stream batched greedy decoding (C4; the reference decodes each
  * vox_stream_t separately, voxtral.c:1105-1145).  A batch object holds scratch for up to
- * max_streams (<= 16) streams of one model.  vox_hip_batch_decode advances every listed
+ * max_streams (<= 32: two 16-row blocks) streams of one model.  vox_hip_batch_decode advances every listed
  * stream that has adapter rows left by one greedy token per step; the weights are streamed
  * once per step for all of them, attention / KV / argmax use each stream's own state.
  * Streams not started yet whose prompt is complete are prefilled first (several of them in

@@ -360,3 +360,43 @@ def test_batch_decode_rows_bounds_each_stream(models, tiny_cfg):
     for s in ss:
         s.close()
     b.close()
+
+
+def test_batch_32_streams_two_row_blocks(models, tiny_cfg):
+    """32 streams in one batch (the bucket of two 16-row MFMA B blocks): the first call
+    prefills all of them in stacked passes (32 prompts of 39 rows exceed one 1024-row pass, so
+    the prompts go in groups) and takes their first token in the batched steps; every stream's
+    ids equal its own oracle session, and streams in the second row block (rows 16-31) keep
+    the logit bar step by step."""
+    import vox_hip
+    import vox_oracle
+    hm, om = models
+    n = 32
+    mels = _mels(tiny_cfg, [420 + 29 * i for i in range(n)], 3200)
+    ss = [vox_hip.Stream(hm) for _ in mels]
+    for s, mel in zip(ss, mels):
+        s.encode_mel(mel)
+    b = vox_hip.Batch(hm, n)
+    steps = 6
+    got = [[] for _ in ss]
+    lg = {i: [] for i in (0, 16, 31)}
+    for _ in range(steps):
+        for i, t in enumerate(b.decode(ss, max_steps=1, stop_at_eos=False)):
+            got[i] += t.tolist()
+        for i in lg:
+            lg[i].append(b.read_logits(ss[i]))
+    for i, t in enumerate(b.decode(ss, max_steps=1000, stop_at_eos=False)):
+        got[i] += t.tolist()
+    for i, mel in enumerate(mels):
+        assert got[i] == _reference_tokens(om, mel), i
+    for i, l in lg.items():
+        o = vox_oracle.OracleStream(om)
+        o.encode_mel(mels[i])
+        t, ol = o.decode(max_steps=steps, stop_at_eos=False, want_logits=True)
+        o.close()
+        assert got[i][:steps] == t.tolist(), i
+        r = rel(np.stack(l), ol)
+        assert r < LOGIT_TOL, (i, r)
+    for s in ss:
+        s.close()
+    b.close()

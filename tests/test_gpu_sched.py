@@ -379,11 +379,14 @@ def test_scheduler_full_size_16_streams_match_single_stream(jfk_samples):
     slot-table batched steps; every stream's ids equal the same audio run alone through the
     single-stream path -- itself pinned to the CPU oracle at full size -- so the batched,
     stacked-prefill and overlapped machinery adds nothing of its own at this scale (an oracle
-    run of ~200 s of audio would take the CPU most of an hour)."""
+    run of all ~200 s of audio would take the CPU most of an hour).  The two shortest streams
+    (6 s and 7 s) are also pinned to the CPU oracle directly."""
     import vox_hip
+    import vox_oracle
     from vox_weights import VOXTRAL_4B, synth_weights
     w = synth_weights(VOXTRAL_4B, seed=0)
     hm = vox_hip.Model(VOXTRAL_4B, w)
+    om = vox_oracle.OracleModel(VOXTRAL_4B, w)
     del w
     long = np.concatenate([jfk_samples] * 3)
     rng = np.random.default_rng(5)
@@ -402,5 +405,37 @@ def test_scheduler_full_size_16_streams_match_single_stream(jfk_samples):
                                                                if ids[k][i] != ref[i]), None))
     ctx.close()
     hm.close()
+    lens = [len(a) for a in audios]
+    for k in sorted(range(16), key=lambda i: lens[i])[:2]:
+        ref, _ = _oracle_ids(om, audios[k], 0.5)
+        assert ids[k] == ref, ("oracle", k, len(ids[k]), len(ref))
+    om.close()
     assert st["steps"] > 0 and st["tokens"] / st["steps"] > 4, st
     print("16-stream full-size scheduler stats", st)
+
+
+def test_scheduler_32_streams_match_oracle(tiny_weights, jfk_samples):
+    """32 streams on one scheduler (VH_SCHED_MAX; the batched steps' second 16-row block, the
+    cross-stream encoder pass over 32 streams' chunks, stacked prefills in groups): two streams
+    start per tick, 8-12 s each, so all 32 are live together; a step cap of 8 as bench.py
+    --stagger; every stream's ids = its oracle session."""
+    import vox_hip
+    import vox_oracle
+    from vox_weights import TINY_LONG
+    hm = vox_hip.Model(TINY_LONG, tiny_weights)
+    om = vox_oracle.OracleModel(TINY_LONG, tiny_weights)
+    long = np.concatenate([jfk_samples] * 2)
+    audios = []
+    for k in range(32):
+        n = int(16000 * (8.0 + 0.5 * (k % 9)))
+        off = (k * 7919) % (len(long) - n)
+        audios.append(np.ascontiguousarray(long[off:off + n]))
+    ids, st = _serve(hm, audios, [k // 2 for k in range(32)], 0.5, max_streams=32, step_cap=8)
+    for k, a in enumerate(audios):
+        ref, _ = _oracle_ids(om, a, 0.5)
+        assert len(ref) > 0
+        assert ids[k] == ref, (k, len(ids[k]), len(ref))
+    assert st["tokens"] / max(1, st["steps"]) > 8, st
+    print("32-stream scheduler stats", st)
+    hm.close()
+    om.close()

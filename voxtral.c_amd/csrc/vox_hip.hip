@@ -653,6 +653,9 @@ static hipError_t queue_high_priority(hipStream_t* q) {
         (void)hipGetLastError();  // not left pending for the next launch check
         hi = 0;
     }
+    // VOX_HIP_BATCH_PRIORITY=0: a normal-priority batch queue (A/B of the served overlap)
+    const char* e = getenv("VOX_HIP_BATCH_PRIORITY");
+    if (e && atoi(e) == 0) return hipStreamCreateWithFlags(q, hipStreamNonBlocking);
     return hipStreamCreateWithPriority(q, hipStreamNonBlocking, hi);
 }
 
@@ -2479,10 +2482,10 @@ struct vox_hip_batch {
     // in device memory and mirrored in pinned host memory (one copy each way per step chunk)
     BatchSlot* slots;
     BatchSlot* hslots;
-    // step graphs [kv16][slot bucket 1, 2, 4, 8, 16][attention splits bucket]: their kernel
+    // step graphs [kv16][slot bucket 1, 2, 4, 8, 16, 32][attention splits bucket]: their kernel
     // arguments point at the slot table and the batch's buffers only, so they stay valid as
     // streams come and go; captured again only when the model's rope table moves
-    hipGraphExec_t gexec[2][5][STEP_GRAPHS];
+    hipGraphExec_t gexec[2][6][STEP_GRAPHS];
     int grope_gen;
     // rows of the last call (b->logits row i = stream luid[i], from its last step when llive[i])
     unsigned long long luid[VOX_MAX_BATCH];
@@ -2590,7 +2593,7 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
             set_err("batched decode needs dec_dim, heads*head_dim and dec_hidden divisible by 256");
             return fail();
         }
-        TRYH(dalloc(&b->part, (size_t)SK_ROWS * n));
+        TRYH(dalloc(&b->part, (size_t)S * n));  // [row block][split][16][N] for the S slot rows
     }
     TRYH(dalloc(&b->ssq, (size_t)SK_ROWS * SKX_TICKETS));  // [slices][16], any slice count
     TRYH(dalloc(&b->ticket, (size_t)SKX_TICKETS));
@@ -2608,9 +2611,9 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
     TRYH(hipHostMalloc((void**)&b->hslots, SLOT_BYTES, hipHostMallocDefault));
     memset((void*)b->hslots, 0, SLOT_BYTES);
     if (model_frag(m)) return fail();
-    TRYH(dalloc(&b->xp_d, (size_t)3 * SK_ROWS * D));
-    TRYH(dalloc(&b->xp_q, (size_t)3 * SK_ROWS * c.dec_heads * c.dec_head_dim));
-    TRYH(dalloc(&b->xp_h, (size_t)3 * SK_ROWS * c.dec_hidden));
+    TRYH(dalloc(&b->xp_d, (size_t)3 * S * D));  // [row block][3][16][K]
+    TRYH(dalloc(&b->xp_q, (size_t)3 * S * c.dec_heads * c.dec_head_dim));
+    TRYH(dalloc(&b->xp_h, (size_t)3 * S * c.dec_hidden));
 #undef TRYH
     return b;
 }
@@ -2678,13 +2681,16 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
     // final norm (after the last w2 residual) + LM head (tied embeddings) + per-slot argmax,
     // state, token log and next inputs (decoder.c:762-779)
     CK(launch_rmsnorm_fplanes(b->x, nb, DD, m->dec_norm, nullptr, c.dec_eps, b->xp_d, b->part, Sres, st));
-    CK(launch_gemm_skf(b->xp_d, DD, m->lm_frag, m->tok_emb_s, c.vocab, nb, b->logits, c.vocab, st));
+    // (one k_skf launch per 16-row block: its planes are read per block from L2)
+    for (int r0 = 0; r0 < nb; r0 += SK_ROWS)
+        CK(launch_gemm_skf(b->xp_d + (size_t)r0 * 3 * DD, DD, m->lm_frag, m->tok_emb_s, c.vocab, std::min(SK_ROWS, nb - r0),
+                           b->logits + (size_t)r0 * c.vocab, c.vocab, st));
     CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, b->palt, b->slots, TOKENS_CAP, slot_toklog(b->slots),
                            m->tok_emb, m->tok_emb_s, DD, b->x, st));
     return 0;
 }
 
-// slot bucket of n streams: 1, 2, 4, 8 or 16 slots (graph g of the bucket)
+// slot bucket of n streams: 1, 2, 4, 8, 16 or 32 slots (graph g of the bucket)
 static int slot_bucket(int n, int* g) {
     int k = 0;
     while ((1 << k) < n) k++;
@@ -2751,6 +2757,14 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B,
     vox_hip_model_t* m = b->m;
     const vox_hip_config_t& c = m->c;
     const int np = 32 + m->delay_tokens;
+    // more prompts than one pass holds (ENC_SUB rows: 26 prompts of 39 rows): stacked passes of
+    // as many as fit
+    const int per = std::max(1, ENC_SUB / np);
+    if (B > per && !ss[0]->kv16) {
+        for (int i0 = 0; i0 < B; i0 += per)
+            if (batch_prefill(b, ss + i0, std::min(per, B - i0), bounded)) return -1;
+        return 0;
+    }
     if ((B == 1 && !bounded) || ss[0]->kv16 || B * np > ENC_SUB) {
         for (int i = 0; i < B; i++) {
             if (stream_prefill(ss[i])) return -1;

@@ -42,7 +42,7 @@ struct GemvArgs {
     float* part_alt;       // EPI_LOGITS_ALT: [blocks][ALT_PART]
 };
 
-constexpr int VOX_MAX_BATCH = 16;    // streams per batched decode step
+constexpr int VOX_MAX_BATCH = 32;    // streams per batched decode step (two 16-row blocks of the MFMA B operand)
 
 // One row of a batched decode step, in device memory (the batch's slot table).  The step
 // graph's kernel arguments point at the table, never at a stream, so streams join and leave

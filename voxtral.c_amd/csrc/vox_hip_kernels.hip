@@ -1345,7 +1345,6 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
     if (DBG == 4) ts[4] = __builtin_amdgcn_s_memtime();
     if (FUSE && S == 1) {
         // output row zb straight into the wo input planes: 8 consecutive dims per thread
-        const size_t Pn = (size_t)SK_ROWS * H * HD;
         for (int e = tid; e < nh * HD / 8; e += NT) {
             const int h = e / (HD / 8), d0 = (e % (HD / 8)) * 8;
             float fw[NWV], den, Mx;
@@ -1368,10 +1367,10 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
                 mp[i / 2] = b0 | ((uint32_t)b1 << 16);
                 lq[i / 2] = c0 | ((uint32_t)c1 << 16);
             }
-            const size_t o = frag_off(zb, (h0 + h) * HD + d0);
-            *reinterpret_cast<uint4*>(F.xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
-            *reinterpret_cast<uint4*>(F.xs + Pn + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
-            *reinterpret_cast<uint4*>(F.xs + 2 * Pn + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+            const int kq = (h0 + h) * HD + d0;
+            *reinterpret_cast<uint4*>(F.xs + frag_at(zb, H * HD, 0, kq)) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+            *reinterpret_cast<uint4*>(F.xs + frag_at(zb, H * HD, 1, kq)) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+            *reinterpret_cast<uint4*>(F.xs + frag_at(zb, H * HD, 2, kq)) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
         }
         dbg_dump();
         return;
@@ -1484,7 +1483,6 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
         if (FUSE) {
             // the attention row of stream zb into the wo input planes, 8 dims per thread
             __syncthreads();
-            const size_t Pn = (size_t)SK_ROWS * H * HD;
             for (int e = tid; e < nh * HD / 8; e += NT) {
                 const int h = e / (HD / 8), d0 = (e % (HD / 8)) * 8;
                 uint32_t hp[4], mp[4], lq[4];
@@ -1497,10 +1495,10 @@ __global__ __launch_bounds__(NWV * 64) void k_attn_decode(const AttnPtrs P, int 
                     mp[i / 2] = b0 | ((uint32_t)b1 << 16);
                     lq[i / 2] = c0 | ((uint32_t)c1 << 16);
                 }
-                const size_t o = frag_off(zb, (h0 + h) * HD + d0);
-                *reinterpret_cast<uint4*>(F.xs + o) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
-                *reinterpret_cast<uint4*>(F.xs + Pn + o) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
-                *reinterpret_cast<uint4*>(F.xs + 2 * Pn + o) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
+                const int kq = (h0 + h) * HD + d0;
+                *reinterpret_cast<uint4*>(F.xs + frag_at(zb, H * HD, 0, kq)) = make_uint4(hp[0], hp[1], hp[2], hp[3]);
+                *reinterpret_cast<uint4*>(F.xs + frag_at(zb, H * HD, 1, kq)) = make_uint4(mp[0], mp[1], mp[2], mp[3]);
+                *reinterpret_cast<uint4*>(F.xs + frag_at(zb, H * HD, 2, kq)) = make_uint4(lq[0], lq[1], lq[2], lq[3]);
             }
         }
         if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3549,8 +3547,8 @@ int skl_splits(int K, int N) {
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
                            float* part, hipStream_t st, const float* ssq, int nsl, float eps) {
     const int S = skl_splits(K, N);
-    // ssq: one row block (its nsl x 16 sums ride with the planes: nsl * 16 <= the block's threads)
-    if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S || (ssq && (nsl < 1 || nsl > SKL_MAX_SLICES || nb > SK_ROWS)))
+    // ssq: each row block's nsl x 16 sums ride with its planes (nsl * 16 <= the block's threads)
+    if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S || (ssq && (nsl < 1 || nsl > SKL_MAX_SLICES)))
         return hipErrorInvalidValue;
     const int ks = K / 64 / S;
     const int nw = ks == 6 ? 4 : skl_nw_for(N, S);

@@ -762,7 +762,7 @@ class HostStream:
 
 
 class Scheduler:
-    """vh_sched_t: up to 16 HostStreams of one model on this GPU; run() decodes every
+    """vh_sched_t: up to 32 HostStreams (VH_SCHED_MAX) of one model on this GPU; run() decodes every
     attached stream's pending adapter rows with batched greedy steps."""
 
     def __init__(self, ctx: HostCtx, max_streams: int):

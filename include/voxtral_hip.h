@@ -229,6 +229,16 @@ int vox_hip_batch_decode(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, 
  * beside the batched steps (the per-GPU scheduler's overlap, vh_sched_run). */
 int vox_hip_batch_decode_rows(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, const int *rows,
                               int max_steps, int stop_at_eos, int *tokens_out, int *counts_out);
+/* vox_hip_batch_decode_rows in two halves: begin enqueues the call's prefills and its first
+ * 16 steps on the batch queue and returns without waiting (0, or <0 on error); finish waits,
+ * runs any further steps and fills tokens_out / counts_out (which must stay valid in between),
+ * returning the total as decode_rows does.  In between the caller may enqueue work on other
+ * queues -- the per-GPU scheduler enqueues the cross-stream encoder pass there, after the
+ * steps, so the steps are on the device first -- but must not touch the listed streams'
+ * decoder state or call another batch function on b. */
+int vox_hip_batch_begin_rows(vox_hip_batch_t *b, vox_hip_stream_t **streams, int n, const int *rows,
+                             int max_steps, int stop_at_eos, int *tokens_out, int *counts_out);
+int vox_hip_batch_finish(vox_hip_batch_t *b);
 /* Logits [vocab] of the last batched step, for a stream that step advanced (the logits the
  * reference's vox_decoder_forward returns, voxtral_decoder.c:762-779; for tests and --alt
  * style callers).  Returns 0, or <0 if s was not in that step. */

@@ -2498,6 +2498,14 @@ struct vox_hip_batch {
     float* pgws;
     int* gflags;
     int gepoch;
+    // a call begun by batch_begin and not yet finished (vox_hip_batch_begin_rows /
+    // vox_hip_batch_finish): its streams, outputs and the steps left after the chunk in flight
+    struct {
+        int active, n, max_steps, stop_at_eos, K, nb, gb, gi, splits, kv16, done, k;
+        vox_hip_stream_t* streams[VOX_MAX_BATCH];
+        int* tokens_out;
+        int* counts_out;
+    } call;
 };
 
 static int* slot_toklog(BatchSlot* slots) { return reinterpret_cast<int*>(slots + VOX_MAX_BATCH); }
@@ -2621,7 +2629,7 @@ extern "C" vox_hip_batch_t* vox_hip_batch_create(vox_hip_model_t* m, int max_str
 // the batched step's projections: k_skl, one burst of column groups per block
 static hipError_t batch_gemm(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* part,
                              hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f) {
-    return launch_gemm_skl(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
+    return launch_gemm_skl(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps, 1);
 }
 
 // one batched step over slots 0..nb-1 of the slot table (their input rows already in b->x)
@@ -2843,9 +2851,13 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B,
 // pass finishes before the steps read its rows); rows[i]: only stream i's first rows[i] rows,
 // which the caller guarantees complete, and the members' queues are left running (an encoder
 // pass enqueued on them after those rows overlaps the steps)
-static int batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, const int* rows, int max_steps,
-                        int stop_at_eos, int* tokens_out, int* counts_out) {
+// batch_begin enqueues the call's prefills, slot table and first chunk of steps and returns
+// without waiting (0: steps in flight, 1: nothing to run); batch_finish waits for them, runs
+// the remaining chunks and fills the outputs.  batch_decode = both.
+static int batch_begin(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, const int* rows, int max_steps,
+                       int stop_at_eos, int* tokens_out, int* counts_out) {
     if (!b || n < 1 || n > b->cap || max_steps < 0) return set_err("bad batch arguments");
+    if (b->call.active) return set_err("batch: a begun call was not finished");
     vox_hip_model_t* m = b->m;
     const vox_hip_config_t& c = m->c;
     const int prompt_len = 1 + 32 + m->delay_tokens;
@@ -2873,7 +2885,7 @@ static int batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, c
             avail[i] = streams[i]->total_adapter;
         }
     }
-    if (max_steps == 0) return 0;
+    if (max_steps == 0) return 1;
     // 1. streams whose prompt is complete and whose decoder has not started: their prefills
     //    in one stacked pass; they take their first token in the batched steps below
     {
@@ -2918,21 +2930,57 @@ static int batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, c
     }
     if (K == 0) {
         CK(hipStreamSynchronize(b->st));
-        return 0;
+        return 1;
     }
     const int gi = graph_index(streams[0], std::min(longest, c.dec_window));
     const int splits = graph_splits(streams[0], gi);
     CK(hipMemcpyAsync(b->slots, hs, sizeof(BatchSlot) * nb, hipMemcpyHostToDevice, b->st));
     CK(launch_embed_batch(b->slots, nb, m->tok_emb, m->tok_emb_s, c.dec_dim, b->x, b->st));
     // 3. the steps, in chunks of STEP_BATCH replays: after each chunk one copy of the slot
-    //    table + token log comes back; the call ends when no slot is live
+    //    table + token log comes back; the call ends when no slot is live.  The first chunk
+    //    goes out here, the rest in batch_finish.
+    const int k = std::min(STEP_BATCH, K);
+    if (batch_run(b, nb, gb, gi, splits, kv16, k)) return -1;
+    CK(hipMemcpyAsync(hs, b->slots, SLOT_BYTES, hipMemcpyDeviceToHost, b->st));
+    auto& cl = b->call;
+    cl.active = 1;
+    cl.n = n;
+    for (int i = 0; i < n; i++) cl.streams[i] = streams[i];
+    cl.max_steps = max_steps;
+    cl.stop_at_eos = stop_at_eos;
+    cl.K = K;
+    cl.nb = nb;
+    cl.gb = gb;
+    cl.gi = gi;
+    cl.splits = splits;
+    cl.kv16 = kv16;
+    cl.done = 0;
+    cl.k = k;
+    cl.tokens_out = tokens_out;
+    cl.counts_out = counts_out;
+    return 0;
+}
+
+static int batch_finish(vox_hip_batch_t* b) {
+    auto& cl = b->call;
+    if (!cl.active) return set_err("batch_finish: no begun call");
+    cl.active = 0;
+    const int n = cl.n, max_steps = cl.max_steps, K = cl.K;
+    vox_hip_stream_t** streams = cl.streams;
+    int* tokens_out = cl.tokens_out;
+    int* counts_out = cl.counts_out;
+    if (K == 0) {
+        // a begun call with nothing to run (vox_hip_batch_begin_rows)
+        for (int i = 0; i < n; i++) counts_out[i] = 0;
+        b->lnb = 0;
+        return 0;
+    }
+    BatchSlot* hs = b->hslots;
     int* htok = slot_toklog(hs);
     int got[VOX_MAX_BATCH] = {0};
-    int done = 0;
-    while (done < K) {
-        const int k = std::min(STEP_BATCH, K - done);
-        if (batch_run(b, nb, gb, gi, splits, kv16, k)) return -1;
-        CK(hipMemcpyAsync(hs, b->slots, SLOT_BYTES, hipMemcpyDeviceToHost, b->st));
+    int done = 0, k = cl.k;
+    for (;;) {
+        // the chunk of k steps in flight (its slot table + token log copy queued behind it)
         CK(hipStreamSynchronize(b->st));
         done += k;
         bool any = false;
@@ -2942,10 +2990,14 @@ static int batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, c
             got[i] = p;
             any = any || hs[i].live;
         }
-        if (!any) break;
+        if (!any || done >= K) break;
+        k = std::min(STEP_BATCH, K - done);
+        if (batch_run(b, cl.nb, cl.gb, cl.gi, cl.splits, cl.kv16, k)) return -1;
+        CK(hipMemcpyAsync(hs, b->slots, SLOT_BYTES, hipMemcpyDeviceToHost, b->st));
     }
     // 4. host mirrors
     int total = 0;
+    const int stop_at_eos = cl.stop_at_eos;
     for (int i = 0; i < n; i++) {
         vox_hip_stream_t* s = streams[i];
         const int p = got[i];
@@ -2963,9 +3015,41 @@ static int batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, c
     return total;
 }
 
+static int batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, const int* rows, int max_steps,
+                        int stop_at_eos, int* tokens_out, int* counts_out) {
+    const int r = batch_begin(b, streams, n, rows, max_steps, stop_at_eos, tokens_out, counts_out);
+    if (r < 0) return -1;
+    return r ? 0 : batch_finish(b);
+}
+
 extern "C" int vox_hip_batch_decode(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, int max_steps,
                                     int stop_at_eos, int* tokens_out, int* counts_out) {
     return batch_decode(b, streams, n, nullptr, max_steps, stop_at_eos, tokens_out, counts_out);
+}
+
+extern "C" int vox_hip_batch_begin_rows(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, const int* rows,
+                                        int max_steps, int stop_at_eos, int* tokens_out, int* counts_out) {
+    if (!rows) return set_err("batch_begin_rows: null rows");
+    const int r = batch_begin(b, streams, n, rows, max_steps, stop_at_eos, tokens_out, counts_out);
+    if (r < 0) return -1;
+    if (r) {
+        // nothing to run: an empty call that batch_finish completes
+        b->call = {};
+        b->call.active = 1;
+        b->call.n = n;
+        for (int i = 0; i < n; i++) b->call.streams[i] = streams[i];
+        b->call.max_steps = max_steps;
+        b->call.tokens_out = tokens_out;
+        b->call.counts_out = counts_out;
+        b->call.K = 0;
+        b->call.k = 0;
+    }
+    return 0;
+}
+
+extern "C" int vox_hip_batch_finish(vox_hip_batch_t* b) {
+    if (!b) return set_err("batch_finish: null batch");
+    return batch_finish(b);
 }
 
 extern "C" int vox_hip_batch_decode_rows(vox_hip_batch_t* b, vox_hip_stream_t** streams, int n, const int* rows,

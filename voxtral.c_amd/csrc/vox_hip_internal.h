@@ -203,10 +203,15 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
 int skl_splits(int K, int N = 0);
 // ssq: RMSNorm applied to the results (planes from launch_resid_xw_fplanes, nsl slices per row)
 constexpr int SKL_MAX_SLICES = 12;  // D <= 3072
+// pair: 17..32 rows through k_skl2 (both row blocks in one block; same bits) where its
+// configuration exists (the batched step)
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
-                           float* part, hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f);
+                           float* part, hipStream_t st, const float* ssq = nullptr, int nsl = 0, float eps = 0.f,
+                           int pair = 0);
 hipError_t launch_gemm_skl_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, int N, int nb, float* part,
                                hipStream_t st);  // tools/kbench sweep
+hipError_t launch_gemm_skl2_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, int N, int nb, float* part,
+                                hipStream_t st);  // tools/kbench sweep: 17..32 rows, weights shared by both row blocks
 // x += the S slabs (+ bias); planes of x * w (* (1 + ada)); the row's sums of squares per
 // 256-column slice to ssq[row / 16][D / 256][row % 16] (the inverse RMS is applied by
 // launch_gemm_skl)

@@ -2439,6 +2439,108 @@ __global__ __launch_bounds__(NW * 64) void k_skl(const uint16_t* __restrict__ xs
     }
 }
 
+// k_skl for 17..32 rows (two row blocks of 16) in one block: the planes of both row blocks'
+// K-slice sit in LDS (2 x KS x 6 KiB) and each weight fragment a wave loads feeds the MFMAs of
+// both, so a weight byte crosses the CU's load path once per step instead of once per row
+// block (k_skl's Z > 1 grid streams each slice twice, the second time from L2).  Same splits,
+// per-output summation order and slab layout [rb][s][16][N] as k_skl: the same bits.
+template <int WQ8, int NW, int KS, int SC = 0>
+__global__ __launch_bounds__(NW * 64) void k_skl2(const uint16_t* __restrict__ xs, int K,
+                                                  const uint8_t* __restrict__ W, const float* __restrict__ wscale,
+                                                  int N, int nb, float* __restrict__ part,
+                                                  const float* __restrict__ ssq = nullptr, int nsl = 0, float eps = 0.f) {
+    __shared__ uint4 xb[2][KS * 6 * 64];  // [row block][block][plane][half][lane]
+    __shared__ float s_sq[SC ? 2 * SK_ROWS * SKL_MAX_SLICES : 1];
+    constexpr int FB = WQ8 ? 1024 : 2048, NH = WQ8 ? 1 : 2;
+    constexpr int NF = KS * 6 / NW;  // 16-B plane pieces per thread and row block
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int KB = K >> 6, S = KB / KS, X = N / (16 * NW);
+    const int u = blockIdx.x;
+    const int s = u / X, kb0 = s * KS;
+    const int g = (u % X) * NW + wave;
+    const size_t P = (size_t)SK_ROWS * K;
+    uint4 f[2][NF];
+#pragma unroll
+    for (int z = 0; z < 2; z++)
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const int idx = tid + i * NW * 64;
+            const int blk = idx / 384, rem = idx % 384;
+            const int p = rem >> 7, t = (rem >> 6) & 1, l = rem & 63;
+            f[z][i] = *reinterpret_cast<const uint4*>(xs + (size_t)z * 3 * P + p * P + (size_t)((kb0 + blk) * 2 + t) * 512 + l * 8);
+        }
+    constexpr int NSQ = SC ? (2 * SK_ROWS * SKL_MAX_SLICES + NW * 64 - 1) / (NW * 64) : 1;
+    float sqv[NSQ];
+    if (SC) {
+#pragma unroll
+        for (int i = 0; i < NSQ; i++) {
+            const int e = tid + i * NW * 64;  // (z, t, j) = ssq[z][t][j], z = e / (nsl * 16)
+            sqv[i] = e < 2 * nsl * SK_ROWS ? ssq[e] : 0.f;
+        }
+    }
+    const __amdgpu_buffer_rsrc_t Wd =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g * KB * FB, 0, KB * FB, 0x00020000);
+    u32x4 a[KS][NH];
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < NH; t++) a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(Wd, lane * 16 + t * 1024, (kb0 + kb) * FB, 2);
+#pragma unroll
+    for (int z = 0; z < 2; z++)
+#pragma unroll
+        for (int i = 0; i < NF; i++) xb[z][tid + i * NW * 64] = f[z][i];
+    if (SC) {
+#pragma unroll
+        for (int i = 0; i < NSQ; i++)
+            if (tid + i * NW * 64 < 2 * nsl * SK_ROWS) s_sq[tid + i * NW * 64] = sqv[i];
+    }
+    __syncthreads();
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kb = 0; kb < KS; kb++)
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            bf16x8 af;
+            if (WQ8) {
+                const u32x4 q = a[kb][0];
+                af = t ? i8x8_bf16(q.z, q.w) : i8x8_bf16(q.x, q.y);
+            } else {
+                const u32x4 q = a[kb][t];
+                af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
+            }
+#pragma unroll
+            for (int z = 0; z < 2; z++)
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    acc[z] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        af, __builtin_bit_cast(bf16x8, xb[z][((kb * 3 + p) * 2 + t) * 64 + lane]), acc[z], 0, 0, 0);
+        }
+    const int j = lane & 15;
+#pragma unroll
+    for (int z = 0; z < 2; z++) {
+        if (SC) {
+            float sv[SKL_MAX_SLICES];
+#pragma unroll
+            for (int t = 0; t < SKL_MAX_SLICES; t++) sv[t] = s_sq[(z * nsl + min(t, nsl - 1)) * SK_ROWS + j];
+            float ss = 0.f;
+#pragma unroll
+            for (int t = 0; t < SKL_MAX_SLICES; t++)
+                if (t < nsl) ss += sv[t];
+            const float inv = 1.0f / sqrtf(ss / (float)K + eps);
+#pragma unroll
+            for (int i = 0; i < 4; i++) acc[z][i] *= inv;
+        }
+        if (z * SK_ROWS + j < nb) {
+            float* pz = part + (size_t)z * S * SK_ROWS * N;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int row = g * 16 + (lane >> 4) * 4 + i;
+                pz[((size_t)s * SK_ROWS + j) * N + row] = WQ8 ? acc[z][i] * wscale[row] : acc[z][i];
+            }
+        }
+    }
+}
+
 // Residual + the planes of an RMSNorm without its row reduction: x += the S slabs of the
 // previous projection (+ bias, summed in split order as k_resid_rmsnorm_fplanes), the row
 // written back, the planes of x * w (* (1 + ada)) -- the inverse RMS is applied by the next
@@ -3544,8 +3646,42 @@ int skl_splits(int K, int N) {
     return c6 < c8 ? KB / 6 : S8;
 }
 
+template <int Q, int NW, int KS>
+static hipError_t skl2_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
+                              float* part, hipStream_t st, const float* ssq, int nsl, float eps) {
+    const int grid = (N / (16 * NW)) * (K / (64 * KS));
+    if (ssq)
+        hipLaunchKernelGGL((k_skl2<Q, NW, KS, 1>), dim3(grid), dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W),
+                           wscale, N, nb, part, ssq, nsl, eps);
+    else
+        hipLaunchKernelGGL((k_skl2<Q, NW, KS, 0>), dim3(grid), dim3(NW * 64), 0, st, xs, K, static_cast<const uint8_t*>(W),
+                           wscale, N, nb, part, nullptr, 0, 0.f);
+    return hipGetLastError();
+}
+
+#define SKL2_CONFIGS(X) X(4, 4) X(8, 4) X(4, 6) X(4, 8) X(8, 8)
+static hipError_t skl2_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, const float* wscale, int N,
+                           int nb, float* part, hipStream_t st, const float* ssq, int nsl, float eps) {
+    if (nb <= SK_ROWS || nb > 2 * SK_ROWS || K % 64 || (K / 64) % ks || N % (16 * nw) || (ks * 6) % nw ||
+        (ssq && (nsl < 1 || nsl > SKL_MAX_SLICES)))
+        return hipErrorInvalidValue;
+#define SKL2_X(NWW, KSS)                                                                                      \
+    if (nw == NWW && ks == KSS)                                                                               \
+        return wscale ? skl2_launch<1, NWW, KSS>(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps)           \
+                      : skl2_launch<0, NWW, KSS>(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
+    SKL2_CONFIGS(SKL2_X)
+#undef SKL2_X
+    return hipErrorInvalidValue;
+}
+
+// tools/kbench: k_skl2 (17..32 rows) at a given waves-per-block / 64-k blocks per split
+hipError_t launch_gemm_skl2_cfg(int nw, int ks, const uint16_t* xs, int K, const void* Wf, int N, int nb, float* part,
+                                hipStream_t st) {
+    return skl2_cfg(nw, ks, xs, K, Wf, nullptr, N, nb, part, st, nullptr, 0, 0.f);
+}
+
 hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb,
-                           float* part, hipStream_t st, const float* ssq, int nsl, float eps) {
+                           float* part, hipStream_t st, const float* ssq, int nsl, float eps, int pair) {
     const int S = skl_splits(K, N);
     // ssq: each row block's nsl x 16 sums ride with its planes (nsl * 16 <= the block's threads)
     if (nb < 1 || nb > SK_MAX_ROWS || K % 64 || !S || (ssq && (nsl < 1 || nsl > SKL_MAX_SLICES)))
@@ -3553,6 +3689,13 @@ hipError_t launch_gemm_skl(const uint16_t* xs, int K, const void* Wf, const floa
     const int ks = K / 64 / S;
     const int nw = ks == 6 ? 4 : skl_nw_for(N, S);
     if (N % (16 * nw)) return hipErrorInvalidValue;
+    // pair (the batched step's 17..32 rows): both row blocks in one k_skl2 block at the same
+    // waves and splits -- the same bits, each weight fragment loaded once (QKV 12.7 -> 11.4,
+    // wo 9.8 -> 8.7, W2 17.7 -> 16.7 us at 32 rows, profiles/r6_kbench_skl2.txt)
+    if (pair && nb > SK_ROWS && nb <= 2 * SK_ROWS) {
+        const hipError_t e = skl2_cfg(nw, ks, xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
+        if (e != hipErrorInvalidValue) return e;
+    }
 #define SKL_X(Q, NWW, KSS) \
     if ((wscale != nullptr) == Q && nw == NWW && ks == KSS) return skl_launch<Q, NWW, KSS>(xs, K, Wf, wscale, N, nb, part, st, ssq, nsl, eps);
     SKL_X(0, 4, 8) SKL_X(0, 8, 8) SKL_X(0, 4, 4) SKL_X(0, 8, 4) SKL_X(0, 4, 6)

@@ -1060,6 +1060,12 @@ void vh_sched_stats(const vh_sched_t *q, vh_sched_stats_t *out) {
     }
 }
 
+static int sched_steps_first(void) {
+    /* VOX_HIP_SCHED_STEPS_FIRST=0: the round-5 order (encoder pass enqueued before the steps) */
+    const char *e = getenv("VOX_HIP_SCHED_STEPS_FIRST");
+    return !(e && atoi(e) == 0);
+}
+
 static int sched_overlap(void) {
     /* VOX_HIP_SCHED_OVERLAP=0: the encoder pass completes before the batched steps start
      * (read per run, so one process can serve both ways) */
@@ -1067,11 +1073,16 @@ static int sched_overlap(void) {
     return !(e && atoi(e) == 0);
 }
 
+static int sched_encode(vh_sched_t *q, int overlap);
+
 /* the batched steps of one run: every stream whose decoder can run (ran[i]) goes into one
  * vox_hip_batch_decode call per round, another round only when a stream hit the step cap;
  * bounded: stream i reads only its first rows[i] adapter rows (an encoder pass may still be
- * running on its queue) */
-static int sched_steps(vh_sched_t *q, int bounded, const int *rows, const int *ran, int *eos, int *total) {
+ * running on its queue).  enc_between: the run's encoder pass is enqueued between the first
+ * round's begin and finish (vox_hip_batch_begin_rows / vox_hip_batch_finish), so the steps are
+ * on the device before the pass; *enc_done tells whether that happened */
+static int sched_steps(vh_sched_t *q, int bounded, const int *rows, const int *ran, int *eos, int *total,
+                       int enc_between, int *enc_done) {
     for (int iter = 0;; iter++) {
         vox_hip_stream_t *hs[VH_SCHED_MAX];
         int idx[VH_SCHED_MAX], counts[VH_SCHED_MAX], gen0[VH_SCHED_MAX], brows[VH_SCHED_MAX], nb = 0;
@@ -1095,10 +1106,21 @@ static int sched_steps(vh_sched_t *q, int bounded, const int *rows, const int *r
             q->batch = vox_hip_batch_create(q->ctx->model, q->cap);
             if (!q->batch) return fail("batch: %s", vox_hip_last_error());
         }
-        const double t0 = now_ms();
+        double t0 = now_ms();
         const int cap = q->step_cap > 0 && q->step_cap < VH_SCHED_STEPS ? q->step_cap : VH_SCHED_STEPS;
-        const int r = bounded ? vox_hip_batch_decode_rows(q->batch, hs, nb, brows, cap, 1, q->tok, counts)
-                              : vox_hip_batch_decode(q->batch, hs, nb, cap, 1, q->tok, counts);
+        int r;
+        if (bounded && enc_between && iter == 0) {
+            if (vox_hip_batch_begin_rows(q->batch, hs, nb, brows, cap, 1, q->tok, counts) < 0)
+                return fail("batched decoder: %s", vox_hip_last_error());
+            const double tb = now_ms();
+            if (sched_encode(q, 1)) return -1;
+            *enc_done = 1;
+            t0 += now_ms() - tb;  /* the pass's enqueue is the encoder's time */
+            r = vox_hip_batch_finish(q->batch);
+        } else {
+            r = bounded ? vox_hip_batch_decode_rows(q->batch, hs, nb, brows, cap, 1, q->tok, counts)
+                        : vox_hip_batch_decode(q->batch, hs, nb, cap, 1, q->tok, counts);
+        }
         if (r < 0) return fail("batched decoder: %s", vox_hip_last_error());
         const double dt = now_ms() - t0;
         q->stats.batch_calls++;
@@ -1133,11 +1155,14 @@ int vh_sched_run(vh_sched_t *q) {
     int total = 0;
     int eos[VH_SCHED_MAX] = {0}, ran[VH_SCHED_MAX] = {0};
     /* Overlap: the batched steps decode the adapter rows that exist when the run starts while
-     * this run's encoder pass (enqueued first, on the streams' queues) computes the next ones.
-     * With a step cap set, those rows are decoded by the next run; with no cap (step_cap <= 0)
-     * this run waits for the pass and drains them in a second round of steps.  Greedy ids do not depend on when a row is decoded, so
-     * a stream's ids are unchanged.  Live-mode streams keep the sequential order: their restart
-     * checks belong after a drain of every row of the chunk (voxtral.c:1189-1239). */
+     * this run's encoder pass (on the streams' queues) computes the next ones.  The steps are
+     * begun first and the pass is enqueued behind them (the pass's ~400 eager launches take the
+     * host longer than the device needs to run them, so a pass enqueued first kept the steps off
+     * the device until it was nearly done: DESIGN.md 16.5).  With a step cap set, the pass's rows
+     * are decoded by the next run; with no cap (step_cap <= 0) this run waits for the pass and
+     * drains them in a second round of steps.  Greedy ids do not depend on when a row is
+     * decoded, so a stream's ids are unchanged.  Live-mode streams keep the sequential order:
+     * their restart checks belong after a drain of every row of the chunk (voxtral.c:1189-1239). */
     int overlap = sched_overlap() && sched_batch_encode();
     for (int i = 0; i < q->n; i++) overlap = overlap && !q->s[i]->continuous;
     int rows[VH_SCHED_MAX] = {0};
@@ -1152,7 +1177,51 @@ int vh_sched_run(vh_sched_t *q) {
             ran[i] = st6[3] || rows[i] >= 1 + 32 + s->ctx->delay_tokens;
         }
     /* 0. every attached stream's deferred chunk through one batched encoder pass (the layers'
-     *    weights read once for all of them) */
+     *    weights read once for all of them); with the overlap it is enqueued after the first
+     *    batched steps (below), so those are on the device first */
+    int enc_done = 0;
+    if (!overlap || !sched_steps_first()) {
+        if (sched_encode(q, overlap)) return -1;
+        enc_done = 1;
+    }
+    /* 1-2. every stream whose decoder can run -- its prompt's adapter rows are there, or it
+     *      already decodes and has rows left -- goes into the batched steps: the new ones'
+     *      prefills share one stacked pass and they take their first token there, streams
+     *      stop on the device when their rows run out or at EOS, streams with --alt keep their
+     *      candidates (vox_hip_batch_decode); one call per round, another only when a stream
+     *      hit the per-call step cap */
+    if (!overlap)
+        for (int i = 0; i < q->n; i++) {
+            ran[i] = decoder_ready(q->s[i]);
+            rows[i] = vox_hip_stream_adapter_tokens(q->s[i]->st);
+        }
+    if (sched_steps(q, overlap, rows, ran, eos, &total, !enc_done, &enc_done)) return -1;
+    if (!enc_done && sched_encode(q, overlap)) return -1;  /* no steps ran this time */
+    /* 3 (overlap). the pass beside the steps completes before the run returns */
+    if (overlap) {
+        for (int i = 0; i < q->n; i++)
+            if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
+        /* without a step cap a run drains every stream (vh_sched_set_step_cap): the rows this
+         * run's pass produced are decoded now, after the pass, instead of by the next run */
+        if (q->step_cap <= 0) {
+            for (int i = 0; i < q->n; i++) {
+                ran[i] = decoder_ready(q->s[i]);
+                rows[i] = vox_hip_stream_adapter_tokens(q->s[i]->st);
+            }
+            if (sched_steps(q, 0, rows, ran, eos, &total, 0, &enc_done)) return -1;
+        }
+    }
+    /* 4. per-stream live-mode restarts (voxtral.c:1189-1239) */
+    for (int i = 0; i < q->n; i++)
+        if (ran[i] == 1 && after_drain(q->s[i], eos[i])) return -1;
+    q->stats.runs++;
+    q->stats.run_ms += now_ms() - t_run;
+    return total;
+}
+
+/* the run's encoder pass over every attached stream's deferred chunk (step 0 of vh_sched_run);
+ * overlap: left running on the streams' queues (vh_sched_run syncs them before it returns) */
+static int sched_encode(vh_sched_t *q, int overlap) {
     {
         vox_hip_stream_t *hs[VH_SCHED_MAX];
         const float *mp[VH_SCHED_MAX];
@@ -1196,38 +1265,7 @@ int vh_sched_run(vh_sched_t *q) {
             }
         }
     }
-    /* 1-2. every stream whose decoder can run -- its prompt's adapter rows are there, or it
-     *      already decodes and has rows left -- goes into the batched steps: the new ones'
-     *      prefills share one stacked pass and they take their first token there, streams
-     *      stop on the device when their rows run out or at EOS, streams with --alt keep their
-     *      candidates (vox_hip_batch_decode); one call per round, another only when a stream
-     *      hit the per-call step cap */
-    if (!overlap)
-        for (int i = 0; i < q->n; i++) {
-            ran[i] = decoder_ready(q->s[i]);
-            rows[i] = vox_hip_stream_adapter_tokens(q->s[i]->st);
-        }
-    if (sched_steps(q, overlap, rows, ran, eos, &total)) return -1;
-    /* 3 (overlap). the pass beside the steps completes before the run returns */
-    if (overlap) {
-        for (int i = 0; i < q->n; i++)
-            if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
-        /* without a step cap a run drains every stream (vh_sched_set_step_cap): the rows this
-         * run's pass produced are decoded now, after the pass, instead of by the next run */
-        if (q->step_cap <= 0) {
-            for (int i = 0; i < q->n; i++) {
-                ran[i] = decoder_ready(q->s[i]);
-                rows[i] = vox_hip_stream_adapter_tokens(q->s[i]->st);
-            }
-            if (sched_steps(q, 0, rows, ran, eos, &total)) return -1;
-        }
-    }
-    /* 4. per-stream live-mode restarts (voxtral.c:1189-1239) */
-    for (int i = 0; i < q->n; i++)
-        if (ran[i] == 1 && after_drain(q->s[i], eos[i])) return -1;
-    q->stats.runs++;
-    q->stats.run_ms += now_ms() - t_run;
-    return total;
+    return 0;
 }
 
 /* ------------------------------------------------------------------------

@@ -43,6 +43,7 @@ EXPORTS = [
     "vox_hip_stream_reset", "vox_hip_stream_reset_decoder", "vox_hip_stream_encode_mel",
     "vox_hip_stream_adapter_tokens", "vox_hip_stream_read_adapter", "vox_hip_stream_decode",
     "vox_hip_batch_create", "vox_hip_batch_free", "vox_hip_batch_decode", "vox_hip_batch_decode_rows",
+    "vox_hip_batch_begin_rows", "vox_hip_batch_finish",
     "vox_hip_batch_read_logits",
     "vox_hip_batch_stats",
     "vox_hip_stream_state", "vox_hip_stream_set_alt", "vox_hip_stream_read_alts", "vox_hip_sgemm_bf16", "vox_hip_sgemm_q8", "vox_hip_fused_qkv_bf16",
@@ -88,6 +89,8 @@ def lib():
         "vox_hip_batch_create": (P, [P, I]), "vox_hip_batch_free": (None, [P]),
         "vox_hip_batch_decode": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, I, I, ip, ip]),
         "vox_hip_batch_decode_rows": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, ip, I, I, ip, ip]),
+        "vox_hip_batch_begin_rows": (I, [P, ctypes.POINTER(ctypes.c_void_p), I, ip, I, I, ip, ip]),
+        "vox_hip_batch_finish": (I, [P]),
         "vox_hip_batch_read_logits": (I, [P, P, fp]),
         "vox_hip_batch_stats": (I, [P, ctypes.POINTER(ctypes.c_longlong)]),
         "vox_hip_stream_set_alt": (I, [P, I, F]),

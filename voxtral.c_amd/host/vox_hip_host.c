@@ -1156,9 +1156,9 @@ int vh_sched_run(vh_sched_t *q) {
     int eos[VH_SCHED_MAX] = {0}, ran[VH_SCHED_MAX] = {0};
     /* Overlap: the batched steps decode the adapter rows that exist when the run starts while
      * this run's encoder pass (on the streams' queues) computes the next ones.  The steps are
-     * begun first and the pass is enqueued behind them (the pass's ~400 eager launches take the
-     * host longer than the device needs to run them, so a pass enqueued first kept the steps off
-     * the device until it was nearly done: DESIGN.md 16.5).  With a step cap set, the pass's rows
+     * begun first and the pass is enqueued behind them, so the run's first steps are on the
+     * device before the host spends ~1.4 ms on the pass's eager launches (served 16 streams
+     * +3.4 %; the two queues' kernels still take turns on the device).  With a step cap set, the pass's rows
      * are decoded by the next run; with no cap (step_cap <= 0) this run waits for the pass and
      * drains them in a second round of steps.  Greedy ids do not depend on when a row is
      * decoded, so a stream's ids are unchanged.  Live-mode streams keep the sequential order:

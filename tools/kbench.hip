@@ -12,7 +12,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_dev.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_gemmf_rr, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -920,49 +920,6 @@ int main(int argc, char** argv) {
                 }
                 g_gemmf_order = 0;  // by shape
             }
-    }
-    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmfx")) {
-        // k_gemmf XCD rounds (order 3: the blocks of an XCD on its own column tiles, row tiles
-        // in rounds of rr) against the shape's default order; a workspace for 16 rounds, the
-        // outputs compared with the default order's (another split of K: not the same bits)
-        const size_t wsn = (size_t)16 * gemmf_grid() * 8192;
-        float* gws = (float*)dmalloc(wsn * 4, 0);
-        int* gfl = (int*)dmalloc(gemmf_flag_ints() * 4, 0);
-        uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 1);
-        uint16_t* go = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 0);
-        float* gc = (float*)dmalloc((size_t)1024 * 18432 * 4, 0);
-        std::vector<float> h0((size_t)1024 * 18432), h1((size_t)1024 * 18432);
-        int epoch = 0;
-        struct G { const char* n; int epi, N, K; const uint16_t* W; };
-        for (int M : {400, 677, 1024})
-            for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
-                        G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]},
-                        G{"dqkv", EPI_STORE, 6144, 3072, wqkv[3]}, G{"dw13", EPI_SWIGLU, 18432, 3072, w13[3]}}) {
-                if (g.n[0] == 'd' && M != 677) continue;
-                const int ldc = g.epi == EPI_SWIGLU ? g.N / 2 : g.N;
-                const size_t nc = (size_t)M * ldc;
-                for (int v = 0; v < 6; v++) {
-                    g_gemmf_order = v == 0 ? 0 : 3;
-                    g_gemmf_rr = v == 0 ? 0 : v;  // 1..4 row tiles a round, 5: the fewest rounds 32 MB hold
-                    const size_t wsv = v == 5 ? (size_t)8 << 20 : wsn;
-                    if (v == 5) g_gemmf_rr = 0;
-                    // EPI_RESID accumulates into C: compare one launch from a zeroed C
-                    CK(hipMemsetAsync(gc, 0, nc * 4, st));
-                    CK(launch_gemmf(g.epi, 3, gp, g.K, M, g.W, g.N, nullptr, gc, ldc, g.epi == EPI_SWIGLU ? go : nullptr, gws, wsv, gfl, ++epoch, st));
-                    CK(hipStreamSynchronize(st));
-                    CK(hipMemcpy((v == 0 ? h0 : h1).data(), gc, nc * 4, hipMemcpyDeviceToHost));
-                    double md = 0, mx = 0;
-                    if (v) for (size_t i = 0; i < nc; i++) { md = std::max(md, (double)fabsf(h0[i] - h1[i])); mx = std::max(mx, (double)fabsf(h0[i])); }
-                    double us = timeit([&] { CK(launch_gemmf(g.epi, 3, gp, g.K, M, g.W, g.N, nullptr, gc, ldc,
-                                                             g.epi == EPI_SWIGLU ? go : nullptr, gws, wsv, gfl, ++epoch, st)); }, 20, st);
-                    printf("gemmfx %-4s M=%4d %5dx%-4d %s rr %d %9.2f us  %8.1f TFLOP/s (useful)  max|d| %.3g of max %.3g\n", g.n, M, g.N, g.K,
-                           v == 0 ? "default" : "xcd    ", v == 5 ? 0 : v, us, 2.0 * M * g.N * g.K / us / 1e6, md, mx);
-                    fflush(stdout);
-                }
-                g_gemmf_order = 0;
-                g_gemmf_rr = 0;
-            }
-        return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmfm")) {
         // k_gemmf at small M (streaming chunks, prefills, the one-shot flush chunk): least

@@ -2132,7 +2132,7 @@ extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
     // k_gemmf stage ranges an owner recomputed because a partial did not arrive in time
     int rec = 0;
     if (s->gflags) {
-        CK(hipMemcpyAsync(&rec, s->gflags + gemmf_recompute_off(), sizeof rec, hipMemcpyDeviceToHost, s->st));
+        CK(hipMemcpyAsync(&rec, s->gflags + gemmf_grid(), sizeof rec, hipMemcpyDeviceToHost, s->st));
         CK(hipStreamSynchronize(s->st));
     }
     out8[6] = rec;

@@ -75,12 +75,6 @@ struct GemmfArgs {
     long long U;         // T * S work units
     int MT;              // row tiles
     int colmajor;        // tile order: 0 = t = mt NT + nt (row tile major), 1 = t = nt MT + mt
-    // XCD rounds (rr > 0): the blocks of XCD x = b % 8 own column tiles [x NT / 8, (x + 1) NT / 8)
-    // and take the row tiles in rounds of rr; in a round they split that round's units
-    // stream-K fashion among themselves, so all of an XCD's blocks work on the same rr row
-    // tiles' planes (shared through its L2) and, round after round, the same weights (resident
-    // in its L2).  Partial tiles and flags per (round, block).
-    int rr;
 };
 
 
@@ -293,6 +287,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wc = wave & 3, r0 = (wave >> 2) * RBW;
     const int G = gridDim.x, b = blockIdx.x;
+    const long long u0 = gf_bound(a.U, G, b), u1 = gf_bound(a.U, G, b + 1);
     constexpr int TILE = C::NWV * RBW * NG * 256;  // floats of one partial tile (waves x RBW x NG x 64 lanes x 4)
     const int rbm = (a.M + 15) >> 4;                // row blocks holding rows
     const __amdgpu_buffer_rsrc_t Ws = __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, 0x7fffffff, 0x00020000);
@@ -300,27 +295,11 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
     auto poff = [&](int slotb, int i, int g) {
         return (int)(((size_t)slotb * TILE + ((size_t)(wave * RBW + i) * NG + g) * 256 + lane * 4) * 4);
     };
-    // A segment: UR units split over Gs blocks of which this is number lb (the group's
-    // blocks in order: physical ids pid(k)), its tile of unit u from tile_of, partial slot
-    // and flag of group block k at slot(k).  One segment over the whole grid by default; one
-    // per round with XCD rounds.
-    const int nseg = a.rr > 0 ? (a.MT + a.rr - 1) / a.rr : 1;
-    const int xcd = b & 7, G8 = G >> 3, lbx = b >> 3;
-    const int ct0 = a.rr > 0 ? xcd * a.NT / 8 : 0, ntx = a.rr > 0 ? (xcd + 1) * a.NT / 8 - ct0 : a.NT;
-    for (int seg = 0; seg < nseg; seg++) {
-    const int rt0 = seg * a.rr, nrt = a.rr > 0 ? min(a.rr, a.MT - rt0) : a.MT;
-    const long long UR = a.rr > 0 ? (long long)nrt * ntx * a.S : a.U;
-    const int Gs = a.rr > 0 ? G8 : G, lb = a.rr > 0 ? lbx : b;
-    auto pid = [&](int k) { return a.rr > 0 ? k * 8 + xcd : k; };
-    auto slot = [&](int k) { return a.rr > 0 ? seg * G + pid(k) : k; };
-    const long long u0 = gf_bound(UR, Gs, lb), u1 = gf_bound(UR, Gs, lb + 1);
     long long u = u0;
     while (u < u1) {
         const int t = (int)(u / a.S), s0 = (int)(u % a.S);
         const int s1 = (int)min((long long)a.S, s0 + (u1 - u));
-        // XCD rounds: tile t of the round = row tile rt0 + t / ntx, column tile ct0 + t % ntx
-        const int mt = a.rr > 0 ? rt0 + t / ntx : a.colmajor ? t % a.MT : t / a.NT;
-        const int nt = a.rr > 0 ? ct0 + t % ntx : a.colmajor ? t / a.MT : t % a.NT;
+        const int mt = a.colmajor ? t % a.MT : t / a.NT, nt = a.colmajor ? t / a.MT : t % a.NT;
         f32x4 acc[RBW][NG];
 #pragma unroll
         for (int i = 0; i < RBW; i++)
@@ -335,10 +314,10 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
             for (int i = 0; i < RBW; i++)
 #pragma unroll
                 for (int g = 0; g < NG; g++)
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][g]), Ws, poff(slot(lb), i, g), 0, 16);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][g]), Ws, poff(b, i, g), 0, 16);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(&a.flags[slot(lb)], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) __hip_atomic_store(&a.flags[b], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             continue;
         }
         // stage 0 is ours: add the later parts in block order, then the epilogue.  The lanes of
@@ -346,7 +325,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
         // last of them once instead of one flag round trip per block
         const long long tend = (long long)(t + 1) * a.S;
         int npb = 0;
-        while (lb + 1 + npb < Gs && gf_bound(UR, Gs, lb + 1 + npb) < tend) npb++;
+        while (b + 1 + npb < G && gf_bound(a.U, G, b + 1 + npb) < tend) npb++;
         // npb <= 62: launch_gemmf refuses a minimum stage count that would let more blocks touch a tile
         if (npb > 0) {
             if (wave == 0) {
@@ -354,7 +333,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
                 bool ok = !mine;
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 while (a.wait_ticks >= 0) {
-                    if (!ok) ok = __hip_atomic_load(&a.flags[slot(min(lb + 1 + lane, Gs - 1))], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+                    if (!ok) ok = __hip_atomic_load(&a.flags[b + 1 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
                     if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > (unsigned long long)a.wait_ticks) break;
                     __builtin_amdgcn_s_sleep(2);
@@ -369,22 +348,22 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
             const unsigned long long okm = *s_okm;
             __syncthreads();
             for (int k = 0; k < npb; k++) {
-                const int pb = lb + 1 + k;
+                const int pb = b + 1 + k;
                 f32x4 part[RBW][NG];
                 if ((okm >> k) & 1) {
 #pragma unroll
                     for (int i = 0; i < RBW; i++)
 #pragma unroll
                         for (int g = 0; g < NG; g++)
-                            part[i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Ws, poff(slot(pb), i, g), 0, 16));
+                            part[i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Ws, poff(pb, i, g), 0, 16));
                 } else {
                     // the publishing block has not run: its stage range of this tile, computed here
 #pragma unroll
                     for (int i = 0; i < RBW; i++)
 #pragma unroll
                         for (int g = 0; g < NG; g++) part[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    const int q0 = (int)(gf_bound(UR, Gs, pb) - (long long)t * a.S);
-                    const int q1 = (int)(min(gf_bound(UR, Gs, pb + 1), tend) - (long long)t * a.S);
+                    const int q0 = (int)(gf_bound(a.U, G, pb) - (long long)t * a.S);
+                    const int q1 = (int)(min(gf_bound(a.U, G, pb + 1), tend) - (long long)t * a.S);
                     gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, q0, q1, part);
                 }
 #pragma unroll
@@ -405,7 +384,6 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
                 gf_out<EPI>(a, m, (nt * 4 + wc) * NG + g, lane, acc[i][g], acc[i][EPI == EPI_SWIGLU ? g + 1 : g]);
         }
     }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -413,8 +391,7 @@ static int g_cus = 0;
 int g_gemmf_blocks = -1;  // grid size (0 = one block per CU; -1: read VOX_HIP_GEMMF_BLOCKS once)
 int g_gemmf_rb = -1;     // row blocks per tile with two planes (0 = by shape; 4 or 8; -1: VOX_HIP_GEMMF_RB once)
 VOX_KB_KNOB(g_gemmf_minu, 0);  // tools/kbench knob: least stages per block (0 = max(4, half a tile))
-int g_gemmf_order = -1;  // 1 = column-tile-major unit order (a weight tile's row tiles adjacent), 2 = row-tile-major, 3 = XCD rounds, 0 = by shape (-1: VOX_HIP_GEMMF_ORDER once)
-VOX_KB_KNOB(g_gemmf_rr, 0);  // row tiles per XCD round (0 = the fewest the workspace holds)
+int g_gemmf_order = -1;  // 1 = column-tile-major unit order (a weight tile's row tiles adjacent), 2 = row-tile-major, 0 = by shape (-1: VOX_HIP_GEMMF_ORDER once)
 // waves per block with two planes: 16 (4 row shares of a 128- or 64-row tile: 32 x 32 or 16 x
 // 32 per wave, four waves per SIMD) by default, 8 with VOX_HIP_GEMMF_WR=2 (64 x 32 per wave,
 // two per SIMD).  Same unit ranges, same per-output summation order: the same bits.  tools/
@@ -456,11 +433,7 @@ int gemmf_grid() {
     return g_gemmf_blocks ? g_gemmf_blocks : g_cus;
 }
 
-// flags: one per (block, round) for up to GF_MAX_SEG rounds of the XCD-rounds order, then the
-// recompute counter
-static constexpr int GF_MAX_SEG = 16;
-size_t gemmf_flag_ints() { return (size_t)gemmf_grid() * GF_MAX_SEG + 1; }
-size_t gemmf_recompute_off() { return (size_t)gemmf_grid() * GF_MAX_SEG; }
+size_t gemmf_flag_ints() { return (size_t)gemmf_grid() + 1; }
 int set_gemmf_wait(int ticks) {
     const int old = g_gemmf_wait;
     g_gemmf_wait = ticks;
@@ -496,7 +469,7 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     GemmfArgs a;
     a.xs = xs; a.K = K; a.M = M; a.W = static_cast<const uint8_t*>(Wf); a.N = N; a.bias = bias; a.C = C; a.ldc = ldc;
     a.xo = xo; a.ws = ws; a.flags = flags; a.epoch = epoch;
-    a.recomputes = flags + gemmf_recompute_off();  // the counter past the flags (gemmf_flag_ints())
+    a.recomputes = flags + gemmf_grid();  // the counter past the flags (gemmf_flag_ints())
     a.wait_ticks = g_gemmf_wait;
     a.S = K / 64;
     a.NT = N / (64 * NGx);
@@ -511,12 +484,10 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     if (g_gemmf_order < 0) {
         const char* e = getenv("VOX_HIP_GEMMF_ORDER");
         const int v = e ? atoi(e) : 0;
-        g_gemmf_order = (v >= 1 && v <= 3) ? v : 0;
+        g_gemmf_order = (v == 1 || v == 2) ? v : 0;
     }
-    a.colmajor = g_gemmf_order == 1 || g_gemmf_order == 2 ? g_gemmf_order == 1
-                                                           : (np == 3 && a.MT > 4 && (a.MT % 4 != 0 || K > 2048));
+    a.colmajor = g_gemmf_order ? g_gemmf_order == 1 : (np == 3 && a.MT > 4 && (a.MT % 4 != 0 || K > 2048));
     a.U = (long long)a.T * a.S;
-    a.rr = 0;
     // one block per CU, but every block at least half a tile's stages (and 4): a tile split
     // over many blocks costs its owner one partial-tile read per extra block.  One or two row
     // tiles (M <= 128 with three planes: prefills, the flush chunk) leave too few tiles for
@@ -532,20 +503,7 @@ hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const
     int G = gemmf_grid();
     if ((long long)G * minu > a.U) G = (int)std::max(1LL, a.U / minu);
     // one partial tile per block: (4 WR waves) x (RB / WR) x NGx x 64 lanes x 4 floats
-    const size_t tile_f = (size_t)4 * RB * NGx * 256;
-    if ((size_t)G * tile_f > ws_floats) return hipErrorInvalidConfiguration;  // workspace too small
-    // XCD rounds: the whole grid, 8 XCDs with a column tile each at least, and a partial tile
-    // per (block, round) in the workspace (rr row tiles a round: the fewest rounds it holds)
-    if (g_gemmf_order == 3 && G == gemmf_grid() && G % 8 == 0 && a.NT >= 8) {
-        const int segcap = (int)std::min<size_t>(GF_MAX_SEG, ws_floats / ((size_t)G * tile_f));
-        int rr = g_gemmf_rr > 0 ? g_gemmf_rr : 1;
-        while ((a.MT + rr - 1) / rr > segcap) rr++;
-        // every block of every round at least 2 stages (none idle in a round: an owner waits
-        // for each later block of its tile; at most 64 of them touch a tile)
-        const int nseg = (a.MT + rr - 1) / rr, nrt_min = a.MT - (nseg - 1) * rr;
-        const long long upb = (long long)nrt_min * (a.NT / 8) * a.S / (G / 8);
-        if (upb >= 2 && (a.S + upb - 1) / upb + 2 <= 64) a.rr = rr;
-    }
+    if ((size_t)G * 4 * RB * NGx * 256 > ws_floats) return hipErrorInvalidConfiguration;  // workspace too small
 #define GF_EPI(E)                                                                               \
     if (epi == E)                                                                               \
         return np == 3 ? gemmf_launch<E, 3, 4, NG, WR>(a, G, st)                                \

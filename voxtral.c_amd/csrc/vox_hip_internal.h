@@ -258,8 +258,7 @@ hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const v
 // flags: gemmf_grid() ints (zeroed once), epoch: > 0, new for every launch on the stream.
 bool gemmf_ok(int M, int N, int K);
 int gemmf_grid();
-size_t gemmf_flag_ints();      // flags buffer: a flag per (block, round), then the recompute counter
-size_t gemmf_recompute_off();  // index of the recompute counter in it
+size_t gemmf_flag_ints();      // flags buffer: gemmf_grid() flags, then the recompute counter
 int set_gemmf_wait(int ticks); // owner's wait per partial in 100 MHz ticks (< 0: always recompute); returns the old
 size_t gemmf_ws_floats(int blocks);
 hipError_t launch_gemmf(int epi, int np, const uint16_t* xs, int K, int M, const void* Wf, int N, const float* bias,

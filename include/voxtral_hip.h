@@ -300,9 +300,7 @@ int vox_hip_decoder_full_step(vox_hip_stream_t *s, const float *rope_freqs, int 
 /* Average device time (ms) of the last decode call's dominant per-layer GEMV launches and
  * the bytes they streamed; filled only when profiling was enabled.  out8: [0] ms, [1] bytes,
  * [2] launches, [3] ms per launch, [5] bytes per launch, [6] encoder-GEMM stage ranges an
- * owner recomputed because a partial tile did not arrive in time (since creation), [7] decode
- * attention blocks of the fused QKV + attention launch whose wait timed out (since creation;
- * 0 unless the device misbehaved). */
+ * owner recomputed because a partial tile did not arrive in time (since creation). */
 int vox_hip_stream_set_profiling(vox_hip_stream_t *s, int enable);
 int vox_hip_stream_profile(vox_hip_stream_t *s, double *out8);
 /* Synchronise the stream's HIP queue. */

@@ -1,14 +1,14 @@
-"""The short-context decode attention inside the QKV GEMV launch (EPI_QKV_ATT,
-csrc/vox_hip_kernels.hip qkv_att_block): voxtral_decoder.c:709-733 (QKV, RoPE, KV append,
-attention over the last min(pos + 1, window) keys) as one launch per layer while the context
-is <= 256 keys.
+"""Single-stream decode across the short-context attention's range and out of it:
+voxtral_decoder.c:709-733 (QKV, RoPE, KV append, attention over the last min(pos + 1,
+window) keys).  Contexts up to 256 keys run k_attn_short (one 1024-thread block per query
+head, keys 64.. loaded after the position read), longer ones the split attention with the
+merging block.
 
-TINY_LONG keeps Voxtral's head_dim 128 and the 8192-key window (4 query heads on 2 kv heads:
-the 4 key blocks of each kv head spread over the 8 XCD slots), so a stream's steps cross the
-64 / 128 / 192-key block boundaries of the fused launch (1..4 key blocks, the per-head merge
-ticket) and then leave it for the split attention past 256 keys.  Oracle: the CPU
-restatement; every id equal, logits within 5e-5 of the largest magnitude (1e-4 with the
-16-bit ring, tests/test_gpu_kv16.py), and no attention block's wait may time out."""
+TINY_LONG keeps Voxtral's head_dim 128 and the 8192-key window, so a stream's greedy steps
+go from the prompt across 64 / 128 / 192 / 256 keys into the split path, with the f32 and
+the 16-bit ring.  Oracle: the CPU restatement; every id equal, logits of every step within
+5e-5 of the largest magnitude (1e-4 with the 16-bit ring, tests/test_gpu_kv16.py).  (Round
+6 also ran this test on the attention folded into the QKV launch)"""
 import os
 
 import numpy as np
@@ -45,9 +45,9 @@ def models(tiny_weights):
 
 
 @pytest.mark.parametrize("kv16", [False, True])
-def test_fused_qkv_attention_vs_oracle(models, kv16):
+def test_short_attention_into_split_vs_oracle(models, kv16):
     """prefill + 300 greedy steps (contexts from the prompt to past 256 keys): ids equal to
-    the oracle's on every step, logits of every step within the bar, no wait timed out."""
+    the oracle's on every step, logits of every step within the bar."""
     import vox_hip
     import vox_oracle
     hm, om = models
@@ -60,7 +60,6 @@ def test_fused_qkv_attention_vs_oracle(models, kv16):
         s.encode_mel(mel[i:i + CHUNK])
     ids, lg = s.decode(max_steps=n, stop_at_eos=False, want_logits=True)
     st = s.state()
-    prof = s.profile()
     s.close()
     vox_oracle.set_kv_fp16(kv16)
     try:
@@ -76,7 +75,6 @@ def test_fused_qkv_attention_vs_oracle(models, kv16):
     first = next((i for i in range(n) if ids[i] != ref[i]), None)
     assert first is None, (first, ids[first], ref[first])
     r = rel(np.asarray(lg), np.asarray(rlg))
-    print(f"fused QKV + attention ({'16-bit' if kv16 else 'f32'} ring): {n} ids equal, logits rel err {r:.2e}, "
-          f"kv_pos {st['kv_pos']}, wait timeouts {prof['attn_wait_timeouts']}")
+    print(f"short + split attention ({'16-bit' if kv16 else 'f32'} ring): {n} ids equal, logits rel err {r:.2e}, "
+          f"kv_pos {st['kv_pos']}")
     assert r < (LOGIT_TOL16 if kv16 else LOGIT_TOL), r
-    assert prof["attn_wait_timeouts"] == 0

@@ -500,7 +500,6 @@ struct vox_hip_stream {
     // decoder
     float *xd, *xnd, *qkvd, *qd_, *attd, *gated, *part, *logits, *pval;
     float *part_alt, *alts;  // stream_fill_alts partials / per-step records [tokens_cap][ALT_REC]
-    float* attf;             // fused QKV + attention launch: key-block partials, then its counters (zeroed)
     float* gws;              // split-K GEMM partials (encoder / prefill / adapter)
     size_t gws_n;
     uint16_t* exp_;          // skinny encoder: row planes [4][3][16][max K] (fragment order)
@@ -624,7 +623,6 @@ extern "C" vox_hip_stream_t* vox_hip_stream_create(vox_hip_model_t* m) {
     // reset by the merging block after every launch)
     TRYH(dalloc(&s->part, (size_t)c.dec_heads * attn_maxch(c.dec_window) * (c.dec_head_dim + 2) + c.dec_kv_heads));
     TRYH(dalloc(&s->part_alt, (size_t)GEMV_MAX_BLOCKS * ALT_PART));
-    TRYH(dalloc(&s->attf, gemv_att_floats(c.dec_heads, c.dec_kv_heads, c.dec_head_dim)));
     s->gws_n = GEMM_WS_ELEMS;
     TRYH(dalloc(&s->gws, s->gws_n));
     TRYH(dalloc(&s->logits, (size_t)c.vocab));
@@ -681,7 +679,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
-    dfree(s->part_alt); dfree(s->attf); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch); dfree(s->abatch); dfree(s->abatch_out);
+    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch); dfree(s->abatch); dfree(s->abatch_out);
     dfree(s->gpa); dfree(s->gpc); dfree(s->gflags); dfree(s->dpa); dfree(s->dpc);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
@@ -1798,17 +1796,6 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
 // otherwise pos/rope_row are host values (boundary twin).
 static int enqueue_lm_head(vox_hip_stream_t* s, const int* state);
 
-// VOX_HIP_ATT_FUSE=0: the short-context decode attention as its own k_attn_short launch
-// instead of inside the QKV GEMV launch (EPI_QKV_ATT)
-static int g_att_fuse = -1;
-static bool att_fuse_env() {
-    if (g_att_fuse < 0) {
-        const char* e = getenv("VOX_HIP_ATT_FUSE");
-        g_att_fuse = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    return g_att_fuse == 1;
-}
-
 static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, const float* rope_row,
                                int splits) {
     vox_hip_model_t* m = s->m;
@@ -1817,8 +1804,6 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
     const int DQ = H * hd, DKV = KVH * hd, DH = c.dec_hidden;
     const float scale = 1.0f / sqrtf((float)hd);
     hipStream_t st = s->st;
-    // contexts <= 256 keys: the attention runs inside the QKV launch
-    const bool fuse = att_fuse_env() && gemv_att_ok(hd, H, KVH, c.dec_window, s->dcap, splits);
     for (int l = 0; l < c.dec_layers; l++) {
         const DecLayerD& L = m->dec[l];
         float* Kc = dec_ring(s, s->dk, l);
@@ -1832,15 +1817,10 @@ static int enqueue_step_layers(vox_hip_stream_t* s, const int* state, int pos, c
         a.state = state; a.pos = pos;
         a.rope = state ? m->rope_dec : rope_row - (size_t)pos * hd;
         a.Kc = Kc; a.Vc = Vc; a.cap = s->dcap; a.kv16 = s->kv16;
+        CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
         // attention over the last min(pos+1, window) keys (decoder.c:724-733)
-        if (fuse) {
-            a.att_heads = H; a.att_scale = scale; a.att_buf = s->attf; a.att_out = s->attd;
-            CK(launch_gemv(PRO_NORM, EPI_QKV_ATT, a, st));
-        } else {
-            CK(launch_gemv(PRO_NORM, EPI_QKV, a, st));
-            CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
-                                  s->part, s->attd, splits, st, s->kv16));
-        }
+        CK(launch_attn_decode(hd, s->qd_, Kc, Vc, s->dcap, state, pos, c.dec_window, scale, H, KVH,
+                              s->part, s->attd, splits, st, s->kv16));
         // wo + residual (decoder.c:735-740)
         memset(&a, 0, sizeof a);
         a.x = s->attd; a.K = DQ; a.W = L.wo; a.wscale = L.so; a.rows = DD; a.y = s->xd;
@@ -2156,15 +2136,7 @@ extern "C" int vox_hip_stream_profile(vox_hip_stream_t* s, double* out8) {
         CK(hipStreamSynchronize(s->st));
     }
     out8[6] = rec;
-    // fused QKV + attention launches whose attention blocks stopped waiting (must stay 0)
-    int to = 0;
-    if (s->attf) {
-        const vox_hip_config_t& c = s->m->c;
-        const size_t off = gemv_att_floats(c.dec_heads, c.dec_kv_heads, c.dec_head_dim) - 1;
-        CK(hipMemcpyAsync(&to, s->attf + off, sizeof to, hipMemcpyDeviceToHost, s->st));
-        CK(hipStreamSynchronize(s->st));
-    }
-    out8[7] = to;
+    out8[7] = 0.0;
     return 0;
 }
 

@@ -8,8 +8,7 @@ namespace vox {
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_GELU = 2, EPI_GELU_ERF = 3, EPI_SWIGLU = 4, EPI_QKV = 5, EPI_LOGITS = 6,
        EPI_LOGITS_ALT = 7,
        EPI_PARTIAL = 8,      // split-K GEMM slice: raw f32 tile into a workspace, epilogue in k_splitk_reduce
-       EPI_QKV_BIAS = 9,     // EPI_QKV with the projection's bias added before RoPE (the encoder's)
-       EPI_QKV_ATT = 10 };   // EPI_QKV plus the short-context decode attention in the same launch
+       EPI_QKV_BIAS = 9 };   // EPI_QKV with the projection's bias added before RoPE (the encoder's)
 constexpr int ALT_TEXT_MIN = 1000;   // TOKEN_TEXT_MIN (voxtral.c:399)
 constexpr int ALT_PART = 10;         // per-block alt partial: m, s, 4 values, 4 ids
 constexpr int ALT_REC = 8;           // per-step alt record: p_best, (id, p) x 3, pad
@@ -37,18 +36,6 @@ struct GemvArgs {
     float* Vc;
     int cap;
     int kv16 = 0;
-    // EPI_QKV_ATT: blocks past gemv_blocks run the attention of one (head, 64-key block) each
-    // once the kv group's q / k / v rows have arrived (att_expect row groups); att_buf holds
-    // the key-block partials [H][4][hd + 2] and then the counters (gemv_att_ints(), zero
-    // between launches: the last user of each resets it)
-    int gemv_blocks;
-    int att_expect;        // row groups per (kv group, XCD slot of the producing block)
-    int att_poll;          // s_sleep(1) rounds between two polls of the arrival counts
-    int att_diag;          // diagnostics only (wrong results): 1 = no wait, 2 = no wait and no counting
-    int att_heads;
-    float att_scale;
-    float* att_buf;
-    float* att_out;
     // EPI_LOGITS(_ALT)
     float* part_val;
     int* part_idx;
@@ -127,11 +114,6 @@ hipError_t launch_attn_rows_mf(int hd, const float* Q, int ldq, const float* Kc,
 hipError_t launch_slabs_rope_kv(const float* part, int S, int M, const float* bias, int qd, int kvd, int hd,
                                 const float* rope, int pos0, float* q, float* Kc, float* Vc, int cap, hipStream_t st);
 hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st);
-// EPI_QKV_ATT: whether the fused launch serves a step (head_dim 128, contexts <= 256 keys with
-// a window past them, 4 key blocks of every kv head spread evenly over the 8 XCDs), and the
-// size of its att_buf in floats
-bool gemv_att_ok(int hd, int H, int KVH, int window, int cap, int splits);
-size_t gemv_att_floats(int H, int KVH, int hd);
 const void* gemv_kernel(int pro, int epi, const GemvArgs& a);
 hipError_t launch_gemv_timed(int pro, int epi, const GemvArgs& a, hipEvent_t start, hipEvent_t stop,
                              hipStream_t st);

@@ -764,233 +764,17 @@ __device__ unsigned long long* g_gemv_stamps;
 #define GEMV_STAMP(k) do {} while (0)
 #endif
 
-// ============================================================================
-// EPI_QKV_ATT: the short-context decode attention (k_attn_short's arithmetic) inside the QKV
-// GEMV launch.  The GEMV blocks publish each row group's q / k / v write-through (sc1) and
-// count it on its kv group; blocks gemv_blocks.. each own one (query head, 64-key block).
-// An attention block loads the keys it covers that earlier steps wrote (plain loads: written
-// by earlier kernels) while the GEMV runs, waits for its kv group's row groups, reads q and
-// the new key / value (sc1), and merges its 4 waves' 16-key partials; with more than one
-// 64-key block the last of a head's blocks merges their partials (a ticket per head).  The
-// k_attn_short launch and its ramp leave the layer, and its K / V loads overlap the GEMV.
-// The 4 query heads of a (kv head, key block) sit on one XCD (same K / V rows through one
-// L2).  Counters in att_buf after the partials: [0, KVH) row groups arrived per kv group,
-// [KVH, 2 KVH) attention blocks past the wait (the last resets both), [2 KVH, 2 KVH + H) the
-// per-head merge tickets, then a count of waits that timed out (must stay 0).  The wait is
-// bounded: the attention blocks come after every GEMV block in the grid, and the GEMV blocks
-// never wait.
-// ============================================================================
-constexpr int QA_NKB = 4;                       // 64-key blocks per head (256 keys)
-constexpr unsigned long long QA_WAIT_TICKS = 100ull * 1000 * 1000;  // 1 s of s_memrealtime (100 MHz)
-
-template <class KT>
-__device__ __forceinline__ void qkv_att_block(const GemvArgs& a, int ab) {
-    constexpr int HD = 128, DQ = HD / 4, DPL = HD / 64, CH = 16;  // CH keys per wave
-    __shared__ float sM[4], sL[4];
-    __shared__ __attribute__((aligned(16))) float sO[4][HD];
-    __shared__ int sLast;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int H = a.att_heads, KVH = a.kvd / HD, hpk = H / KVH;
-    // block ab -> (kv head, key block) combo c on XCD slot x = ab % 8, query head hi of its group
-    const int x = ab & 7, j = ab >> 3, c = (j / hpk) * 8 + x, hi = j % hpk;
-    const int kvh = c / QA_NKB, kb = c % QA_NKB, h = kvh * hpk + hi;
-    const int lp = a.state ? a.state[0] : a.pos;
-    if (kb * 64 > lp) return;  // no key of this block in the context (nothing to count)
-    const int nkb = lp / 64 + 1;
-    const int kvd = a.kvd, k0 = kb * 64 + wave * CH;
-    const int r = lane >> 3, cq = lane & 7;
-    const KT* __restrict__ Kc = reinterpret_cast<const KT*>(a.Kc);
-    const KT* __restrict__ Vc = reinterpret_cast<const KT*>(a.Vc);
-    // this wave's 16 key slots, speculatively (slot lp is rewritten by this launch: reloaded
-    // below; slots past lp are masked)
-    float4 kv[DQ / 4];
-    float2 vv[CH];
-    const bool any = k0 <= lp;  // wave-uniform
-    if (any) {
-#pragma unroll
-        for (int i = 0; i < DQ / 4; i++)
-            kv[i] = kv_ld4(Kc + (size_t)(k0 + r + 8 * (i & 1)) * kvd + kvh * HD + (i >> 1) * DQ + cq * 4);
-#pragma unroll
-        for (int k = 0; k < CH; k++) vv[k] = kv_ld2(Vc + (size_t)(k0 + k) * kvd + kvh * HD + lane * DPL);
-    } else {
-#pragma unroll
-        for (int i = 0; i < DQ / 4; i++) kv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int k = 0; k < CH; k++) vv[k] = make_float2(0.f, 0.f);
-    }
-    // arrival counts per (kv group, XCD slot of the producing GEMV block): 8 addresses of
-    // att_expect each, polled together by 8 lanes of wave 0
-    int* cnt = reinterpret_cast<int*>(a.att_buf + (size_t)H * QA_NKB * (HD + 2));
-    int* pass = cnt + 8 * KVH;
-    if (wave == 0 && a.att_diag == 0) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        bool ok = lane >= 8;
-        for (;;) {
-            if (!ok) ok = __hip_atomic_load(cnt + kvh * 8 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.att_expect;
-            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > QA_WAIT_TICKS) {
-                if (lane == 0) __hip_atomic_fetch_add(pass + KVH + H, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            for (int k = 0; k < a.att_poll; k++) __builtin_amdgcn_s_sleep(1);
-        }
-        if (lane == 0 && __hip_atomic_fetch_add(pass + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hpk * nkb - 1) {
-            for (int k = 0; k < 8; k++) __hip_atomic_store(cnt + kvh * 8 + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(pass + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    // q and the new key / value: written this launch on other CUs (write-through), read sc1
-    const __amdgpu_buffer_rsrc_t Qr = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, H * HD * 4, 0x00020000);
-    float4 qv[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; jj++)
-        qv[jj] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(Qr, (h * HD + jj * DQ + cq * 4) * 4, 0, 16));
-    if (any && lp < k0 + CH) {
-        const int rr = lp - k0;
-        constexpr int ES = (int)sizeof(KT);
-        const __amdgpu_buffer_rsrc_t Kr = __builtin_amdgcn_make_buffer_rsrc(a.Kc, 0, 0x7fffffff, 0x00020000);
-        const __amdgpu_buffer_rsrc_t Vr = __builtin_amdgcn_make_buffer_rsrc(a.Vc, 0, 0x7fffffff, 0x00020000);
-        const int krow = (lp * kvd + kvh * HD) * ES;
-        if (r == (rr & 7)) {
-#pragma unroll
-            for (int i = 0; i < DQ / 4; i++)
-                if ((i & 1) == (rr >> 3)) {
-                    const int off = krow + ((i >> 1) * DQ + cq * 4) * ES;
-                    if constexpr (ES == 4) {
-                        kv[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(Kr, off, 0, 16));
-                    } else {
-                        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(Kr, off, 0, 16);
-                        const h16x4 hv = __builtin_bit_cast(h16x4, t);
-                        kv[i] = make_float4((float)hv[0], (float)hv[1], (float)hv[2], (float)hv[3]);
-                    }
-                }
-        }
-        float2 nv;
-        if constexpr (ES == 4) {
-            const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(Vr, krow + lane * DPL * ES, 0, 16);
-            nv = make_float2(__uint_as_float(t.x), __uint_as_float(t.y));
-        } else {
-            const h16x2 hv = __builtin_bit_cast(h16x2, __builtin_amdgcn_raw_buffer_load_b32(Vr, krow + lane * DPL * ES, 0, 16));
-            nv = make_float2((float)hv[0], (float)hv[1]);
-        }
-#pragma unroll
-        for (int k = 0; k < CH; k++)
-            if (k == rr) vv[k] = nv;
-    }
-    const float scale = a.att_scale;
-    const int kn = min(CH, lp + 1 - k0);  // keys of this wave inside the context (<= 0: none)
-    float aa = 0.f, ab2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < DQ / 4; i++) {
-        const float4 qq = qv[i >> 1];
-        float& acc = (i & 1) ? ab2 : aa;
-        acc = fmaf(qq.x, kv[i].x, acc);
-        acc = fmaf(qq.y, kv[i].y, acc);
-        acc = fmaf(qq.z, kv[i].z, acc);
-        acc = fmaf(qq.w, kv[i].w, acc);
-    }
-    aa += dpp<0xB1>(aa); aa += dpp<0x4E>(aa); aa += dpp<0x141>(aa);
-    ab2 += dpp<0xB1>(ab2); ab2 += dpp<0x4E>(ab2); ab2 += dpp<0x141>(ab2);
-    const float sa = (r < kn) ? aa * scale : -INFINITY, sbv = (r + 8 < kn) ? ab2 * scale : -INFINITY;
-    float mx = fmaxf(sa, sbv);
-    mx = fmaxf(mx, dpp<0x140>(mx));
-    mx = rows4_max(mx);
-    const float m = (kn > 0) ? mx : -1e30f;
-    const float p = (r < kn) ? expf(sa - mx) : 0.f, pb = (r + 8 < kn) ? expf(sbv - mx) : 0.f;
-    float t = p + pb;
-    t += dpp<0x140>(t);
-    t = rows4_sum(t);
-    float o0 = 0.f, o1 = 0.f;
-#pragma unroll
-    for (int k = 0; k < CH; k++) {
-        const float pv = k >= 8 ? pb : p;
-        const float pk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), 8 * (k & 7)));
-        const float2 v = k < kn ? vv[k] : make_float2(0.f, 0.f);
-        o0 = fmaf(pk, v.x, o0);
-        o1 = fmaf(pk, v.y, o1);
-    }
-    if (lane == 0) {
-        sM[wave] = m;
-        sL[wave] = kn > 0 ? t : 0.f;
-    }
-    *reinterpret_cast<float2*>(&sO[wave][lane * DPL]) = make_float2(o0, o1);
-    __syncthreads();
-    float* part = a.att_buf;
-    const __amdgpu_buffer_rsrc_t Pr = __builtin_amdgcn_make_buffer_rsrc(part, 0, H * QA_NKB * (HD + 2) * 4, 0x00020000);
-    if (tid < HD) {
-        float M = -1e30f;
-#pragma unroll
-        for (int w = 0; w < 4; w++) M = fmaxf(M, sM[w]);
-        float den = 0.f, num = 0.f;
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const float f = expf(sM[w] - M);
-            den = fmaf(f, sL[w], den);
-            num = fmaf(f, sO[w][tid], num);
-        }
-        if (nkb == 1) {
-            a.att_out[(size_t)h * HD + tid] = den > 0.f ? num * (1.0f / den) : 0.f;
-        } else {
-            const int po = ((h * QA_NKB + kb) * (HD + 2)) * 4;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(num), Pr, po + tid * 4, 0, 16);
-            if (tid == 0) {
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(M), Pr, po + HD * 4, 0, 16);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(den), Pr, po + (HD + 1) * 4, 0, 16);
-            }
-        }
-    }
-    if (nkb == 1) return;
-    // the last of the head's nkb blocks merges the partials (in key-block order)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) sLast = __hip_atomic_fetch_add(pass + KVH + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nkb - 1;
-    __syncthreads();
-    if (!sLast) return;
-    if (tid == 0) __hip_atomic_store(pass + KVH + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid < HD) {
-        float pm[QA_NKB], pl[QA_NKB], pn[QA_NKB];
-#pragma unroll
-        for (int k = 0; k < QA_NKB; k++) {
-            const int po = ((h * QA_NKB + min(k, nkb - 1)) * (HD + 2)) * 4;
-            pn[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(Pr, po + tid * 4, 0, 16));
-            pm[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(Pr, po + HD * 4, 0, 16));
-            pl[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(Pr, po + (HD + 1) * 4, 0, 16));
-        }
-        float M = -1e30f;
-#pragma unroll
-        for (int k = 0; k < QA_NKB; k++)
-            if (k < nkb) M = fmaxf(M, pm[k]);
-        float den = 0.f, num = 0.f;
-#pragma unroll
-        for (int k = 0; k < QA_NKB; k++)
-            if (k < nkb) {
-                const float f = expf(pm[k] - M);
-                den = fmaf(f, pl[k], den);
-                num = fmaf(f, pn[k], num);
-            }
-        a.att_out[(size_t)h * HD + tid] = den > 0.f ? num * (1.0f / den) : 0.f;
-    }
-}
-
 template <int PRO, int EPI, int RB, int KQ, int WQ8>
 __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
     constexpr int XPC = WQ8 ? 4 : 2;  // float4 of x per 16-B chunk
     __shared__ float red[2][4][RB];
     __shared__ float sred[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if constexpr (EPI == EPI_QKV_ATT) {
-        if ((int)blockIdx.x >= a.gemv_blocks) {
-            if (a.kv16) qkv_att_block<kvh_t>(a, (int)blockIdx.x - a.gemv_blocks);
-            else qkv_att_block<float>(a, (int)blockIdx.x - a.gemv_blocks);
-            return;
-        }
-    }
     const int K = a.K, KC = WQ8 ? K >> 4 : K >> 3;
     const int ngroups = a.rows / RB;
     // Groups: block b takes b, b + G, b + 2G, ... (static; run-time claims measured 3-4x
     // slower)
-    const int G = EPI == EPI_QKV_ATT ? a.gemv_blocks : (int)gridDim.x;
+    const int G = gridDim.x;
     int g = blockIdx.x;
     int rows[RB];
     uint4 wv[KQ][RB];
@@ -1084,7 +868,7 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
         }
     }
 
-    constexpr bool QKVE = (EPI == EPI_QKV || EPI == EPI_QKV_BIAS || EPI == EPI_QKV_ATT);
+    constexpr bool QKVE = (EPI == EPI_QKV || EPI == EPI_QKV_BIAS);
     int lp = 0;
     if (QKVE) lp = a.state ? a.state[0] : a.pos;
     float best = -INFINITY;
@@ -1193,19 +977,6 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 a.y[er0] = ein0 + v0;  // RESID: residual + bias were read at the top
             } else if (EPI == EPI_SWIGLU) {
                 a.y[gcur * (RB / 2) + lane] = silu(v0) * v1;
-            } else if (EPI == EPI_QKV_ATT) {
-                // write-through (sc1): the attention blocks read them in this launch
-                const float o0 = v0 * ein0 - v1 * ein1, o1 = v0 * ein1 + v1 * ein0;
-                const bool isq = er0 < a.qd, isk = !isq && er0 < a.qd + a.kvd;
-                float* base = isq ? a.y : isk ? a.Kc : a.Vc;
-                const int e = isq ? er0 : (lp % a.cap) * a.kvd + (er0 - a.qd - (isk ? 0 : a.kvd));
-                const float w0 = isq || isk ? o0 : v0, w1 = isq || isk ? o1 : v1;
-                const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-                if (isq || !a.kv16) {
-                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(w0), __float_as_uint(w1)}, R, e * 4, 0, 16);
-                } else {
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, h16x2{(kvh_t)w0, (kvh_t)w1}), R, e * 2, 0, 16);
-                }
             } else if (QKVE) {
                 if (er0 < a.qd + a.kvd) {
                     const float o0 = v0 * ein0 - v1 * ein1, o1 = v0 * ein1 + v1 * ein0;
@@ -1218,16 +989,6 @@ __global__ __launch_bounds__(256) void k_gemv(GemvArgs a) {
                 } else {
                     kv_st2_rt(a.Vc, (size_t)(lp % a.cap) * a.kvd + (er0 - a.qd - a.kvd), v0, v1, a.kv16);
                 }
-            }
-        }
-        if (EPI == EPI_QKV_ATT && wave == 0 && a.att_diag < 2) {
-            // this row group has landed: count it on its (kv group, XCD slot) (stores retired first)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) {
-                const int row = gcur * RB, hpkd = a.qd / (a.kvd / a.hd);
-                const int kvg = row < a.qd ? row / hpkd : row < a.qd + a.kvd ? (row - a.qd) / a.hd : (row - a.qd - a.kvd) / a.hd;
-                int* cnt = reinterpret_cast<int*>(a.att_buf + (size_t)a.att_heads * QA_NKB * (a.hd + 2));
-                __hip_atomic_fetch_add(cnt + kvg * 8 + (blockIdx.x & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         if (LOGIT && wave == 0 && lane == 0) {
@@ -3473,7 +3234,7 @@ const void* gemv_kernel(int pro, int epi, const GemvArgs& a) {
         return rb == 8 ? (a.wscale ? gemv_fn<P, E, 8, 1>(kq) : gemv_fn<P, E, 8, 0>(kq))   \
              : rb == 2 ? (a.wscale ? gemv_fn<P, E, 2, 1>(kq) : gemv_fn<P, E, 2, 0>(kq))   \
                        : (a.wscale ? gemv_fn<P, E, 4, 1>(kq) : gemv_fn<P, E, 4, 0>(kq));
-    GEMV_FN(PRO_NONE, EPI_STORE) GEMV_FN(PRO_NONE, EPI_RESID) GEMV_FN(PRO_NORM, EPI_QKV) GEMV_FN(PRO_NORM, EPI_QKV_ATT)
+    GEMV_FN(PRO_NONE, EPI_STORE) GEMV_FN(PRO_NONE, EPI_RESID) GEMV_FN(PRO_NORM, EPI_QKV)
     GEMV_FN(PRO_NORM_ADA, EPI_SWIGLU) GEMV_FN(PRO_NORM, EPI_LOGITS) GEMV_FN(PRO_NORM, EPI_LOGITS_ALT)
     GEMV_FN(PRO_NORM, EPI_QKV_BIAS) GEMV_FN(PRO_NORM, EPI_SWIGLU)
 #undef GEMV_FN
@@ -3504,51 +3265,15 @@ bool gemv_ok(int rows, int K, int q8) {
     return rows > 0 && K > 0 && K % (q8 ? 16 : 8) == 0 && rows % gemv_rb(rows) == 0 && (kc + 255) / 256 <= 5;
 }
 
-bool gemv_att_ok(int hd, int H, int KVH, int window, int cap, int splits) {
-    // the contexts k_attn_short serves (launch_attn_decode), 4 x 64-key blocks per head, the
-    // (kv head, key block) combos a multiple of the 8 XCDs
-    return splits == 1 && hd == 128 && KVH > 0 && H % KVH == 0 && window > 256 && cap >= 256 &&
-           (KVH * QA_NKB) % 8 == 0;
-}
-// partials, then 8 arrival counts per kv group, the pass counts, the per-head merge tickets
-// and the timeout count
-size_t gemv_att_floats(int H, int KVH, int hd) { return (size_t)H * QA_NKB * (hd + 2) + 9 * KVH + H + 1; }
-static int g_att_poll = -1, g_att_diag = -1;
-
-hipError_t launch_gemv(int pro, int epi, const GemvArgs& a0, hipStream_t st) {
-    const int rb = gemv_rb(a0.rows);
-    if (!gemv_ok(a0.rows, a0.K, a0.wscale != nullptr)) return hipErrorInvalidValue;
-    if (epi == EPI_QKV_BIAS && !a0.bias) return hipErrorInvalidValue;
-    int grid = gemv_grid(a0.rows);
-    GemvArgs a = a0;
-    if (epi == EPI_QKV_ATT) {
-        // GEMV blocks, then one block per (query head, 64-key block); a row group inside one
-        // head, and the kv group's row groups counted against att_expect
-        const int KVH = a.hd ? a.kvd / a.hd : 0;
-        if (pro != PRO_NORM || !a.att_buf || !a.att_out || a.hd != 128 || KVH <= 0 || a.qd % a.hd ||
-            a.att_heads * a.hd != a.qd || a.att_heads % KVH || a.rows != a.qd + 2 * a.kvd || a.hd % rb ||
-            (KVH * QA_NKB) % 8 || a.cap < 256)
-            return hipErrorInvalidValue;
-        // every XCD slot produces the same number of a kv group's row groups: the grid and the
-        // q / k / v row-group ranges of a kv group multiples of 8
-        if (grid % 8 || (a.qd / KVH / rb) % 8 || (a.hd / rb) % 8) return hipErrorInvalidValue;
-        if (g_att_poll < 0) {
-            const char* e = getenv("VOX_HIP_ATT_POLL");
-            g_att_poll = e ? std::max(0, atoi(e)) : 1;
-            e = getenv("VOX_HIP_ATT_DIAG");
-            g_att_diag = e ? atoi(e) : 0;
-        }
-        a.gemv_blocks = grid;
-        a.att_expect = (a.qd / KVH + 2 * a.hd) / rb / 8;
-        a.att_poll = g_att_poll;
-        a.att_diag = g_att_diag;
-        grid += a.att_heads * QA_NKB;
-    }
+hipError_t launch_gemv(int pro, int epi, const GemvArgs& a, hipStream_t st) {
+    const int rb = gemv_rb(a.rows);
+    if (!gemv_ok(a.rows, a.K, a.wscale != nullptr)) return hipErrorInvalidValue;
+    if (epi == EPI_QKV_BIAS && !a.bias) return hipErrorInvalidValue;
+    const int grid = gemv_grid(a.rows);
 #define GEMV_CASE(P, E) \
     if (pro == P && epi == E)                                                            \
         return rb == 8 ? gemv_q<P, E, 8>(a, grid, st) : rb == 2 ? gemv_q<P, E, 2>(a, grid, st) : gemv_q<P, E, 4>(a, grid, st);
     GEMV_CASE(PRO_NONE, EPI_STORE) GEMV_CASE(PRO_NONE, EPI_RESID) GEMV_CASE(PRO_NORM, EPI_QKV)
-    GEMV_CASE(PRO_NORM, EPI_QKV_ATT)
     GEMV_CASE(PRO_NORM_ADA, EPI_SWIGLU) GEMV_CASE(PRO_NORM, EPI_LOGITS) GEMV_CASE(PRO_NORM, EPI_LOGITS_ALT)
     // the encoder's single-row chunks (run_encoder_rows_gemv)
     GEMV_CASE(PRO_NORM, EPI_QKV_BIAS) GEMV_CASE(PRO_NORM, EPI_SWIGLU)

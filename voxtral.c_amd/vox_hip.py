@@ -345,7 +345,7 @@ class Stream:
         lib().vox_hip_stream_profile(self.h, o)
         # kind 0: the events bracket the W1|W3 GEMV of every layer
         return {"ms": o[0], "bytes": o[1], "launches": int(o[2]), "avg_ms": o[3], "kind": int(o[4]),
-                "bytes_per_launch": o[5], "gemmf_recomputes": int(o[6]), "attn_wait_timeouts": int(o[7])}
+                "bytes_per_launch": o[5], "gemmf_recomputes": int(o[6])}
 
     def sync(self):
         lib().vox_hip_stream_sync(self.h)

@@ -12,7 +12,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_dev.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_gemmf_pair, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -920,47 +920,6 @@ int main(int argc, char** argv) {
                 }
                 g_gemmf_order = 0;  // by shape
             }
-    }
-    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "pair")) {
-        // k_gemmf: a barrier per 64-deep stage on a 3-slot ring against one per pair of stages
-        // on a 4-slot ring (gf_stages_pair); outputs compared bit for bit (same summation order)
-        const size_t wsn = 2 * gemmf_ws_floats(gemmf_grid());
-        float* gws = (float*)dmalloc(wsn * 4, 0);
-        int* gfl = (int*)dmalloc(gemmf_flag_ints() * 4, 0);
-        uint16_t* gp = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 1);
-        uint16_t* go = (uint16_t*)dmalloc((size_t)64 * 3 * 16 * 9216 * 2, 0);
-        float* gc = (float*)dmalloc((size_t)1024 * 18432 * 4, 0);
-        std::vector<float> h0((size_t)1024 * 18432), h1((size_t)1024 * 18432);
-        int epoch = 0;
-        struct G { const char* n; int epi, N, K; const uint16_t* W; };
-        for (int M : {38, 70, 400, 677, 1024})
-            for (int np : {3, 2})
-                for (G g : {G{"qkv", EPI_STORE, 6144, 1280, wqkv[1]}, G{"w13", EPI_SWIGLU, 10240, 1280, w13[1]},
-                            G{"wo", EPI_RESID, 1280, 2048, wo[1]}, G{"w2", EPI_RESID, 1280, 5120, w2[1]},
-                            G{"dqkv", EPI_STORE, 6144, 3072, wqkv[3]}, G{"dw13", EPI_SWIGLU, 18432, 3072, w13[3]},
-                            G{"dwo", EPI_RESID, 3072, 4096, wo[3]}, G{"dw2", EPI_RESID, 3072, 9216, w2[3]}}) {
-                    if (np == 2 && M != 677) continue;
-                    if (g.n[0] == 'd' && M != 38 && M != 677) continue;
-                    if (g.n[0] != 'd' && M == 38) continue;
-                    const int ldc = g.epi == EPI_SWIGLU ? g.N / 2 : g.N;
-                    const size_t nc = (size_t)M * ldc;
-                    double t[2];
-                    for (int v = 0; v < 2; v++) {
-                        g_gemmf_pair = v;
-                        CK(hipMemsetAsync(gc, 0, nc * 4, st));
-                        CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, ldc, nullptr, gws, wsn, gfl, ++epoch, st));
-                        CK(hipStreamSynchronize(st));
-                        CK(hipMemcpy((v ? h1 : h0).data(), gc, nc * 4, hipMemcpyDeviceToHost));
-                        t[v] = timeit([&] { CK(launch_gemmf(g.epi, np, gp, g.K, M, g.W, g.N, nullptr, gc, ldc,
-                                                            g.epi == EPI_SWIGLU ? go : nullptr, gws, wsn, gfl, ++epoch, st)); }, 20, st);
-                    }
-                    const bool same = !memcmp(h0.data(), h1.data(), nc * 4);
-                    printf("pair %-4s M=%4d %5dx%-4d np%d  per stage %8.2f us  per pair %8.2f us  (%+5.1f %%)  %s\n", g.n, M, g.N, g.K, np,
-                           t[0], t[1], 100.0 * (t[1] - t[0]) / t[0], same ? "same bits" : "BITS DIFFER");
-                    fflush(stdout);
-                }
-        g_gemmf_pair = -1;
-        return 0;
     }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmfm")) {
         // k_gemmf at small M (streaming chunks, prefills, the one-shot flush chunk): least

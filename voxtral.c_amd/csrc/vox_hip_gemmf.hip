@@ -227,76 +227,6 @@ __device__ __forceinline__ void gf_stages(const GemmfArgs& a, uint16_t* lds, int
     __builtin_amdgcn_s_barrier();
 }
 
-// stages [s0, s1) with a 4-slot ring taken in PAIRS of stages (slots 0-1, 2-3): one barrier
-// and one wait per two 64-deep stages instead of one per stage (the stage barrier that all 8
-// waves meet paces the kernel).  Pair p's DMA lands during pair p - 1's
-// MFMAs; at the end of pair p every wave waits for pair p + 1's DMA (nothing else is in flight
-// then), meets the barrier, and issues pair p + 2 into pair p's slots.  The same fragments in
-// the same order as gf_stages: the same bits.
-template <int NP, int RB, int NG, int WR>
-__device__ __forceinline__ void gf_stages_pair(const GemmfArgs& a, uint16_t* lds, int mt, int nt, int s0, int s1,
-                                               f32x4 (&acc)[RB / WR][NG]) {
-    using C = GfCfg<NP, RB, NG, WR>;
-    constexpr int PER = C::NA + C::NB;
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int KB = a.K >> 6;
-    const size_t plane = (size_t)SK_ROWS * a.K;
-    const uint16_t* xb = a.xs + (size_t)(mt * RB) * 3 * plane;
-    const uint8_t* wt = a.W + (size_t)nt * 4 * NG * KB * 2048;
-    GfHalf<NP, RB, NG, WR> H0, H1;
-    gf_issue<NP, RB, NG, WR, 0>(xb, plane, wt, KB, s0, lds, wave, lane);
-    if (s0 + 1 < s1) gf_issue<NP, RB, NG, WR, 1>(xb, plane, wt, KB, s0 + 1, lds, wave, lane);
-    if (s0 + 2 < s1) gf_issue<NP, RB, NG, WR, 2>(xb, plane, wt, KB, s0 + 2, lds, wave, lane);
-    if (s0 + 3 < s1) gf_issue<NP, RB, NG, WR, 3>(xb, plane, wt, KB, s0 + 3, lds, wave, lane);
-    // the first pair landed (the second may stay in flight)
-    if (VOX_GF_DIAG != 2) {
-        const int k = min(2, s1 - s0 - 2);
-        if (k >= 2) wait_vm<2 * PER>();
-        else if (k == 1) wait_vm<PER>();
-        else wait_vm<0>();
-    }
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    gf_read<NP, RB, NG, WR, 0, 0>(lds, wave, lane, H0);
-    wait_lgkm0();
-#define GF_MM(H) \
-    __builtin_amdgcn_sched_barrier(0); \
-    gf_mma<NP, RB, NG, WR>(H, acc);    \
-    __builtin_amdgcn_sched_barrier(0); \
-    wait_lgkm0();
-#define GF_PAIR(J)                                                                                        \
-    if (s + J < s1) {                                                                                     \
-        gf_read<NP, RB, NG, WR, J, 1>(lds, wave, lane, H1);                                               \
-        GF_MM(H0)                                                                                         \
-        if (s + J + 1 < s1) {                                                                             \
-            gf_read<NP, RB, NG, WR, J + 1, 0>(lds, wave, lane, H0);                                       \
-            GF_MM(H1)                                                                                     \
-            gf_read<NP, RB, NG, WR, J + 1, 1>(lds, wave, lane, H1);                                       \
-            GF_MM(H0)                                                                                     \
-            if (s + J + 2 < s1) {                                                                         \
-                if (VOX_GF_DIAG != 2) wait_vm<0>();                                                       \
-                asm volatile("" ::: "memory");                                                            \
-                __builtin_amdgcn_s_barrier();                                                             \
-                asm volatile("" ::: "memory");                                                            \
-                if (s + J + 4 < s1) gf_issue<NP, RB, NG, WR, J>(xb, plane, wt, KB, s + J + 4, lds, wave, lane);          \
-                if (s + J + 5 < s1) gf_issue<NP, RB, NG, WR, J + 1>(xb, plane, wt, KB, s + J + 5, lds, wave, lane);      \
-                gf_read<NP, RB, NG, WR, (J + 2) % 4, 0>(lds, wave, lane, H0);                             \
-            }                                                                                             \
-            GF_MM(H1)                                                                                     \
-        } else {                                                                                          \
-            GF_MM(H1)                                                                                     \
-        }                                                                                                 \
-    }
-    for (int s = s0; s < s1; s += 4) {
-        GF_PAIR(0)
-        GF_PAIR(2)
-    }
-#undef GF_PAIR
-#undef GF_MM
-    __builtin_amdgcn_s_barrier();
-}
-
 __device__ __forceinline__ long long gf_bound(long long U, int G, int b) { return U * b / G; }
 
 // epilogue of one 16 x 16 output fragment of weight group gg for row m (lane & 15 of its row
@@ -347,14 +277,13 @@ __device__ __forceinline__ void gf_out(const GemmfArgs& a, int m, int gg, int la
     *cp = v;
 }
 
-template <int EPI, int NP, int RB, int NG, int WR, int PAIR>
+template <int EPI, int NP, int RB, int NG, int WR>
 __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
     using C = GfCfg<NP, RB, NG, WR>;
     constexpr int RBW = C::RBW;
     extern __shared__ __attribute__((aligned(16))) uint16_t gf_lds[];
-    // the owner's flag mask: the ring's first 8 bytes (the ring is idle between stage ranges:
-    // they end on a barrier, and the mask is read before the next range's DMA)
-    unsigned long long* s_okm = reinterpret_cast<unsigned long long*>(gf_lds);
+    // the owner's flag mask, one 8-byte word past the ring (the same array)
+    unsigned long long* s_okm = reinterpret_cast<unsigned long long*>(gf_lds + 3 * C::SLOT);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wc = wave & 3, r0 = (wave >> 2) * RBW;
     const int G = gridDim.x, b = blockIdx.x;
@@ -376,8 +305,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
         for (int i = 0; i < RBW; i++)
 #pragma unroll
             for (int g = 0; g < NG; g++) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (PAIR) gf_stages_pair<NP, RB, NG, WR>(a, gf_lds, mt, nt, s0, s1, acc);
-        else gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, s0, s1, acc);
+        gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, s0, s1, acc);
         u += s1 - s0;
         if (s0 > 0) {
             // a later part of tile t: publish it for the tile's owner (write-through stores,
@@ -436,8 +364,7 @@ __global__ __launch_bounds__(256 * WR, 1) void k_gemmf(const GemmfArgs a) {
                         for (int g = 0; g < NG; g++) part[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
                     const int q0 = (int)(gf_bound(a.U, G, pb) - (long long)t * a.S);
                     const int q1 = (int)(min(gf_bound(a.U, G, pb + 1), tend) - (long long)t * a.S);
-                    if constexpr (PAIR) gf_stages_pair<NP, RB, NG, WR>(a, gf_lds, mt, nt, q0, q1, part);
-                    else gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, q0, q1, part);
+                    gf_stages<NP, RB, NG, WR>(a, gf_lds, mt, nt, q0, q1, part);
                 }
 #pragma unroll
                 for (int i = 0; i < RBW; i++)
@@ -472,37 +399,19 @@ int g_gemmf_order = -1;  // 1 = column-tile-major unit order (a weight tile's ro
 // QKV / wo equal; M = 1024 W1|W3 54.5 -> 48.4 us.  Three planes keep 8 (24 chunks a stage).
 int g_gemmf_wr = -1;
 
-// stage pairs on a 4-slot ring (gf_stages_pair) where 4 slots fit the CU's 160 KiB, else the
-// 3-slot ring with a barrier per stage (VOX_HIP_GEMMF_PAIR=0 forces the latter)
-int g_gemmf_pair = -1;  // -1: read VOX_HIP_GEMMF_PAIR once
-template <int NP, int RB, int NG, int WR>
-constexpr bool gf_pair_fits() { return 4 * GfCfg<NP, RB, NG, WR>::SLOT * 2 <= 160 * 1024; }
-
-template <int EPI, int NP, int RB, int NG, int WR, int PAIR>
-static hipError_t gemmf_launch_p(const GemmfArgs& a, int G, hipStream_t st) {
+template <int EPI, int NP, int RB, int NG, int WR>
+static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
     using C = GfCfg<NP, RB, NG, WR>;
     static bool attr = false;
-    const size_t lds = (size_t)(PAIR ? 4 : 3) * C::SLOT * 2;
+    const size_t lds = (size_t)3 * C::SLOT * 2 + 16;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemmf<EPI, NP, RB, NG, WR, PAIR>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemmf<EPI, NP, RB, NG, WR>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL((k_gemmf<EPI, NP, RB, NG, WR, PAIR>), dim3(G), dim3(256 * WR), lds, st, a);
+    hipLaunchKernelGGL((k_gemmf<EPI, NP, RB, NG, WR>), dim3(G), dim3(256 * WR), lds, st, a);
     return hipGetLastError();
-}
-
-template <int EPI, int NP, int RB, int NG, int WR>
-static hipError_t gemmf_launch(const GemmfArgs& a, int G, hipStream_t st) {
-    if (g_gemmf_pair < 0) {
-        const char* e = getenv("VOX_HIP_GEMMF_PAIR");
-        g_gemmf_pair = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    if constexpr (gf_pair_fits<NP, RB, NG, WR>()) {
-        if (g_gemmf_pair) return gemmf_launch_p<EPI, NP, RB, NG, WR, 1>(a, G, st);
-    }
-    return gemmf_launch_p<EPI, NP, RB, NG, WR, 0>(a, G, st);
 }
 
 size_t gemmf_ws_floats(int blocks) { return (size_t)blocks * (8 * 2 * 4 * 256); }

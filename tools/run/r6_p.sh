@@ -1,0 +1,21 @@
+# Round 6 call P: the scheduler run returns without waiting for its encoder pass (step cap
+# set; the next run syncs the streams before counting rows) vs the tail sync of rounds 4-5
+# (VOX_HIP_SCHED_TAIL_SYNC=1): scheduler + batch suites, then served 16 / 32 streams alternated
+export TMPDIR=/tmp
+O=gpurun_out/r6p; mkdir -p $O
+timeout -k 10 700 python -u -m pytest -m gpu -x -v --timeout 600 --timeout-method thread tests/test_gpu_sched.py tests/test_host_c.py > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+grep -E "passed|failed" $O/test.log | tail -3
+b() { n=$1; shift; timeout -k 10 400 python -u bench.py "$@" > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; exit 1; }; }
+for i in 1 2; do
+  VOX_HIP_SCHED_TAIL_SYNC=1 b s16_sync_$i --stagger --streams 16 --no-cpu-baseline
+  b s16_nosync_$i --stagger --streams 16 --no-cpu-baseline
+done
+VOX_HIP_SCHED_TAIL_SYNC=1 b s32_sync --stagger --streams 32 --no-cpu-baseline
+b s32_nosync --stagger --streams 32 --no-cpu-baseline
+VOX_HIP_SCHED_TAIL_SYNC=1 b s8_sync --stagger --streams 8 --no-cpu-baseline
+b s8_nosync --stagger --streams 8 --no-cpu-baseline
+for f in $O/s*.json; do python3 -c "import json; d=json.load(open('$f')); bd=d['batched_decode']; print('$f', d['value'], round(bd['ms']/bd['steps'],3), bd['rows_per_step'], d['tick_latency_ms'])"; done
+export VOX_HIP_GRAPH=0
+timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/trn -o run --output-format csv -- python3 bench.py --stagger --streams 16 --steps 1 --warmup 0 --serve-seconds 20 --no-cpu-baseline > $O/trn.log 2>&1 || { tail -20 $O/trn.log; exit 1; }
+python3 tools/serve_timeline.py $(find /tmp/trn -name "*kernel_trace.csv" | head -1) > $O/timeline.txt 2>&1; head -12 $O/timeline.txt; grep -A12 "idle gaps" $O/timeline.txt
+echo rc=0

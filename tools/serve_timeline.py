@@ -147,11 +147,46 @@ def main():
             shown += 1
             if shown >= 2:
                 break
+    top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 8
     for c in ("step", "prefill", "encoder"):
         tot = sum(per[c].values())
         print(f"  {c}: top kernels")
-        for n, t in per[c].most_common(8):
+        for n, t in per[c].most_common(top):
             print(f"     {t / 1e6:8.2f} ms {100 * t / max(1, tot):5.1f} %  {n}")
+    # idle gaps: the device runs nothing between the last kernel to end and the next to start;
+    # each gap is attributed to (class of the kernel that ended last -> class of the next one)
+    # and to the next kernel's name (what the host submitted after the gap)
+    labelled = []
+    in_prefill = False
+    for a, b, q, n in rows:
+        if q == batch_q:
+            if n.startswith("k_embed_rows"):
+                in_prefill = True
+            elif n.startswith(STEP_NAMES):
+                in_prefill = False
+            c = "prefill" if in_prefill else "step"
+        else:
+            c = "encoder"
+        labelled.append((a, b, c, n))
+    gaps = collections.Counter()
+    gapn = collections.Counter()
+    sizes = collections.Counter()
+    end, endc = labelled[0][1], labelled[0][2]
+    for a, b, c, n in labelled[1:]:
+        if a > end:
+            g = a - end
+            gaps[(endc, c)] += g
+            gapn[n] += g
+            sizes["< 10 us" if g < 1e4 else "10-100 us" if g < 1e5 else "0.1-1 ms" if g < 1e6 else ">= 1 ms"] += g
+        if b > end:
+            end, endc = b, c
+    tot = sum(gaps.values())
+    print(f"  idle gaps: {tot / 1e6:.1f} ms; by size: " + ", ".join(f"{k} {v / 1e6:.1f} ms" for k, v in sizes.most_common()))
+    for (x, y), g in gaps.most_common():
+        print(f"     {x:8s} -> {y:8s} {g / 1e6:8.1f} ms ({100 * g / max(1, tot):5.1f} %)")
+    print("  idle before (next kernel):")
+    for n, g in gapn.most_common(8):
+        print(f"     {g / 1e6:8.1f} ms  {n[:70]}")
 
 
 if __name__ == "__main__":

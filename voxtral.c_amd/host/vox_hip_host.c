@@ -1073,6 +1073,11 @@ static int sched_overlap(void) {
     return !(e && atoi(e) == 0);
 }
 
+static int sched_tail_sync(void) {
+    const char *e = getenv("VOX_HIP_SCHED_TAIL_SYNC");
+    return e && atoi(e) == 1;
+}
+
 static int sched_encode(vh_sched_t *q, int overlap);
 
 /* the batched steps of one run: every stream whose decoder can run (ran[i]) goes into one
@@ -1197,10 +1202,16 @@ int vh_sched_run(vh_sched_t *q) {
         }
     if (sched_steps(q, overlap, rows, ran, eos, &total, !enc_done, &enc_done)) return -1;
     if (!enc_done && sched_encode(q, overlap)) return -1;  /* no steps ran this time */
-    /* 3 (overlap). the pass beside the steps completes before the run returns */
+    /* 3 (overlap). without a step cap the pass completes before the run returns (its rows are
+     *    drained below); with one, the run returns while the pass may still be running: the
+     *    caller's feeds and resets queue behind it on the streams' queues, and the next run
+     *    syncs every stream before it counts rows (above), so the host work between runs
+     *    overlaps the pass instead of leaving the device idle (VOX_HIP_SCHED_TAIL_SYNC=1: wait
+     *    here as before round 6) */
     if (overlap) {
-        for (int i = 0; i < q->n; i++)
-            if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
+        if (q->step_cap <= 0 || sched_tail_sync())
+            for (int i = 0; i < q->n; i++)
+                if (vox_hip_stream_sync(q->s[i]->st)) return fail("encoder: %s", vox_hip_last_error());
         /* without a step cap a run drains every stream (vh_sched_set_step_cap): the rows this
          * run's pass produced are decoded now, after the pass, instead of by the next run */
         if (q->step_cap <= 0) {

@@ -12,7 +12,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_dev.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_mel_fpb, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -288,6 +288,31 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     const bool only_gemmf = getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gemmf");
+    if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "mel")) {
+        // k_mel_frames: frames per block 1 / 2 / 4 / 8 at a 0.5 s feed (50 frames) and a 30 s
+        // clip (3000), outputs compared bit for bit with one frame per block
+        const int NS = 500000;
+        float* smp = (float*)dmalloc((size_t)NS * 4, 1);
+        float* win = (float*)dmalloc(400 * 4, 1);
+        float* dc = (float*)dmalloc(400 * 201 * 4, 1);
+        float* ds = (float*)dmalloc(400 * 201 * 4, 1);
+        float* ft = (float*)dmalloc(201 * 128 * 4, 1);
+        float* mo = (float*)dmalloc((size_t)3000 * 128 * 4, 0);
+        std::vector<float> r1((size_t)3000 * 128), rx((size_t)3000 * 128);
+        for (int nf : {50, 3000})
+            for (int F : {1, 2, 4, 8}) {
+                g_mel_fpb = F;
+                CK(launch_mel_frames(smp, 0, nf, win, dc, ds, ft, -8.0f, mo, st));
+                CK(hipStreamSynchronize(st));
+                CK(hipMemcpy((F == 1 ? r1 : rx).data(), mo, (size_t)nf * 128 * 4, hipMemcpyDeviceToHost));
+                const bool same = F == 1 || !memcmp(r1.data(), rx.data(), (size_t)nf * 128 * 4);
+                const double us = timeit([&] { CK(launch_mel_frames(smp, 0, nf, win, dc, ds, ft, -8.0f, mo, st)); }, 50, st);
+                printf("mel frames %5d  %d per block  %8.2f us  %s\n", nf, F, us, same ? "same bits" : "BITS DIFFER");
+                fflush(stdout);
+            }
+        g_mel_fpb = 0;
+        return 0;
+    }
     if (getenv("VOX_KB_ONLY") && !strcmp(getenv("VOX_KB_ONLY"), "gpe")) {
         // where the fused prologue / epilogue cost of the W1|W3 and QKV GEMVs sits: each
         // prologue x epilogue combination of the same weights, bf16 and Q8

@@ -2892,7 +2892,12 @@ __global__ void k_mel_tail(const float* __restrict__ melp, int n_new, int MB, fl
 // ============================================================================
 constexpr int MELK_FFT = 400, MELK_FREQ = 201, MELK_HOP = 160, MELK_BINS = 128;
 
-__global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ samples, long long start0,
+// F frames per block: every table element a thread loads serves F frames (the tables are
+// 2 x 321 KB, read from L2 by every block: one frame per block spent most of its time on
+// them); each frame's products and sums are the same operations in the same order as with
+// one frame per block, so the bits do not depend on F
+template <int F>
+__global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ samples, long long start0, int nframes,
                                                     const float* __restrict__ window,
                                                     const float* __restrict__ dcosT,
                                                     const float* __restrict__ dsinT,
@@ -2901,29 +2906,50 @@ __global__ __launch_bounds__(256) void k_mel_frames(const float* __restrict__ sa
     // hipcc contracts a * b + c into an FMA by default; the reference rounds the product
     // first, which moves low-power bins by up to 1e-4 relative
 #pragma clang fp contract(off)
-    __shared__ float win[MELK_FFT];
-    __shared__ float pw[MELK_FREQ];
+    __shared__ float win[F][MELK_FFT];
+    __shared__ float pw[F][MELK_FREQ];
     const int tid = threadIdx.x;
-    const float* sp = samples + start0 + (long long)blockIdx.x * MELK_HOP;
-    for (int i = tid; i < MELK_FFT; i += 256) win[i] = sp[i] * window[i];
+    const int f0 = blockIdx.x * F, nf = min(F, nframes - f0);
+    for (int i = tid; i < F * MELK_FFT; i += 256) {
+        const int f = i / MELK_FFT, n = i % MELK_FFT;
+        win[f][n] = f < nf ? samples[start0 + (long long)(f0 + f) * MELK_HOP + n] * window[n] : 0.f;
+    }
     __syncthreads();
     if (tid < MELK_FREQ) {
-        float re = 0.f, im = 0.f;
+        float re[F], im[F];
+#pragma unroll
+        for (int f = 0; f < F; f++) re[f] = im[f] = 0.f;
         for (int n = 0; n < MELK_FFT; n++) {
-            const float w = win[n];
-            re = re + w * dcosT[n * MELK_FREQ + tid];
-            im = im + w * dsinT[n * MELK_FREQ + tid];
+            const float c = dcosT[n * MELK_FREQ + tid], sn = dsinT[n * MELK_FREQ + tid];
+#pragma unroll
+            for (int f = 0; f < F; f++) {
+                const float w = win[f][n];
+                re[f] = re[f] + w * c;
+                im[f] = im[f] + w * sn;
+            }
         }
-        pw[tid] = re * re + im * im;
+#pragma unroll
+        for (int f = 0; f < F; f++) pw[f][tid] = re[f] * re[f] + im[f] * im[f];
     }
     __syncthreads();
     if (tid < MELK_BINS) {
-        float sum = 0.f;
-        for (int k = 0; k < MELK_FREQ; k++) sum = sum + filtT[k * MELK_BINS + tid] * pw[k];
-        if (sum < 1e-10f) sum = 1e-10f;
-        float v = log10f(sum);
-        if (v < log_min) v = log_min;
-        mel[(size_t)blockIdx.x * MELK_BINS + tid] = (v + 4.0f) / 4.0f;
+        float sum[F];
+#pragma unroll
+        for (int f = 0; f < F; f++) sum[f] = 0.f;
+        for (int k = 0; k < MELK_FREQ; k++) {
+            const float fw = filtT[k * MELK_BINS + tid];
+#pragma unroll
+            for (int f = 0; f < F; f++) sum[f] = sum[f] + fw * pw[f][k];
+        }
+#pragma unroll
+        for (int f = 0; f < F; f++) {
+            if (f >= nf) break;
+            float v = sum[f];
+            if (v < 1e-10f) v = 1e-10f;
+            v = log10f(v);
+            if (v < log_min) v = log_min;
+            mel[(size_t)(f0 + f) * MELK_BINS + tid] = (v + 4.0f) / 4.0f;
+        }
     }
 }
 
@@ -3768,12 +3794,21 @@ hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, f
     return hipSuccess;
 }
 
+VOX_KB_KNOB(g_mel_fpb, 0);  // tools/kbench knob: frames per k_mel_frames block (0 = by count)
 hipError_t launch_mel_frames(const float* samples, long long start0, int nframes, const float* window,
                              const float* dcosT, const float* dsinT, const float* filtT, float log_min, float* mel,
                              hipStream_t st) {
     if (nframes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mel_frames, dim3(nframes), dim3(256), 0, st, samples, start0, window, dcosT, dsinT, filtT,
-                       log_min, mel);
+    // frames per block: one for a streaming feed (50 frames: 20.4 us against 38.3 with 4, the
+    // block's serial DFT sets the time), 4 from 512 frames on (a clip's mel: 3000 frames 109.9
+    // -> 43.4 us); tools/kbench VOX_KB_ONLY=mel, profiles/r6_kbench_mel.txt
+    const int F = g_mel_fpb ? g_mel_fpb : nframes >= 512 ? 4 : 1;
+#define MEL_F(FF)                                                                                              \
+    if (F == FF) hipLaunchKernelGGL(k_mel_frames<FF>, dim3((nframes + FF - 1) / FF), dim3(256), 0, st, samples, \
+                                    start0, nframes, window, dcosT, dsinT, filtT, log_min, mel);
+    MEL_F(1) MEL_F(2) MEL_F(4) MEL_F(8)
+#undef MEL_F
+    if (F != 1 && F != 2 && F != 4 && F != 8) return hipErrorInvalidValue;
     LAUNCH_CHECK();
     return hipSuccess;
 }

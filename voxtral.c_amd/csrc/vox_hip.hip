@@ -508,6 +508,7 @@ struct vox_hip_stream {
     int* eticket;            // k_sklx slice tickets [SKX_TICKETS] (zeroed, self-resetting)
     int enc_async;           // vox_hip_stream_encode_mel returns without a stream sync
     float* xbatch;           // stacked encoder rows of a batched pass led by this stream
+    float *cs_im, *cs_c0;    // its stacked conv-stem im2col rows / conv0 rows (enc_prefix_batch)
     float *abatch, *abatch_out;  // its stacked adapter input rows (4 x enc_dim) / adapter rows
     float* essq;             // k_sklx row sums of squares per column slice [2][slices][16]
     uint16_t *gpa, *gpc;     // k_gemmf planes: norm / attention rows (K <= max(enc_dim, heads x hd)), gate rows
@@ -679,7 +680,7 @@ extern "C" void vox_hip_stream_free(vox_hip_stream_t* s) {
     dfree(s->gate); dfree(s->enc_res); dfree(s->rope_rows); dfree(s->adapter); dfree(s->ad_mid);
     dfree(s->xd); dfree(s->xnd); dfree(s->qkvd); dfree(s->qd_); dfree(s->attd); dfree(s->gated);
     dfree(s->part); dfree(s->logits); dfree(s->pval); dfree(s->pidx); dfree(s->state); dfree(s->twin_state); dfree(s->tokens);
-    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch); dfree(s->abatch); dfree(s->abatch_out);
+    dfree(s->part_alt); dfree(s->alts); dfree(s->gws); dfree(s->exp_); dfree(s->eslab); dfree(s->eticket); dfree(s->essq); dfree(s->exp2); dfree(s->xbatch); dfree(s->abatch); dfree(s->abatch_out); dfree(s->cs_im); dfree(s->cs_c0);
     dfree(s->gpa); dfree(s->gpc); dfree(s->gflags); dfree(s->dpa); dfree(s->dpc);
     if (s->evt[0]) hipEventDestroy(s->evt[0]);
     if (s->evt[1]) hipEventDestroy(s->evt[1]);
@@ -1367,6 +1368,94 @@ static int enc_prefix(vox_hip_stream_t* s, const float* mel, int n, int mel_on_d
     return 0;
 }
 
+// enc_prefix for several streams at once, on lead's queue, the two conv GEMMs run once over
+// every stream's rows (the conv weights read once per pass; 2 launches instead of 2 per
+// stream).  Stream b's conv0 rows form segment [c0_tail(2) | residual (res) | new (n)] of one
+// stacked buffer, laid out as enc_prefix's c0_p: the GEMM also computes the tail / residual
+// rows (from stale im2col rows; rows are independent) and the true ones are copied over them;
+// conv1 writes stream b's T1[b] encoder rows straight to X at its stacked offset.  Per row the
+// same products as enc_prefix (voxtral.c:594-756).  Returns the stacked rows N (-1 error).
+static const int CS_ROWS = 2 * ENC_SUB + 5 * VOX_MAX_BATCH;  // conv0 rows of a batched pass
+static bool enc_prefix_batch_fits(vox_hip_stream_t* const* ss, const int* n, int B) {
+    long long r0 = 0, r1 = 0;
+    for (int b = 0; b < B; b++)
+        if (n[b] > 0) {
+            r0 += 2 + ss[b]->res_count + n[b];
+            r1 += (ss[b]->res_count + n[b]) / 2;
+        }
+    return r0 <= CS_ROWS && r1 <= ENC_SUB;
+}
+
+static int enc_prefix_batch(vox_hip_stream_t* lead, vox_hip_stream_t* const* ss, const float* const* mels,
+                            const int* n, int B, int mel_on_device, float* X, int* T1, int* off) {
+    vox_hip_model_t* m = lead->m;
+    const vox_hip_config_t& c = m->c;
+    const int MB = c.mel_bins, ED = c.enc_dim;
+    hipStream_t st = lead->st;
+    if (!lead->cs_im) {
+        CK(dalloc(&lead->cs_im, std::max((size_t)CS_ROWS * MB * 3, (size_t)ENC_SUB * ED * 3)));
+        CK(dalloc(&lead->cs_c0, (size_t)CS_ROWS * ED));
+    }
+    std::vector<int> seg(B, 0), res(B, 0), tot(B, 0);
+    int R0 = 0, N = 0;
+    for (int b = 0; b < B; b++) {
+        T1[b] = 0;
+        off[b] = N;
+        if (n[b] <= 0) continue;
+        vox_hip_stream_t* s = ss[b];
+        if (stream_alloc_frames(s, n[b] + 4)) return -1;
+        seg[b] = R0;
+        res[b] = s->res_count;
+        tot[b] = s->res_count + n[b];
+        R0 += 2 + s->res_count + n[b];
+        const int feed = tot[b] - (tot[b] & 1);
+        T1[b] = feed > 0 ? feed / 2 : 0;
+        N += T1[b];
+    }
+    // the members' queues (their mel frames) before the lead's
+    for (int b = 0; b < B; b++)
+        if (ss[b] != lead && n[b] > 0) {
+            CK(hipEventRecord(ss[b]->sev, ss[b]->st));
+            CK(hipStreamWaitEvent(st, ss[b]->sev, 0));
+        }
+    // ---- conv0 (voxtral.c:594-651) over every stream's [mel_tail(2) | new n] ----
+    for (int b = 0; b < B; b++) {
+        if (n[b] <= 0) continue;
+        vox_hip_stream_t* s = ss[b];
+        CK(hipMemcpyAsync(s->mel_p, s->mel_tail, (size_t)2 * MB * 4, hipMemcpyDeviceToDevice, st));
+        CK(hipMemcpyAsync(s->mel_p + (size_t)2 * MB, mels[b], (size_t)n[b] * MB * 4,
+                          mel_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+        CK(launch_mel_tail(s->mel_p, n[b], MB, s->mel_tail, st));
+        CK(launch_im2col3(s->mel_p, MB, n[b], 1, 0, lead->cs_im + (size_t)(seg[b] + 2 + res[b]) * MB * 3, st));
+    }
+    CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, lead->cs_im, MB * 3, m->conv0_w, nullptr, MB * 3, R0, ED,
+                   m->conv0_b, lead->cs_c0, ED, st, lead->gws, lead->gws_n));
+    // the true tail / residual rows over the computed ones; the new residual row kept
+    for (int b = 0; b < B; b++) {
+        if (n[b] <= 0) continue;
+        vox_hip_stream_t* s = ss[b];
+        float* c0p = lead->cs_c0 + (size_t)seg[b] * ED;
+        CK(hipMemcpyAsync(c0p, s->c0_tail, (size_t)2 * ED * 4, hipMemcpyDeviceToDevice, st));
+        if (res[b]) CK(hipMemcpyAsync(c0p + (size_t)2 * ED, s->c0_res, (size_t)ED * 4, hipMemcpyDeviceToDevice, st));
+        const int new_res = tot[b] & 1;
+        if (new_res)
+            CK(hipMemcpyAsync(s->c0_res, c0p + (size_t)(2 + tot[b] - 1) * ED, (size_t)ED * 4, hipMemcpyDeviceToDevice, st));
+        s->res_count = new_res;
+        // ---- conv1 im2col over [c0_tail(2) | feed], first output discarded (voxtral.c:694-756) ----
+        if (T1[b] > 0) {
+            const int feed = 2 * T1[b];
+            CK(launch_im2col3(c0p, ED, T1[b], 2, 1, lead->cs_im + (size_t)off[b] * ED * 3, st));
+            CK(hipMemcpyAsync(s->c0_tail, c0p + (size_t)feed * ED, (size_t)2 * ED * 4, hipMemcpyDeviceToDevice, st));
+        }
+    }
+    if (N > 0)
+        CK(launch_gemm(c.gelu_erf ? EPI_GELU_ERF : EPI_GELU, 3, lead->cs_im, ED * 3, m->conv1_w, nullptr, ED * 3, N, ED,
+                       m->conv1_b, X, ED, st, lead->gws, lead->gws_n));
+    for (int b = 0; b < B; b++)
+        if (T1[b] > 0 && ensure_rope(ss[b], ss[b]->enc_pos + T1[b] + 1)) return -1;
+    return N;
+}
+
 static int enc_suffix(vox_hip_stream_t* s, float* xin, int T1) {
     vox_hip_model_t* m = s->m;
     const vox_hip_config_t& c = m->c;
@@ -1561,19 +1650,39 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
     std::vector<float*> xin(B);
     std::vector<long long> pos0(B);
     int N = 0;
-    for (int b = 0; b < B; b++) {
-        if (enc_prefix(ss[b], mels[b], n[b], mel_on_device, &T1[b], &xin[b])) return -1;
-        off[b] = N;
-        pos0[b] = ss[b]->enc_pos;
-        N += T1[b];
-    }
     bool all_async = true;
+    // encoder rows each stream's frames complete (enc_prefix's stride alignment, on the host)
     int active = 0;
     for (int b = 0; b < B; b++) {
         all_async = all_async && ss[b]->enc_async;
-        active += T1[b] > 0;
+        if (n[b] > 0) {
+            const int tot = ss[b]->res_count + n[b];
+            active += tot - (tot & 1) > 0;
+        }
     }
-    if (N > ENC_SUB || active <= 1) {
+    // several streams with rows: the conv stems stacked on the lead's queue (one GEMM per
+    // conv for all of them, VOX_HIP_ENC_STEM_BATCH=0: one stream at a time), rows straight
+    // into the stacked layer input
+    static int stem_batch = -1;
+    if (stem_batch < 0) {
+        const char* e = getenv("VOX_HIP_ENC_STEM_BATCH");
+        stem_batch = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    const bool stacked = stem_batch && active > 1 && enc_prefix_batch_fits(ss, n, B);
+    if (stacked) {
+        if (!lead->xbatch) CK(dalloc(&lead->xbatch, (size_t)ENC_SUB * ED));
+        N = enc_prefix_batch(lead, ss, mels, n, B, mel_on_device, lead->xbatch, T1.data(), off.data());
+        if (N < 0) return -1;
+        for (int b = 0; b < B; b++) pos0[b] = ss[b]->enc_pos;
+    } else {
+        for (int b = 0; b < B; b++) {
+            if (enc_prefix(ss[b], mels[b], n[b], mel_on_device, &T1[b], &xin[b])) return -1;
+            off[b] = N;
+            pos0[b] = ss[b]->enc_pos;
+            N += T1[b];
+        }
+    }
+    if (!stacked && (N > ENC_SUB || active <= 1)) {
         // one stream at a time: rows beyond one pass, or a single stream with rows (its own
         // path keeps the skinny fused kernels for a short chunk)
         for (int b = 0; b < B; b++) {
@@ -1589,17 +1698,19 @@ extern "C" int vox_hip_stream_encode_mel_batch(vox_hip_stream_t* const* ss, cons
             if (added[b] < 0) return -1;
         }
     } else {
-        if (!lead->xbatch) CK(dalloc(&lead->xbatch, (size_t)ENC_SUB * ED));
-        // the lead's queue waits for every member's conv stem (each stream's own reusable
-        // event), stacks the rows, runs the layers
-        for (int b = 1; b < B; b++) {
-            CK(hipEventRecord(ss[b]->sev, ss[b]->st));
-            CK(hipStreamWaitEvent(lead->st, ss[b]->sev, 0));
+        if (!stacked) {
+            if (!lead->xbatch) CK(dalloc(&lead->xbatch, (size_t)ENC_SUB * ED));
+            // the lead's queue waits for every member's conv stem (each stream's own reusable
+            // event), stacks the rows, runs the layers
+            for (int b = 1; b < B; b++) {
+                CK(hipEventRecord(ss[b]->sev, ss[b]->st));
+                CK(hipStreamWaitEvent(lead->st, ss[b]->sev, 0));
+            }
+            for (int b = 0; b < B; b++)
+                if (T1[b] > 0)
+                    CK(hipMemcpyAsync(lead->xbatch + (size_t)off[b] * ED, xin[b], (size_t)T1[b] * ED * 4,
+                                      hipMemcpyDeviceToDevice, lead->st));
         }
-        for (int b = 0; b < B; b++)
-            if (T1[b] > 0)
-                CK(hipMemcpyAsync(lead->xbatch + (size_t)off[b] * ED, xin[b], (size_t)T1[b] * ED * 4,
-                                  hipMemcpyDeviceToDevice, lead->st));
         // adapter buffers sized now, before the pass is on the lead's queue: growing one later
         // (stream_alloc_adapter synchronises the stream's queue) would wait for the whole pass
         for (int b = 0; b < B; b++)

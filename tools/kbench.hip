@@ -12,7 +12,7 @@
 #include "../voxtral.c_amd/csrc/vox_hip_dev.h"
 
 using namespace vox;
-namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_mel_fpb, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
+namespace vox { extern int g_skf_r, g_skf_nw, g_skf_d, g_skl_nw, g_gemv_rb, g_attn_lw, g_attn_blocks, g_attn_short, g_gemmf_rb, g_gemmf_minu, g_gemmf_wr, g_gemmf_order, g_mel_fpb, g_skf2_r, g_attn_kvfast, g_attn_bsplit, g_gemv_maxb; }
 #ifdef VOX_GEMV_STAMPS
 namespace vox { hipError_t gemv_set_stamps(unsigned long long* p); }
 #endif
@@ -558,6 +558,27 @@ int main(int argc, char** argv) {
             char nm[96];
             snprintf(nm, sizeof nm, "skf lm 131072x3072 nb%d", nb);
             add(nm, timeit([&] { CK(launch_gemm_skf(xp, D, emb, nullptr, V, nb, Cs, V, st)); }, iters / 4 + 1, st), (double)V * D * 2);
+        }
+        // the LM head at 32 rows: two launches (one per 16-row block) against one k_skf<Z = 2>
+        // launch (R = 1 / 2 / 4 row groups per block); logits compared bit for bit
+        {
+            add("skf lm nb32 as 2 launches", timeit([&] {
+                    CK(launch_gemm_skf(xp, D, emb, nullptr, V, 16, Cs, V, st));
+                    CK(launch_gemm_skf(xp + (size_t)3 * 16 * D, D, emb, nullptr, V, 16, Cs + (size_t)16 * V, V, st));
+                }, iters / 4 + 1, st), (double)V * D * 2);
+            std::vector<float> l0((size_t)32 * V), l1((size_t)32 * V);
+            CK(hipStreamSynchronize(st));
+            CK(hipMemcpy(l0.data(), Cs, l0.size() * 4, hipMemcpyDeviceToHost));
+            for (int r : {1, 2, 4}) {
+                g_skf2_r = r;
+                CK(launch_gemm_skf2(xp, D, emb, nullptr, V, 32, Cs, V, st));
+                CK(hipStreamSynchronize(st));
+                CK(hipMemcpy(l1.data(), Cs, l1.size() * 4, hipMemcpyDeviceToHost));
+                char nm[96];
+                snprintf(nm, sizeof nm, "skf2 lm nb32 R%d (%s)", r, memcmp(l0.data(), l1.data(), l0.size() * 4) ? "BITS DIFFER" : "same bits");
+                add(nm, timeit([&] { CK(launch_gemm_skf2(xp, D, emb, nullptr, V, 32, Cs, V, st)); }, iters / 4 + 1, st), (double)V * D * 2);
+            }
+            g_skf2_r = 4;
         }
         return 0;
     }

@@ -2800,10 +2800,19 @@ static int batch_step(vox_hip_batch_t* b, int nb, int splits, int kv16) {
     // final norm (after the last w2 residual) + LM head (tied embeddings) + per-slot argmax,
     // state, token log and next inputs (decoder.c:762-779)
     CK(launch_rmsnorm_fplanes(b->x, nb, DD, m->dec_norm, nullptr, c.dec_eps, b->xp_d, b->part, Sres, st));
-    // (one k_skf launch per 16-row block: its planes are read per block from L2)
-    for (int r0 = 0; r0 < nb; r0 += SK_ROWS)
-        CK(launch_gemm_skf(b->xp_d + (size_t)r0 * 3 * DD, DD, m->lm_frag, m->tok_emb_s, c.vocab, std::min(SK_ROWS, nb - r0),
-                           b->logits + (size_t)r0 * c.vocab, c.vocab, st));
+    // 17..32 rows: both 16-row blocks in one k_skf launch (the embeddings read once;
+    // VOX_HIP_SKF2=0: one launch per 16-row block)
+    static int skf2 = -1;
+    if (skf2 < 0) {
+        const char* e = getenv("VOX_HIP_SKF2");
+        skf2 = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    if (skf2 && nb > SK_ROWS)
+        CK(launch_gemm_skf2(b->xp_d, DD, m->lm_frag, m->tok_emb_s, c.vocab, nb, b->logits, c.vocab, st));
+    else
+        for (int r0 = 0; r0 < nb; r0 += SK_ROWS)
+            CK(launch_gemm_skf(b->xp_d + (size_t)r0 * 3 * DD, DD, m->lm_frag, m->tok_emb_s, c.vocab,
+                               std::min(SK_ROWS, nb - r0), b->logits + (size_t)r0 * c.vocab, c.vocab, st));
     CK(launch_argmax_batch(b->logits, nb, c.vocab, b->pval, b->pidx, b->palt, b->slots, TOKENS_CAP, slot_toklog(b->slots),
                            m->tok_emb, m->tok_emb_s, DD, b->x, st));
     return 0;

@@ -198,6 +198,9 @@ hipError_t launch_swiglu_fplanes(const float* part, int S, int H, int nb, uint16
 // C[j][n] = sum_k x_j[k] W[n][k] (LM head: k_skf)
 hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* C,
                            int ldc, hipStream_t st);
+// launch_gemm_skf for 17..32 rows (two 16-row blocks of planes, one weight read)
+hipError_t launch_gemm_skf2(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* C,
+                            int ldc, hipStream_t st);
 // split-K slabs part[s][16][N], s < skl_splits(K, N) (projections: k_skl; k_sklx and the
 // encoder's skinny chain use skl_splits(K))
 int skl_splits(int K, int N = 0);

@@ -2216,27 +2216,30 @@ __device__ __forceinline__ bf16x8 i8x8_bf16(uint32_t lo, uint32_t hi) {
     return __builtin_bit_cast(bf16x8, make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16)));
 }
 
-// one 64-k block of R row groups (A halves) and of the three planes (B halves)
-template <int WQ8, int R>
+// one 64-k block of R row groups (A halves) and of the three planes (B halves) of Z 16-row
+// blocks of streams
+template <int WQ8, int R, int Z = 1>
 struct SkfRegs {
     u32x4 a[R][WQ8 ? 1 : 2];
-    uint4 x[3][2];
+    uint4 x[Z][3][2];
 };
 
 // block b of the wave's range; past the range the loads go through zero-length descriptors
 // (they return 0 and move no bytes, so the ring below needs no branches)
-template <int WQ8, int R>
-__device__ __forceinline__ void skf_load(SkfRegs<WQ8, R>& s, __amdgpu_buffer_rsrc_t W, __amdgpu_buffer_rsrc_t X,
+template <int WQ8, int R, int Z>
+__device__ __forceinline__ void skf_load(SkfRegs<WQ8, R, Z>& s, __amdgpu_buffer_rsrc_t W, __amdgpu_buffer_rsrc_t X,
                                          int kbytes, int b, int pbytes) {
     constexpr int FB = WQ8 ? 1024 : 2048;
     const int lo = (threadIdx.x & 63) * 16;
 #pragma unroll
-    for (int p = 0; p < 3; p++)
+    for (int z = 0; z < Z; z++)
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(X, lo + t * 1024, p * pbytes + b * 2048, 0);
-            s.x[p][t] = make_uint4(v.x, v.y, v.z, v.w);
-        }
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(X, lo + t * 1024, (z * 3 + p) * pbytes + b * 2048, 0);
+                s.x[z][p][t] = make_uint4(v.x, v.y, v.z, v.w);
+            }
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
@@ -2244,8 +2247,8 @@ __device__ __forceinline__ void skf_load(SkfRegs<WQ8, R>& s, __amdgpu_buffer_rsr
             s.a[r][t] = __builtin_amdgcn_raw_buffer_load_b128(W, lo + t * 1024, r * kbytes + b * FB, 2);
 }
 
-template <int WQ8, int R>
-__device__ __forceinline__ void skf_mma(const SkfRegs<WQ8, R>& s, f32x4 (&acc)[R]) {
+template <int WQ8, int R, int Z>
+__device__ __forceinline__ void skf_mma(const SkfRegs<WQ8, R, Z>& s, f32x4 (&acc)[Z][R]) {
 #pragma unroll
     for (int t = 0; t < 2; t++)
 #pragma unroll
@@ -2259,20 +2262,24 @@ __device__ __forceinline__ void skf_mma(const SkfRegs<WQ8, R>& s, f32x4 (&acc)[R
                 af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
             }
 #pragma unroll
-            for (int p = 0; p < 3; p++)
-                acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, s.x[p][t]), acc[r], 0, 0, 0);
+            for (int z = 0; z < Z; z++)
+#pragma unroll
+                for (int p = 0; p < 3; p++)
+                    acc[z][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8, s.x[z][p][t]), acc[z][r], 0, 0, 0);
         }
 }
 
 // Block = R row groups (16R rows) x all of K, K split over NW waves in 64-k blocks; the
-// wave partials meet in LDS and the block stores its 16R x 16 outputs C[j][row] (the LM head:
+// wave partials meet in LDS and the block stores its 16R x 16Z outputs C[j][row] (the LM head:
 // its planes fit no LDS, and at 8192 row groups the per-block plane re-reads are amortised
-// over R = 4 groups).
-template <int WQ8, int R, int NW, int D>
+// over R = 4 groups).  Z = 2: both 16-row blocks of a 32-stream step against each weight
+// fragment the wave loads, so the 805 MB of embeddings cross the load path once per step
+// instead of once per row block (the planes of a row block z follow block z - 1's three).
+template <int WQ8, int R, int NW, int D, int Z = 1>
 __global__ __launch_bounds__(NW * 64) void k_skf(const uint16_t* __restrict__ xs, int K,
                                                  const uint8_t* __restrict__ W, const float* __restrict__ wscale,
                                                  int N, int nb, float* __restrict__ C, int ldc) {
-    __shared__ float red[NW][R][4][64];
+    __shared__ float red[NW][Z * R][4][64];
     constexpr int FB = WQ8 ? 1024 : 2048;
     // wave index through readfirstlane: a provably uniform block range keeps the buffer
     // loads' soffset in an SGPR (else every load becomes a waterfall loop)
@@ -2285,20 +2292,22 @@ __global__ __launch_bounds__(NW * 64) void k_skf(const uint16_t* __restrict__ xs
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g0 * kbytes, 0, R * kbytes, 0x00020000);
     const int pbytes = SK_ROWS * K * 2;  // one plane
     const __amdgpu_buffer_rsrc_t Xd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xs), 0, 3 * pbytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xs), 0, Z * 3 * pbytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t Wz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W), 0, 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t Xz = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xs), 0, 0, 0x00020000);
-    f32x4 acc[R];
+    f32x4 acc[Z][R];
 #pragma unroll
-    for (int r = 0; r < R; r++) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < Z; z++)
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[z][r] = f32x4{0.f, 0.f, 0.f, 0.f};
     // register ring of D blocks: block b + D - 1 is requested before block b's MFMAs, so a
     // wave keeps D - 1 blocks of weights and planes in flight
-    SkfRegs<WQ8, R> s[D];
+    SkfRegs<WQ8, R, Z> s[D];
 #define SKF_LOAD(slot, blk)                                                                  \
     do {                                                                                     \
         const int bb__ = (blk);                                                              \
         const bool in__ = bb__ < b1;                                                         \
-        skf_load<WQ8, R>(s[slot], in__ ? Wd : Wz, in__ ? Xd : Xz, kbytes, in__ ? bb__ : 0, pbytes); \
+        skf_load<WQ8, R, Z>(s[slot], in__ ? Wd : Wz, in__ ? Xd : Xz, kbytes, in__ ? bb__ : 0, pbytes); \
     } while (0)
 #pragma unroll
     for (int i = 0; i < D - 1; i++) SKF_LOAD(i, b0 + i);
@@ -2307,27 +2316,29 @@ __global__ __launch_bounds__(NW * 64) void k_skf(const uint16_t* __restrict__ xs
         for (int i = 0; i < D; i++) {
             SKF_LOAD((i + D - 1) % D, b + i + D - 1);
             __builtin_amdgcn_sched_barrier(0);
-            skf_mma<WQ8, R>(s[i], acc);  // zeros past the range: acc + 0
+            skf_mma<WQ8, R, Z>(s[i], acc);  // zeros past the range: acc + 0
             __builtin_amdgcn_sched_barrier(0);
         }
     }
 #undef SKF_LOAD
 #pragma unroll
-    for (int r = 0; r < R; r++)
+    for (int z = 0; z < Z; z++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) red[wave][r][i][lane] = acc[r][i];
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) red[wave][z * R + r][i][lane] = acc[z][r][i];
     __syncthreads();
-    // output o: group r = o >> 8, row rr = (o >> 4) & 15, stream j = o & 15; D layout:
-    // col = lane&15, row = (lane>>4)*4 + i
-    for (int o = tid; o < R * 256; o += NW * 64) {
-        const int r = o >> 8, rr = (o >> 4) & 15, j = o & 15;
-        if (j >= nb) continue;
+    // output o: row block z = o / (256 R), group r = (o >> 8) % R, row rr = (o >> 4) & 15,
+    // stream j = o & 15 of the row block; D layout: col = lane&15, row = (lane>>4)*4 + i
+    for (int o = tid; o < Z * R * 256; o += NW * 64) {
+        const int zr = o >> 8, z = zr / R, r = zr % R, rr = (o >> 4) & 15, j = o & 15;
+        if (z * 16 + j >= nb) continue;
         const int ln = ((rr >> 2) << 4) + j, i = rr & 3;
         const int row = (g0 + r) * 16 + rr;
         float v = 0.f;
 #pragma unroll
-        for (int w = 0; w < NW; w++) v += red[w][r][i][ln];
-        C[(size_t)j * ldc + row] = WQ8 ? v * wscale[row] : v;
+        for (int w = 0; w < NW; w++) v += red[w][zr][i][ln];
+        C[(size_t)(z * 16 + j) * ldc + row] = WQ8 ? v * wscale[row] : v;
     }
 }
 
@@ -3588,10 +3599,10 @@ VOX_KB_KNOB(g_skf_nw, 0);
 VOX_KB_KNOB(g_skf_d, 0);
 VOX_KB_KNOB(g_skl_nw, 0);
 
-template <int Q, int R, int NW, int D>
+template <int Q, int R, int NW, int D, int Z = 1>
 static hipError_t skf_launch(const uint16_t* xs, int K, const void* W, const float* wscale, int N, int nb,
                              float* C, int ldc, hipStream_t st) {
-    hipLaunchKernelGGL((k_skf<Q, R, NW, D>), dim3(N / (16 * R)), dim3(NW * 64), 0, st, xs, K,
+    hipLaunchKernelGGL((k_skf<Q, R, NW, D, Z>), dim3(N / (16 * R)), dim3(NW * 64), 0, st, xs, K,
                        static_cast<const uint8_t*>(W), wscale, N, nb, C, ldc);
     return hipGetLastError();
 }
@@ -3618,6 +3629,24 @@ hipError_t launch_gemm_skf(const uint16_t* xs, int K, const void* Wf, const floa
                            int ldc, hipStream_t st) {
     if (nb < 1 || nb > SK_ROWS || N % 64 || K % 64 || !C) return hipErrorInvalidValue;
     return wscale ? skf_cfg<1>(xs, K, Wf, wscale, N, nb, C, ldc, st) : skf_cfg<0>(xs, K, Wf, wscale, N, nb, C, ldc, st);
+}
+
+// 17..32 rows (two 16-row blocks of planes, block 1's after block 0's three) in one launch
+// reading every weight once: R = 4 row groups per block, 4 waves, 2-deep ring.  tools/kbench
+// (profiles/r6_kbench_skf2.txt), the LM head at 32 rows: two 16-row launches 250.0 us, one
+// launch at R = 1 / 2 / 4 328.1 / 192.1 / 149.3 us, the same bits
+VOX_KB_KNOB(g_skf2_r, 4);
+hipError_t launch_gemm_skf2(const uint16_t* xs, int K, const void* Wf, const float* wscale, int N, int nb, float* C,
+                            int ldc, hipStream_t st) {
+    if (nb <= SK_ROWS || nb > 2 * SK_ROWS || N % 64 || K % 64 || !C) return hipErrorInvalidValue;
+    const int r = g_skf2_r;
+    if ((N / 16) % r) return hipErrorInvalidValue;
+    if (r == 1) return wscale ? skf_launch<1, 1, 4, 2, 2>(xs, K, Wf, wscale, N, nb, C, ldc, st)
+                              : skf_launch<0, 1, 4, 2, 2>(xs, K, Wf, wscale, N, nb, C, ldc, st);
+    if (r == 4) return wscale ? skf_launch<1, 4, 4, 2, 2>(xs, K, Wf, wscale, N, nb, C, ldc, st)
+                              : skf_launch<0, 4, 4, 2, 2>(xs, K, Wf, wscale, N, nb, C, ldc, st);
+    return wscale ? skf_launch<1, 2, 4, 2, 2>(xs, K, Wf, wscale, N, nb, C, ldc, st)
+                  : skf_launch<0, 2, 4, 2, 2>(xs, K, Wf, wscale, N, nb, C, ldc, st);
 }
 
 template <int Q, int NW, int KS>

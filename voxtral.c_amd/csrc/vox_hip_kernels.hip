@@ -2552,14 +2552,6 @@ __global__ __launch_bounds__(NW * 64) void k_skl2(const uint16_t* __restrict__ x
     }
 }
 
-// k_sklx (below) at PRO_SCALE / EPI_SWIGLU for 17..32 rows (the batched step's W1|W3), both
-// 16-row blocks in one block as k_skl2: each weight fragment feeds the MFMAs of both row
-// blocks (their planes in LDS), one ticket per column slice, and the slice's last block
-// finishes the SwiGLU of both.  Same splits, slabs and per-output order: the same bits.
-template <int NW, int KS>
-__global__ __launch_bounds__(NW * 64) void k_sklx2(const uint16_t* __restrict__ xs, int K,
-                                                   const uint8_t* __restrict__ W, int N, int nb, const SklFused f);
-
 // Residual + the planes of an RMSNorm without its row reduction: x += the S slabs of the
 // previous projection (+ bias, summed in split order as k_resid_rmsnorm_fplanes), the row
 // written back, the planes of x * w (* (1 + ada)) -- the inverse RMS is applied by the next
@@ -3811,23 +3803,6 @@ hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const v
     if (epi == SKX_EPI_QKV && (!f.q || !f.Kc || !f.Vc || !f.rope || f.hd % 2 || f.qd % f.hd || f.cap < 1 ||
                                N != f.qd + 2 * f.kvd))
         return hipErrorInvalidValue;
-    // 17..32 rows of the batched W1|W3: both row blocks in one block (VOX_HIP_SKLX2=0: one
-    // block per row block)
-    static int sklx2 = -1;
-    if (sklx2 < 0) {
-        const char* e = getenv("VOX_HIP_SKLX2");
-        sklx2 = (e && atoi(e) == 0) ? 0 : 1;
-    }
-    if (sklx2 && nb > SK_ROWS && nb <= 2 * SK_ROWS && pro == SKX_PRO_SCALE && epi == SKX_EPI_SWIGLU) {
-#define SKX2_X(NWW, KSS)                                                                                  \
-        if (nw == NWW && ks == KSS) {                                                                     \
-            hipLaunchKernelGGL((k_sklx2<NWW, KSS>), dim3((N / (16 * NWW)) * S), dim3(NWW * 64), 0, st, xs, K, \
-                               static_cast<const uint8_t*>(Wf), N, nb, f);                                \
-            return hipGetLastError();                                                                     \
-        }
-        SKX2_X(4, 4) SKX2_X(4, 8) SKX2_X(8, 4) SKX2_X(8, 8)
-#undef SKX2_X
-    }
 #define SKX_X(NWW, KSS, PP, EE) \
     if (nw == NWW && ks == KSS && pro == PP && epi == EE) return sklx_launch<NWW, KSS, PP, EE>(xs, K, Wf, N, nb, f, st);
 #define SKX_CFG(PP, EE) SKX_X(4, 4, PP, EE) SKX_X(4, 8, PP, EE) SKX_X(8, 4, PP, EE) SKX_X(8, 8, PP, EE)
@@ -3838,134 +3813,6 @@ hipError_t launch_gemm_sklx(int pro, int epi, const uint16_t* xs, int K, const v
 #undef SKX_CFG
 #undef SKX_X
     return hipErrorInvalidValue;
-}
-
-template <int NW, int KS>
-__global__ __launch_bounds__(NW * 64) void k_sklx2(const uint16_t* __restrict__ xs, int K,
-                                                   const uint8_t* __restrict__ W, int N, int nb, const SklFused f) {
-    __shared__ uint4 xb[2][KS * 6 * 64];  // [row block][block][plane][half][lane]
-    __shared__ float s_ss[2][2 * NW * 64];
-    __shared__ int s_fin;
-    constexpr int FB = 2048;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int KB = K >> 6, S = KB / KS, X = N / (16 * NW);
-    const int u = blockIdx.x;
-    const int s = u / X, xi = u % X, kb0 = s * KS;
-    const int g = xi * NW + wave;
-    const __amdgpu_buffer_rsrc_t Wd =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(W) + (size_t)g * KB * FB, 0, KB * FB, 0x00020000);
-    u32x4 a[KS][2];
-    constexpr int NF = KS * 6 / NW;
-    const size_t P = (size_t)SK_ROWS * K;
-    uint4 fp[2][NF];
-#pragma unroll
-    for (int z = 0; z < 2; z++)
-#pragma unroll
-        for (int i = 0; i < NF; i++) {
-            const int idx = tid + i * NW * 64;
-            const int blk = idx / 384, rem = idx % 384;
-            const int p = rem >> 7, t = (rem >> 6) & 1, l = rem & 63;
-            fp[z][i] = *reinterpret_cast<const uint4*>(xs + (size_t)z * 3 * P + p * P + (size_t)((kb0 + blk) * 2 + t) * 512 + l * 8);
-        }
-    // the producer's per-slice row sums of squares of both row blocks, all in flight at once
-    const int nss = f.nsl * SK_ROWS;
-    float ssv[2][2];
-#pragma unroll
-    for (int z = 0; z < 2; z++) {
-        const float* sp = f.ssq_in + (size_t)z * nss;
-        ssv[z][0] = tid < nss ? sp[tid] : 0.f;
-        ssv[z][1] = tid + NW * 64 < nss ? sp[tid + NW * 64] : 0.f;
-    }
-#pragma unroll
-    for (int kb = 0; kb < KS; kb++)
-#pragma unroll
-        for (int t = 0; t < 2; t++)
-            a[kb][t] = __builtin_amdgcn_raw_buffer_load_b128(Wd, lane * 16 + t * 1024, (kb0 + kb) * FB, 2);
-#pragma unroll
-    for (int z = 0; z < 2; z++) {
-#pragma unroll
-        for (int i = 0; i < NF; i++) xb[z][tid + i * NW * 64] = fp[z][i];
-        if (tid < nss) s_ss[z][tid] = ssv[z][0];
-        if (tid + NW * 64 < nss) s_ss[z][tid + NW * 64] = ssv[z][1];
-    }
-    __syncthreads();
-    // the inverse RMS of this lane's row j = lane & 15 in each row block (slices in order)
-    float inv[2];
-#pragma unroll
-    for (int z = 0; z < 2; z++) {
-        float ss = 0.f;
-        for (int q = 0; q < f.nsl; q++) ss += s_ss[z][q * SK_ROWS + (lane & 15)];
-        inv[z] = 1.0f / sqrtf(ss / (float)K + f.eps);
-    }
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int kb = 0; kb < KS; kb++)
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            const u32x4 q = a[kb][t];
-            const bf16x8 af = __builtin_bit_cast(bf16x8, make_uint4(q.x, q.y, q.z, q.w));
-#pragma unroll
-            for (int z = 0; z < 2; z++)
-#pragma unroll
-                for (int p = 0; p < 3; p++)
-                    acc[z] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        af, __builtin_bit_cast(bf16x8, xb[z][((kb * 3 + p) * 2 + t) * 64 + lane]), acc[z], 0, 0, 0);
-        }
-    // slabs [z][s][16][N] out write-through (sc1), then the slice's ticket (k_sklx)
-    const __amdgpu_buffer_rsrc_t Pd =
-        __builtin_amdgcn_make_buffer_rsrc(f.part, 0, 2 * S * SK_ROWS * N * 4, 0x00020000);
-#pragma unroll
-    for (int z = 0; z < 2; z++) {
-        const int j = lane & 15;
-#pragma unroll
-        for (int i = 0; i < 4; i++) acc[z][i] *= inv[z];
-        if (z * SK_ROWS + j < nb)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4{__float_as_uint(acc[z][0]), __float_as_uint(acc[z][1]), __float_as_uint(acc[z][2]), __float_as_uint(acc[z][3])},
-                Pd, ((((size_t)z * S + s) * SK_ROWS + j) * N + g * 16 + (lane >> 4) * 4) * 4, 0, 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* tk = f.ticket + xi;
-    if (tid == 0) s_fin = S == 1 || __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-    __syncthreads();
-    if (!s_fin) return;
-    if (tid == 0 && S > 1) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ---- this block completes slice xi of both row blocks: hidden units of rows z * 16 + j ----
-    auto slab2 = [&](int z, int j, int n) -> float2 {  // psum2 over write-through slabs (sc1 loads)
-        float2 v = make_float2(0.f, 0.f);
-        for (int s0 = 0; s0 < S; s0 += 8) {
-            u32x2 t[8];
-#pragma unroll
-            for (int c = 0; c < 8; c++)
-                if (s0 + c < S)
-                    t[c] = __builtin_amdgcn_raw_buffer_load_b64(Pd, ((((size_t)z * S + s0 + c) * SK_ROWS + j) * N + n) * 4, 0, 16);
-#pragma unroll
-            for (int c = 0; c < 8; c++)
-                if (s0 + c < S) {
-                    v.x = (s0 + c) ? v.x + __uint_as_float(t[c].x) : __uint_as_float(t[c].x);
-                    v.y = (s0 + c) ? v.y + __uint_as_float(t[c].y) : __uint_as_float(t[c].y);
-                }
-        }
-        return v;
-    };
-    // thread: row j, hidden units h0, h0 + 1 (W1 row rg, W3 row rg + 16: upload_w13)
-    constexpr int TPR = NW * 4;
-    const int j = tid / TPR, pp = tid % TPR;
-#pragma unroll
-    for (int z = 0; z < 2; z++) {
-        if (z * SK_ROWS + j >= nb) continue;
-        const int H = N / 2, h0 = xi * NW * 8 + 2 * pp;
-        const int rg = (h0 >> 4) * 32 + (h0 & 15);
-        const float2 g2 = slab2(z, j, rg), u2 = slab2(z, j, rg + 16);
-        uint16_t hh[2], mm[2], ll[2];
-        split3(silu(g2.x) * u2.x, hh[0], mm[0], ll[0]);
-        split3(silu(g2.y) * u2.y, hh[1], mm[1], ll[1]);
-        const int jj = z * SK_ROWS + j;
-        *reinterpret_cast<uint32_t*>(f.planes + frag_at(jj, H, 0, h0)) = hh[0] | ((uint32_t)hh[1] << 16);
-        *reinterpret_cast<uint32_t*>(f.planes + frag_at(jj, H, 1, h0)) = mm[0] | ((uint32_t)mm[1] << 16);
-        *reinterpret_cast<uint32_t*>(f.planes + frag_at(jj, H, 2, h0)) = ll[0] | ((uint32_t)ll[1] << 16);
-    }
 }
 
 hipError_t launch_im2col3(const float* src, int C, int T, int stride, int off, float* A,

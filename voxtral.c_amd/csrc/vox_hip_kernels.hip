@@ -3429,12 +3429,13 @@ static hipError_t attn_batch_fused(const AttnPtrs& p, const AttnFuse& f, int nb,
                                    int H, int KVH, int splits, int maxs, hipStream_t st) {
     if (g_attn_bsplit < 0) {
         const char* e = getenv("VOX_HIP_ATT_BSPLIT");
-        g_attn_bsplit = (e && atoi(e) == 0) ? 0 : 1;
+        g_attn_bsplit = e ? std::max(0, std::min(2, atoi(e))) : 1;
     }
     // contexts <= 256 keys: one 1024-thread block per (stream, kv head) -- unless those blocks
     // cannot fill the chip (16 streams x 8 kv heads = 128 blocks on 256 CUs): then the 128-key
-    // blocks of the long path (two per (stream, kv head), last arriver merges)
-    if (splits == 1 && (!g_attn_bsplit || nb * KVH >= 256)) {
+    // blocks of the long path (two per (stream, kv head), last arriver merges);
+    // VOX_HIP_ATT_BSPLIT=2: the 128-key blocks at any row count
+    if (splits == 1 && (!g_attn_bsplit || (g_attn_bsplit == 1 && nb * KVH >= 256))) {
         hipLaunchKernelGGL((k_attn_decode<128, 4, 0, 1, ATT_WAVES, KT>), dim3(1, KVH, nb), dim3(1024), 0, st, p, cap, 0,
                            window, scale, H, KVH, maxs, f);
         LAUNCH_CHECK();

@@ -1606,11 +1606,11 @@ static int run_encoder_rows_batch(vox_hip_stream_t* lead, float* X, int N, vox_h
             er.Vc[b] = ss[b]->ev + (size_t)l * ss[b]->ecap * EKV;
         }
         CK(launch_rope_kv_rows(lead->qkv, N, EQ, EKV, hd, m->rope_enc, er, lead->q, lead->ecap, st));
+        // (k_gemmf's wo reads planes: the attention writes them itself)
         CK(launch_attn_rows(hd, lead->q, er, N, lead->ecap, lead->att, H, KVH, c.enc_window, scale, lead->gws,
-                            lead->gws_n, st));
+                            lead->gws_n, st, gf ? lead->gpa : nullptr));
         if (gf) {
             const DecFragD& F = m->efrag[l];
-            CK(launch_split_fplanes(lead->att, N, EQ, lead->gpa, st));
             if (gemmf(lead, EPI_RESID, lead->gpa, EQ, N, F.wo, ED, L.bo, X, ED, nullptr)) return -1;
             CK(launch_rmsnorm_fplanes(X, N, ED, L.ffn_norm, nullptr, c.enc_eps, lead->gpa, nullptr, 0, st));
             if (gemmf(lead, EPI_SWIGLU, lead->gpa, ED, N, F.w13, 2 * EH, nullptr, nullptr, EH, lead->gpc)) return -1;

@@ -146,7 +146,7 @@ hipError_t launch_rope_kv_rows(const float* qkv, int N, int qd, int kvd, int hd,
 // windowed attention of every stream's rows against its own ring, one launch (+ one combine):
 // Q / O stacked [N, H*hd]
 hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, int cap, float* O, int H, int KVH,
-                            int window, float scale, float* ws, size_t ws_elems, hipStream_t st);
+                            int window, float scale, float* ws, size_t ws_elems, hipStream_t st, uint16_t* xs = nullptr);
 constexpr int STEP_GRAPHS = 8;       // step graphs by attention split count 1, 2, 4, ..., 128
 hipError_t launch_attn_batch_dbg(const AttnPtrs& p, const AttnFuse& f, int nb, int cap, int window, float scale, int H,
                                  int KVH, int splits, hipStream_t st);

@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
                                                  const float* __restrict__ Vc, int cap, float* __restrict__ O,
                                                  int ldo, int M, int H, int KVH, int q_pos0, int k_first, int window,
                                                  float scale, int ns, float* __restrict__ part,
-                                                 const EncRows er = EncRows{}) {
+                                                 const EncRows er = EncRows{}, uint16_t* __restrict__ xs = nullptr) {
     constexpr int DG = HD / 4;   // S^T: dims per lane group
     constexpr int NB = HD / 16;  // P V: output dims per lane (d = NB j + b)
     __shared__ float sm[4][16], sl[4][16];
@@ -612,6 +612,21 @@ __global__ __launch_bounds__(256) void k_attn_mf(const float* __restrict__ Q, in
         if ((tid & 15) == 0) {
             pp[HD] = mx;
             pp[HD + 1] = den;
+        }
+    } else if (xs) {
+        // the output row straight into the fragment-major planes of the wo input (H * HD
+        // columns; what k_split_fplanes made of O), four dims per 8-byte piece of each plane
+        const float inv = den > 0.f ? 1.0f / den : 0.f;
+        const int row = rbase + q0 + r, K = H * HD;
+#pragma unroll
+        for (int e0 = 0; e0 < NB; e0 += 4) {
+            uint16_t hh[4], mm[4], ll[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) split3(num[e0 + e] * inv, hh[e], mm[e], ll[e]);
+            const int k = h * HD + d0 + e0;
+            *reinterpret_cast<uint2*>(xs + frag_at(row, K, 0, k)) = make_uint2(hh[0] | ((uint32_t)hh[1] << 16), hh[2] | ((uint32_t)hh[3] << 16));
+            *reinterpret_cast<uint2*>(xs + frag_at(row, K, 1, k)) = make_uint2(mm[0] | ((uint32_t)mm[1] << 16), mm[2] | ((uint32_t)mm[3] << 16));
+            *reinterpret_cast<uint2*>(xs + frag_at(row, K, 2, k)) = make_uint2(ll[0] | ((uint32_t)ll[1] << 16), ll[2] | ((uint32_t)ll[3] << 16));
         }
     } else {
         const float inv = den > 0.f ? 1.0f / den : 0.f;
@@ -3121,10 +3136,22 @@ hipError_t launch_rope_kv_rows(const float* qkv, int N, int qd, int kvd, int hd,
     return hipSuccess;
 }
 
+// VOX_HIP_ATT_PLANES=0: the attention writes f32 rows and k_split_fplanes makes the wo planes
+// (the round-5 path) instead of the attention writing the planes itself
+static int g_att_planes = -1;
+static bool att_planes() {
+    if (g_att_planes < 0) {
+        const char* e = getenv("VOX_HIP_ATT_PLANES");
+        g_att_planes = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return g_att_planes == 1;
+}
+
 hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, int cap, float* O, int H, int KVH,
-                            int window, float scale, float* ws, size_t ws_elems, hipStream_t st) {
+                            int window, float scale, float* ws, size_t ws_elems, hipStream_t st, uint16_t* xs) {
     if (N <= 0) return hipSuccess;
     if (er.B < 1 || er.B > VOX_MAX_BATCH || (hd != 64 && hd != 128)) return hipErrorInvalidValue;
+    if (xs && N > PLANE_MAX_ROWS) return hipErrorInvalidValue;
     int qbm = 0, keys = 0;
     for (int b = 0; b < er.B; b++) {
         qbm = std::max(qbm, (er.nr[b] + 15) / 16);
@@ -3141,19 +3168,23 @@ hipError_t launch_attn_rows(int hd, const float* Q, const EncRows& er, int N, in
         while (ns > 1 && (size_t)H * N * ns * (hd + 2) > ws_elems) ns--;
     }
     dim3 grid(H, qbm, ns * er.B);
+    // xs: the output rows as the wo input's planes (by the attention itself, or by the combine)
+    uint16_t* kxs = ns == 1 && att_planes() ? xs : nullptr;
     if (hd == 64)
         hipLaunchKernelGGL((k_attn_mf<64, float, 1>), grid, dim3(256), 0, st, Q, H * hd, nullptr, nullptr, cap, O, H * hd,
-                           N, H, KVH, 0, 0, window, scale, ns, ws, er);
+                           N, H, KVH, 0, 0, window, scale, ns, ws, er, kxs);
     else
         hipLaunchKernelGGL((k_attn_mf<128, float, 1>), grid, dim3(256), 0, st, Q, H * hd, nullptr, nullptr, cap, O,
-                           H * hd, N, H, KVH, 0, 0, window, scale, ns, ws, er);
+                           H * hd, N, H, KVH, 0, 0, window, scale, ns, ws, er, kxs);
     LAUNCH_CHECK();
     if (ns > 1) {
         if (hd == 64)
-            hipLaunchKernelGGL(k_attn_tiled_combine<64>, dim3(H, N), dim3(64), 0, st, ws, ns, N, O, H * hd, nullptr);
+            hipLaunchKernelGGL(k_attn_tiled_combine<64>, dim3(H, N), dim3(64), 0, st, ws, ns, N, O, H * hd, xs);
         else
-            hipLaunchKernelGGL(k_attn_tiled_combine<128>, dim3(H, N), dim3(128), 0, st, ws, ns, N, O, H * hd, nullptr);
+            hipLaunchKernelGGL(k_attn_tiled_combine<128>, dim3(H, N), dim3(128), 0, st, ws, ns, N, O, H * hd, xs);
         LAUNCH_CHECK();
+    } else if (xs && !kxs) {
+        return launch_split_fplanes(O, N, H * hd, xs, st);
     }
     return hipSuccess;
 }
@@ -3189,10 +3220,10 @@ hipError_t launch_attn_rows_mf(int hd, const float* Q, int ldq, const float* Kc,
                            q_pos0, k_first, window, scale, ns, ws);
     } else if (hd == 64) {
         hipLaunchKernelGGL(k_attn_mf<64>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
-                           k_first, window, scale, ns, ws);
+                           k_first, window, scale, ns, ws, EncRows{}, ns == 1 && att_planes() ? xs : nullptr);
     } else {
         hipLaunchKernelGGL(k_attn_mf<128>, grid, dim3(256), 0, st, Q, ldq, Kc, Vc, cap, O, ldo, M, H, KVH, q_pos0,
-                           k_first, window, scale, ns, ws);
+                           k_first, window, scale, ns, ws, EncRows{}, ns == 1 && att_planes() ? xs : nullptr);
     }
     LAUNCH_CHECK();
     if (ns > 1) {
@@ -3202,7 +3233,7 @@ hipError_t launch_attn_rows_mf(int hd, const float* Q, int ldq, const float* Kc,
         else
             hipLaunchKernelGGL(k_attn_tiled_combine<128>, dim3(H, M), dim3(128), 0, st, ws, ns, M, O, ldo, xs);
         LAUNCH_CHECK();
-    } else if (xs) {
+    } else if (xs && (kv16 || !att_planes())) {
         return launch_split_fplanes(O, M, H * hd, xs, st);
     }
     return hipSuccess;

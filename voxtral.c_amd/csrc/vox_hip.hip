@@ -1840,9 +1840,9 @@ static int dec_layers_gemmf(vox_hip_stream_t* s, const GemmfQ& q, float* x, int 
         // RMSNorm -> planes, QKV (decoder.c:509-530)
         CK(launch_rmsnorm_fplanes(x, n, DD, L.attn_norm, nullptr, c.dec_eps, s->dpa, nullptr, 0, q.st));
         if (gemmf_on(q, EPI_STORE, s->dpa, DD, n, F.wqkv, DQ + 2 * DKV, nullptr, s->qkvd, DQ + 2 * DKV, nullptr)) return -1;
+        // RoPE + K/V append + attention, its rows as the wo planes in s->dpa (attn's job)
         if (attn(l)) return -1;
         // wo + residual (decoder.c:552-560)
-        CK(launch_split_fplanes(s->attd, n, DQ, s->dpa, q.st));
         if (gemmf_on(q, EPI_RESID, s->dpa, DQ, n, F.wo, DD, nullptr, x, DD, nullptr)) return -1;
         // RMSNorm * (1 + ada) -> planes, W1|W3 with SwiGLU into the w2 planes, w2 + residual (:562-606)
         CK(launch_rmsnorm_fplanes(x, n, DD, L.ffn_norm, m->ada_scale + (size_t)l * DD, c.dec_eps, s->dpa, nullptr, 0,
@@ -1881,7 +1881,7 @@ static int run_decoder_rows(vox_hip_stream_t* s, float* x, int n, int pos0, cons
             float* Vc = dec_ring(s, s->dv, l);
             CK(launch_rope_kv(s->qkvd, n, DQ, DKV, hd, rope, pos0, s->qd_, Kc, Vc, s->dcap, st, s->kv16));
             CK(launch_attn_rows_mf(hd, s->qd_, DQ, Kc, Vc, s->dcap, s->attd, DQ, n, H, KVH, pos0, 0, c.dec_window, scale,
-                                   st, s->gws, s->gws_n, nullptr, s->kv16));
+                                   st, s->gws, s->gws_n, s->dpa, s->kv16));
             return 0;
         });
     }
@@ -2933,7 +2933,8 @@ static int batch_prefill(vox_hip_batch_t* b, vox_hip_stream_t* const* ss, int B,
                     er.Vc[i] = dec_ring(ss[i], ss[i]->dv, l);
                 }
                 CK(launch_rope_kv_rows(lead->qkvd, N, DQ, DKV, hd, m->rope_dec, er, lead->qd_, cap, st));
-                CK(launch_attn_rows(hd, lead->qd_, er, N, cap, lead->attd, H, KVH, c.dec_window, scale, gws, gws_n, st));
+                CK(launch_attn_rows(hd, lead->qd_, er, N, cap, lead->attd, H, KVH, c.dec_window, scale, gws, gws_n, st,
+                                    lead->dpa));
                 return 0;
             }))
             return -1;
